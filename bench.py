@@ -1,0 +1,215 @@
+"""Throughput of the Mimi encode hot path on MI355X: audio-seconds encoded per wall-second (K = 8, 24 kHz).
+
+    python bench.py [--gpus N --steps K --warmup W --batch B --seconds S]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Workload (BASELINE.json configs[1]): one step = one ``mimi_encode`` of a batch of B = 32 synthetic 10 s /
+24 kHz clips (speech-like, seeded) already resident in HBM, K = 8 codebooks, weights = the seeded synthetic
+kyutai/mimi-shaped checkpoint (random init; throughput does not depend on values).  Multi-GPU: one process
+per GPU, each encodes its own batches (utterance round-robin, no data-path collective: SURVEY.md §8e);
+per-GPU work is fixed as N grows ("weak").  The timed region is bracketed by barrier + synchronize; the
+max over ranks is reported.  Rank 0 prints ONE JSON line.
+
+roofline: per-kernel device time from HIP events recorded by the engine on its launch stream during the
+timed steps, aggregated per kernel symbol; the dominant kernel's algorithmic FLOPs / its time vs the fp32
+MFMA peak.  cpu_baseline: the oracle (torch CPU restatement of MimiModel.encode) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "tokenize-audio_amd"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 MFMA/vector peak
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--num-quantizers", type=int, default=8)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0,
+                    help="wall budget of the CPU-baseline sample (0 disables)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-profile", action="store_true", help="do not record per-stage events")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds_budget: float, threads: int, clip_s: float):
+    """The oracle on the host cores: whole 10 s clips, batch 1 (config 1 of BASELINE.json), until the budget
+    is spent.  Returns the same metric (audio-s / wall-s)."""
+    import torch
+
+    from mimi_hip import synthetic
+    from oracle import mimi_ref
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    sd = synthetic.make_state_dict(seed=0, num_quantizers=8)
+    sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
+    n = int(clip_s * 24000)
+    clip = torch.from_numpy(synthetic.speech_like(n, 0, 0))[None, None]
+    mimi_ref.encode(clip, sdt, 8)  # warm
+    done, t0 = 0, time.perf_counter()
+    while True:
+        mimi_ref.encode(clip, sdt, 8)
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= seconds_budget or done >= 200:
+            break
+    try:
+        cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        cpu_model = "unknown"
+    return {"value": round(done * clip_s / el, 3), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
+            "sample": f"{done} x {clip_s:g} s clips, batch 1, K=8, oracle/mimi_ref.py (torch {torch.__version__} CPU, "
+                      f"{threads} threads, {cpu_model})"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from mimi_hip import synthetic
+    from mimi_hip.config import encoded_length
+    from mimi_hip.model import MimiHipModel
+
+    K = args.num_quantizers
+    B = args.batch
+    L = int(round(args.seconds * 24000))
+    model = MimiHipModel(synthetic.make_state_dict(seed=0, num_quantizers=K), device=dev)
+    # this rank's utterances: a distinct seeded slice of the shard (round-robin i -> rank i % N)
+    audio = torch.from_numpy(synthetic.clip_batch(B, L, seed=1000 + rank)).to(dev)
+    codes = torch.empty((B, K, encoded_length(L)), dtype=torch.int32, device=dev)
+
+    def step():
+        model.encode_int32(audio, K, out=codes)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        model.profile_reset()
+        model.set_profiling(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = {}
+    if not args.no_profile:
+        model.set_profiling(False)
+        prof = model.profile_read()
+
+    # PCIe-inclusive rate (host f32 in -> device codes -> host): reported beside, never as `value`
+    host_audio = audio.cpu().pin_memory()
+    torch.cuda.synchronize()
+    tp0 = time.perf_counter()
+    for _ in range(max(1, min(args.steps, 3))):
+        a = host_audio.to(dev, non_blocking=True)
+        c = model.encode_int32(a, K)
+        c.cpu()
+    torch.cuda.synchronize()
+    pcie_rate = max(1, min(args.steps, 3)) * B * args.seconds / (time.perf_counter() - tp0)
+
+    total_audio_s = world * B * args.seconds * args.steps
+    value = total_audio_s / elapsed
+    result = {
+        "metric": "audio-sec encoded/sec (Mimi 8-codebook, 24 kHz)",
+        "value": round(value, 2),
+        "unit": "audio-sec/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded speech-like 24 kHz clips; seeded random-init kyutai/mimi-shaped weights)",
+        "config": {"workload": f"LibriTTS-R-style batch encode: batch={B} x {args.seconds:g} s @ 24 kHz, "
+                               f"K={K} codebooks, 1 encode per step per GPU",
+                   "global_batch": world * B, "clip_seconds": args.seconds, "num_quantizers": K,
+                   "parallelism": f"utterance round-robin x{world} (no collective)"},
+        "pcie_inclusive_value": round(pcie_rate * world, 2),
+    }
+    if prof:
+        per_kernel = {}
+        for stage, st in prof.items():
+            k = per_kernel.setdefault(st["kernel"], {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "launches": 0,
+                                                      "stages": []})
+            k["ms"] += st["ms"]
+            k["flops"] += st["flops"]
+            k["bytes"] += st["bytes"]
+            k["launches"] += st["launches"]
+            k["stages"].append(stage)
+        dom_name, dom = max(per_kernel.items(), key=lambda kv: kv[1]["ms"])
+        t_launch = dom["ms"] / 1000.0 / dom["launches"]
+        gemm_like = dom["flops"] > 0
+        if gemm_like:
+            achieved = dom["flops"] / dom["launches"] / t_launch / 1e12
+            roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / FP32_PEAK_TFLOPS, 4)}
+        else:
+            achieved = dom["bytes"] / dom["launches"] / t_launch / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4)}
+        roof.update({"traffic": None, "kernel": dom_name, "stages": dom["stages"],
+                     "avg_launch_ms": round(1000 * t_launch, 4), "launches": dom["launches"],
+                     "algorithmic_per_launch": dom["flops"] / dom["launches"] if gemm_like
+                     else dom["bytes"] / dom["launches"]})
+        result["roofline"] = roof
+        tot_ms = sum(v["ms"] for v in per_kernel.values())
+        tot_fl = sum(v["flops"] for v in per_kernel.values())
+        result["whole_encode"] = {"device_ms_per_step": round(tot_ms / args.steps, 3),
+                                  "tflops": round(tot_fl / (tot_ms / 1000) / 1e12, 2),
+                                  "frac_fp32_peak": round(tot_fl / (tot_ms / 1000) / 1e12 / FP32_PEAK_TFLOPS, 4)}
+        result["stages_ms_per_step"] = {s: round(v["ms"] / args.steps, 3) for s, v in prof.items()}
+    if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.cpu_threads, args.seconds)
+    if rank == 0:
+        line = json.dumps(result)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

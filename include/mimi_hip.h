@@ -1,0 +1,143 @@
+/*
+ * mimi_hip.h — C ABI of the MI355X-native Mimi encode engine (libmimi_hip.so).
+ *
+ * Drop-in boundary.  The reference's encode path is Python over third-party
+ * ``transformers.MimiModel`` (no native FFI of its own); the entry points below are what a binding of that
+ * path binds, one for one:
+ *
+ *   mimi_create / mimi_load_safetensors / mimi_set_weight / mimi_finalize
+ *       replace ``MimiModel.from_pretrained(model_id).to(device).eval()``
+ *       (/root/reference/emilia-mimi/process_shard.py:57-60; TF/modeling_mimi.py:1186-1228)
+ *   mimi_encode
+ *       replaces ``MimiModel.encode(input_values, padding_mask, num_quantizers)``
+ *       (/root/reference/emilia-mimi/process_shard.py:82-85, :124-127; TF/modeling_mimi.py:1297-1386)
+ *   mimi_rvq_encode
+ *       replaces ``MimiSplitResidualVectorQuantizer.encode`` (TF/modeling_mimi.py:1099-1126) on a given
+ *       pre-quantizer embedding (used by the bit-exact quantizer parity test)
+ *   mimi_encoded_length
+ *       replaces ``MimiModel.get_encoded_length`` (TF/modeling_mimi.py:1265-1278)
+ *
+ * Conventions: plain pointers and sizes, no exceptions, no torch types.  Every function returns a
+ * mimi_status; on failure ``mimi_last_error()`` (thread-local) describes it.  Device pointers are HIP
+ * device memory on the engine's device; ``stream`` is a hipStream_t (NULL = the HIP null stream);
+ * work is enqueued asynchronously on it, ordered after earlier work on that stream.
+ * One engine may be shared by several host threads (calls are serialised by a per-engine mutex).
+ */
+#ifndef MIMI_HIP_H
+#define MIMI_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mimi_engine mimi_engine;
+
+typedef enum mimi_status {
+    MIMI_OK = 0,
+    MIMI_ERR_INVALID_ARGUMENT = 1, /* ValueError in the reference (e.g. K > 32, channels not in {1,2}) */
+    MIMI_ERR_HIP = 2,              /* a HIP runtime call failed */
+    MIMI_ERR_OUT_OF_MEMORY = 3,    /* workspace allocation failed (reference: torch OOM) */
+    MIMI_ERR_WEIGHTS = 4,          /* missing / mis-shaped parameter */
+    MIMI_ERR_UNSUPPORTED = 5,      /* config outside the implemented architecture family */
+    MIMI_ERR_IO = 6,               /* checkpoint file unreadable / malformed */
+    MIMI_ERR_STATE = 7             /* call order violated (e.g. encode before finalize) */
+} mimi_status;
+
+/* Encode-path fields of MimiConfig (TF/configuration_mimi.py:86-123). */
+typedef struct mimi_config {
+    int32_t sampling_rate;          /* 24000 */
+    int32_t audio_channels;         /* 1 */
+    int32_t hidden_size;            /* 512 */
+    int32_t num_filters;            /* 64 */
+    int32_t num_ratios;             /* 4 */
+    int32_t upsampling_ratios[8];   /* {8, 6, 5, 4}; the encoder uses them reversed */
+    int32_t kernel_size;            /* 7 */
+    int32_t last_kernel_size;       /* 3 */
+    int32_t residual_kernel_size;   /* 3 */
+    int32_t compress;               /* 2 */
+    int32_t codebook_size;          /* 2048 */
+    int32_t codebook_dim;           /* 256 */
+    int32_t num_quantizers;         /* 32 */
+    int32_t num_semantic_quantizers;/* 1 */
+    int32_t vq_hidden_dim;          /* 256 */
+    int32_t num_hidden_layers;      /* 8 */
+    int32_t intermediate_size;      /* 2048 */
+    int32_t num_attention_heads;    /* 8 */
+    int32_t head_dim;               /* 64 */
+    int32_t sliding_window;         /* 250 */
+    int32_t downsample_kernel;      /* 4 = 2 * encodec_frame_rate / frame_rate */
+    int32_t downsample_stride;      /* 2 */
+    float norm_eps;                 /* 1e-5 */
+    float rope_theta;               /* 10000 */
+    float codebook_eps;             /* 1e-5 (MimiEuclideanCodebook epsilon) */
+} mimi_config;
+
+/* Fill *cfg with the kyutai/mimi defaults. */
+void mimi_config_default(mimi_config* cfg);
+
+/* Create an engine on HIP device `device` (cfg NULL = defaults).  Weights are supplied next. */
+int mimi_create(const mimi_config* cfg, int device, mimi_engine** out);
+
+/* Supply one parameter by its HF name, fp32, host memory, copied. */
+int mimi_set_weight(mimi_engine* e, const char* name, const float* host_data, int64_t numel);
+
+/* Read every encode-path parameter from a safetensors file (F32 tensors, HF names). */
+int mimi_load_safetensors(mimi_engine* e, const char* path);
+
+/* Check all parameters are present, re-lay them out for the kernels and upload them. */
+int mimi_finalize(mimi_engine* e);
+
+/*
+ * Encode `batch` mono waveforms of `length` samples (device f32, [batch][length], already padded to a
+ * common length by the caller as EncodecFeatureExtractor does) into `num_quantizers` codebooks.
+ * dev_codes: device int32 [batch][num_quantizers][mimi_encoded_length(length)].
+ * num_quantizers <= 0 means config.num_quantizers (the reference default, TF/modeling_mimi.py:1335).
+ */
+int mimi_encode(mimi_engine* e, const float* dev_audio, int32_t batch, int64_t length,
+                int32_t num_quantizers, int32_t* dev_codes, void* stream);
+
+/*
+ * The quantizer alone: dev_embedding is the pre-quantizer embedding, device f32 [frames][hidden_size]
+ * (frame-major, i.e. the reference's [B, 512, T] transposed to [B*T, 512]).  dev_codes: int32
+ * [num_quantizers][frames].
+ */
+int mimi_rvq_encode(mimi_engine* e, const float* dev_embedding, int64_t frames, int32_t num_quantizers,
+                    int32_t* dev_codes, void* stream);
+
+/* Frames produced for `length` samples with the default config (reference float32 length math). */
+int64_t mimi_encoded_length(int64_t length);
+int64_t mimi_encoded_length_cfg(const mimi_config* cfg, int64_t length);
+
+/* Device bytes the workspace needs for (batch, length); the engine grows it on demand. */
+int64_t mimi_workspace_bytes(const mimi_engine* e, int32_t batch, int64_t length);
+
+/* Release everything. */
+void mimi_destroy(mimi_engine* e);
+
+/* Thread-local description of the last failure in this thread. */
+const char* mimi_last_error(void);
+
+/* ---- instrumentation (bench / tests) ---- */
+
+/* When enabled, mimi_encode records a HIP event pair around every stage on the stream it runs on. */
+int mimi_set_profiling(mimi_engine* e, int enable);
+/* Per-stage totals accumulated over all profiled encodes since the last reset: names (128 chars
+ * each, "stage|kernel symbol"), device ms (event pairs on the launch stream), launch counts, and algorithmic work as
+ * (flops, bytes) pairs in flops_bytes[2*i], flops_bytes[2*i+1].  Synchronises the recorded events. */
+int mimi_profile_read(mimi_engine* e, int32_t max_stages, char* names /* max_stages*128 */,
+                      double* total_ms, int64_t* launches, double* flops_bytes, int32_t* n_stages);
+int mimi_profile_reset(mimi_engine* e);
+
+/* When enabled, mimi_encode keeps a copy of each stage's output (for per-stage parity tests). */
+int mimi_set_taps(mimi_engine* e, int enable);
+/* Copy tap `name` to host: dst holds cap floats; *numel receives the element count; dims[0..2] the
+ * [batch][time][channels] shape.  Synchronises. */
+int mimi_get_tap(mimi_engine* e, const char* name, float* host_dst, int64_t cap, int64_t* numel,
+                 int64_t dims[3]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIMI_HIP_H */

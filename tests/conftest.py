@@ -1,0 +1,34 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "tokenize-audio_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+
+    import numpy as np
+    with np.load(os.path.join(GOLDEN, "golden.npz"), allow_pickle=False) as z:
+        arrays = {k: z[k] for k in z.files}
+    with open(os.path.join(GOLDEN, "golden_meta.json")) as f:
+        meta = json.load(f)
+    return arrays, meta
+
+
+@pytest.fixture(scope="session")
+def state_dict():
+    from mimi_hip import synthetic
+    return synthetic.make_state_dict(seed=0)

@@ -1,0 +1,1157 @@
+// Mimi encode engine: weights, workspace, stage sequencing and the C ABI of include/mimi_hip.h.
+//
+// Data layout in HBM (all fp32, channels-last so that every conv is a plain GEMM, see gemm.hip):
+//   audio            [B][L]
+//   SEANet stage s   x_s [B][T_s][C_s]  (C_s = 64 << s, T_0 = L, T_{s+1} = ceil(T_s / ratio_s))
+//   transformer      [B][T][512]  (T = T_4 frames at 25 Hz), fused qkv [B][T][1536], mlp [B][T][2048]
+//   quantizer input  [B*T'][512]  (T' = ceil(T/2) frames at 12.5 Hz), projections [B*T'][512]
+//   codes            int32 [B][K][T']
+// Weights are re-laid out once at finalize: conv W[co][ci][k] -> W'[co][k*Cin + ci]; q/k/v fused into
+// one [1536][512]; the two input_proj stacked into one [512][512]; codebooks materialised as
+// embed = embed_sum / clamp(cluster_usage, eps) (TF/modeling_mimi.py:979-983) in row layout (for the
+// residual update) and in MFMA-fragment layout (for the distance GEMM), with |e|^2 in torch's order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mimi_hip.h"
+#include "kernels.h"
+
+using namespace mimi;
+
+// ------------------------------------------------------------------------------------------------
+// errors
+// ------------------------------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+
+static int set_err(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                \
+    do {                                                                                             \
+        hipError_t _e = (expr);                                                                      \
+        if (_e != hipSuccess) {                                                                      \
+            return set_err(_e == hipErrorOutOfMemory ? MIMI_ERR_OUT_OF_MEMORY : MIMI_ERR_HIP,        \
+                           "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+        }                                                                                            \
+    } while (0)
+
+extern "C" const char* mimi_last_error(void) { return g_last_error.c_str(); }
+
+// ------------------------------------------------------------------------------------------------
+// config / length math
+// ------------------------------------------------------------------------------------------------
+extern "C" void mimi_config_default(mimi_config* c) {
+    std::memset(c, 0, sizeof(*c));
+    c->sampling_rate = 24000;
+    c->audio_channels = 1;
+    c->hidden_size = 512;
+    c->num_filters = 64;
+    c->num_ratios = 4;
+    c->upsampling_ratios[0] = 8;
+    c->upsampling_ratios[1] = 6;
+    c->upsampling_ratios[2] = 5;
+    c->upsampling_ratios[3] = 4;
+    c->kernel_size = 7;
+    c->last_kernel_size = 3;
+    c->residual_kernel_size = 3;
+    c->compress = 2;
+    c->codebook_size = 2048;
+    c->codebook_dim = 256;
+    c->num_quantizers = 32;
+    c->num_semantic_quantizers = 1;
+    c->vq_hidden_dim = 256;
+    c->num_hidden_layers = 8;
+    c->intermediate_size = 2048;
+    c->num_attention_heads = 8;
+    c->head_dim = 64;
+    c->sliding_window = 250;
+    c->downsample_kernel = 4;
+    c->downsample_stride = 2;
+    c->norm_eps = 1e-5f;
+    c->rope_theta = 10000.0f;
+    c->codebook_eps = 1e-5f;
+}
+
+// MimiConv1d output length, reproducing the reference's float32 tensor arithmetic
+// (TF/modeling_mimi.py:269-279): n_frames = ceil(float32(L - s) / float32(s) + 1) - 1; out = n_frames + 1.
+static int64_t conv_out_len(int64_t length, int kernel, int stride) {
+    const int64_t pt = kernel - stride;
+    volatile float num = (float)(length - kernel + pt);
+    volatile float q = num / (float)stride;
+    volatile float nf = q + 1.0f;
+    const int64_t n_frames = (int64_t)std::ceil((float)nf) - 1;
+    return n_frames + 1;
+}
+
+struct StagePlan {
+    int64_t T[5];  // T[0] = conv0 out; T[s+1] = down conv s out
+    int64_t frames25, frames12;
+};
+
+static StagePlan plan_lengths(const mimi_config& c, int64_t L) {
+    StagePlan p{};
+    int64_t t = conv_out_len(L, c.kernel_size, 1);
+    p.T[0] = t;
+    for (int s = 0; s < c.num_ratios; ++s) {
+        const int ratio = c.upsampling_ratios[c.num_ratios - 1 - s];
+        t = conv_out_len(t, c.residual_kernel_size, 1);
+        t = conv_out_len(t, 1, 1);
+        t = conv_out_len(t, 2 * ratio, ratio);
+        p.T[s + 1] = t;
+    }
+    t = conv_out_len(t, c.last_kernel_size, 1);
+    p.frames25 = t;
+    p.frames12 = conv_out_len(t, c.downsample_kernel, c.downsample_stride);
+    return p;
+}
+
+extern "C" int64_t mimi_encoded_length_cfg(const mimi_config* cfg, int64_t length) {
+    mimi_config d;
+    if (!cfg) {
+        mimi_config_default(&d);
+        cfg = &d;
+    }
+    if (length < 0) return -1;
+    return plan_lengths(*cfg, length).frames12;
+}
+
+extern "C" int64_t mimi_encoded_length(int64_t length) { return mimi_encoded_length_cfg(nullptr, length); }
+
+// ------------------------------------------------------------------------------------------------
+// engine
+// ------------------------------------------------------------------------------------------------
+struct DevConv {
+    int cin = 0, cout = 0, k = 0, stride = 1;
+    float* w = nullptr;  // [cout][k*cin]
+    float* b = nullptr;  // [cout] or null
+};
+
+struct DevXfmr {
+    float *ln1_w, *ln1_b, *wqkv, *wo, *ls1, *ln2_w, *ln2_b, *w1, *w2, *ls2;
+};
+
+struct ProfEvent {
+    std::string name;  // "stage|kernel symbol"
+
+    hipEvent_t ev;
+    double flops;
+    double bytes;
+};
+
+struct ProfStat {
+    double ms = 0, flops = 0, bytes = 0;
+    int64_t launches = 0;
+};
+
+struct mimi_engine {
+    mimi_config cfg;
+    int device = 0;
+    std::mutex mu;
+    bool finalized = false;
+    int levels_available = 0;
+
+    std::unordered_map<std::string, std::vector<float>> host_w;
+    std::unordered_map<std::string, std::vector<int64_t>> expected;  // name -> shape
+    std::vector<void*> allocations;
+
+    DevConv conv0;
+    std::vector<DevConv> res3, res1, down;
+    DevConv final_conv;
+    std::vector<DevXfmr> xf;
+    DevConv ds;
+    float* inproj = nullptr;  // [2*vq][hidden]
+    float* cb_rows = nullptr;
+    float* cb_frag = nullptr;
+    float* cb_norm = nullptr;
+
+    float* rope_cos = nullptr;
+    float* rope_sin = nullptr;
+    int64_t rope_T = 0;
+
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+
+    hipEvent_t ws_free = nullptr;  // recorded at the end of every encode: the next one (any stream) waits on it
+    bool profiling = false;
+    std::vector<ProfEvent> pending;  // recorded since last read; first event of each encode named ""
+    std::vector<hipEvent_t> event_pool;
+    std::map<std::string, ProfStat> prof;
+    std::vector<std::string> prof_order;
+
+    bool taps = false;
+    struct Tap {
+        float* d = nullptr;
+        size_t cap = 0;
+        int64_t dims[3] = {0, 0, 0};
+    };
+    std::map<std::string, Tap> tapmap;
+};
+
+static int dev_alloc(mimi_engine* e, void** p, size_t bytes) {
+    hipError_t err = hipMalloc(p, bytes);
+    if (err != hipSuccess)
+        return set_err(err == hipErrorOutOfMemory ? MIMI_ERR_OUT_OF_MEMORY : MIMI_ERR_HIP, "hipMalloc(%zu): %s",
+                       bytes, hipGetErrorString(err));
+    e->allocations.push_back(*p);
+    return MIMI_OK;
+}
+
+static int upload(mimi_engine* e, float** dst, const std::vector<float>& host) {
+    int rc = dev_alloc(e, reinterpret_cast<void**>(dst), host.size() * sizeof(float));
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(*dst, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+    return MIMI_OK;
+}
+
+static std::string conv_name_first() { return "encoder.layers.0.conv"; }
+
+static void build_expected(mimi_engine* e) {
+    const mimi_config& c = e->cfg;
+    auto& ex = e->expected;
+    ex.clear();
+    ex[conv_name_first() + ".weight"] = {c.num_filters, c.audio_channels, c.kernel_size};
+    ex[conv_name_first() + ".bias"] = {c.num_filters};
+    int idx = 1;
+    int C = c.num_filters;
+    for (int s = 0; s < c.num_ratios; ++s) {
+        const int ratio = c.upsampling_ratios[c.num_ratios - 1 - s];
+        const std::string p = "encoder.layers." + std::to_string(idx) + ".block.";
+        ex[p + "1.conv.weight"] = {C / c.compress, C, c.residual_kernel_size};
+        ex[p + "1.conv.bias"] = {C / c.compress};
+        ex[p + "3.conv.weight"] = {C, C / c.compress, 1};
+        ex[p + "3.conv.bias"] = {C};
+        idx += 2;
+        const std::string d = "encoder.layers." + std::to_string(idx) + ".conv.";
+        ex[d + "weight"] = {2 * C, C, 2 * ratio};
+        ex[d + "bias"] = {2 * C};
+        idx += 1;
+        C *= 2;
+    }
+    idx += 1;
+    const std::string f = "encoder.layers." + std::to_string(idx) + ".conv.";
+    ex[f + "weight"] = {c.hidden_size, C, c.last_kernel_size};
+    ex[f + "bias"] = {c.hidden_size};
+    const int h = c.hidden_size;
+    for (int l = 0; l < c.num_hidden_layers; ++l) {
+        const std::string p = "encoder_transformer.layers." + std::to_string(l) + ".";
+        for (const char* n : {"q_proj", "k_proj", "v_proj"})
+            ex[p + "self_attn." + n + ".weight"] = {c.num_attention_heads * c.head_dim, h};
+        ex[p + "self_attn.o_proj.weight"] = {h, c.num_attention_heads * c.head_dim};
+        ex[p + "mlp.fc1.weight"] = {c.intermediate_size, h};
+        ex[p + "mlp.fc2.weight"] = {h, c.intermediate_size};
+        for (const char* n : {"input_layernorm", "post_attention_layernorm"}) {
+            ex[p + n + ".weight"] = {h};
+            ex[p + n + ".bias"] = {h};
+        }
+        ex[p + "self_attn_layer_scale.scale"] = {h};
+        ex[p + "mlp_layer_scale.scale"] = {h};
+    }
+    ex["downsample.conv.weight"] = {h, h, c.downsample_kernel};
+    for (const char* q : {"semantic", "acoustic"})
+        ex[std::string("quantizer.") + q + "_residual_vector_quantizer.input_proj.weight"] = {c.vq_hidden_dim, h, 1};
+}
+
+static std::string codebook_prefix(const mimi_config& c, int level) {
+    if (level < c.num_semantic_quantizers)
+        return "quantizer.semantic_residual_vector_quantizer.layers." + std::to_string(level) + ".codebook.";
+    return "quantizer.acoustic_residual_vector_quantizer.layers." + std::to_string(level - c.num_semantic_quantizers) +
+           ".codebook.";
+}
+
+static int check_supported(const mimi_config& c) {
+    if (c.audio_channels != 1) return set_err(MIMI_ERR_UNSUPPORTED, "audio_channels must be 1");
+    if (c.num_filters != 64 || c.kernel_size != 7)
+        return set_err(MIMI_ERR_UNSUPPORTED, "first conv must be 1->64, k=7");
+    if (c.hidden_size != 512 || c.head_dim != 64 || c.num_attention_heads * c.head_dim != c.hidden_size)
+        return set_err(MIMI_ERR_UNSUPPORTED, "transformer must be 512 wide with 64-dim heads");
+    if (c.codebook_dim != 256 || c.vq_hidden_dim != 256 || c.codebook_size % 256 != 0)
+        return set_err(MIMI_ERR_UNSUPPORTED, "codebooks must be [n*256][256]");
+    if (c.num_ratios < 1 || c.num_ratios > 8) return set_err(MIMI_ERR_UNSUPPORTED, "num_ratios out of range");
+    if (c.residual_kernel_size * c.num_filters / c.compress % 32 != 0 && c.compress != 2)
+        return set_err(MIMI_ERR_UNSUPPORTED, "compress must be 2");
+    if (c.num_semantic_quantizers < 1 || c.num_semantic_quantizers >= c.num_quantizers)
+        return set_err(MIMI_ERR_UNSUPPORTED, "num_semantic_quantizers out of range");
+    return MIMI_OK;
+}
+
+extern "C" int mimi_create(const mimi_config* cfg, int device, mimi_engine** out) {
+    if (!out) return set_err(MIMI_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    std::unique_ptr<mimi_engine> e(new mimi_engine());
+    if (cfg)
+        e->cfg = *cfg;
+    else
+        mimi_config_default(&e->cfg);
+    int rc = check_supported(e->cfg);
+    if (rc) return rc;
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return set_err(MIMI_ERR_INVALID_ARGUMENT, "device %d of %d", device, ndev);
+    e->device = device;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipEventCreateWithFlags(&e->ws_free, hipEventDisableTiming));
+    build_expected(e.get());
+    *out = e.release();
+    return MIMI_OK;
+}
+
+extern "C" int mimi_set_weight(mimi_engine* e, const char* name, const float* data, int64_t numel) {
+    if (!e || !name || (!data && numel > 0)) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null argument");
+    if (e->finalized) return set_err(MIMI_ERR_STATE, "weights are frozen after mimi_finalize");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->host_w[name].assign(data, data + numel);
+    return MIMI_OK;
+}
+
+// --- minimal safetensors reader (8-byte LE header length, JSON header, raw little-endian data) ---
+namespace {
+struct StEntry {
+    std::string dtype;
+    std::vector<int64_t> shape;
+    int64_t begin = 0, end = 0;
+};
+
+struct JsonCursor {
+    const std::string& s;
+    size_t i = 0;
+    explicit JsonCursor(const std::string& str) : s(str) {}
+    void ws() {
+        while (i < s.size() && (s[i] == ' ' || s[i] == '\n' || s[i] == '\t' || s[i] == '\r')) ++i;
+    }
+    bool eat(char c) {
+        ws();
+        if (i < s.size() && s[i] == c) {
+            ++i;
+            return true;
+        }
+        return false;
+    }
+    bool str(std::string& out) {
+        ws();
+        if (i >= s.size() || s[i] != '"') return false;
+        ++i;
+        out.clear();
+        while (i < s.size() && s[i] != '"') {
+            if (s[i] == '\\' && i + 1 < s.size()) ++i;
+            out.push_back(s[i++]);
+        }
+        if (i >= s.size()) return false;
+        ++i;
+        return true;
+    }
+    bool num(int64_t& v) {
+        ws();
+        size_t j = i;
+        if (j < s.size() && s[j] == '-') ++j;
+        while (j < s.size() && isdigit((unsigned char)s[j])) ++j;
+        if (j == i) return false;
+        v = std::stoll(s.substr(i, j - i));
+        i = j;
+        return true;
+    }
+    bool skip_value() {  // skip any JSON value (used for __metadata__)
+        ws();
+        if (i >= s.size()) return false;
+        if (s[i] == '"') {
+            std::string t;
+            return str(t);
+        }
+        if (s[i] == '{' || s[i] == '[') {
+            const char open = s[i], close = open == '{' ? '}' : ']';
+            int depth = 0;
+            bool in_str = false;
+            for (; i < s.size(); ++i) {
+                const char ch = s[i];
+                if (in_str) {
+                    if (ch == '\\') ++i;
+                    else if (ch == '"') in_str = false;
+                    continue;
+                }
+                if (ch == '"') in_str = true;
+                else if (ch == open) ++depth;
+                else if (ch == close && --depth == 0) {
+                    ++i;
+                    return true;
+                }
+            }
+            return false;
+        }
+        while (i < s.size() && s[i] != ',' && s[i] != '}' && s[i] != ']') ++i;
+        return true;
+    }
+    bool int_list(std::vector<int64_t>& v) {
+        v.clear();
+        if (!eat('[')) return false;
+        if (eat(']')) return true;
+        do {
+            int64_t x;
+            if (!num(x)) return false;
+            v.push_back(x);
+        } while (eat(','));
+        return eat(']');
+    }
+};
+
+bool parse_header(const std::string& hdr, std::map<std::string, StEntry>& out, std::string& err) {
+    JsonCursor c(hdr);
+    if (!c.eat('{')) return err = "header is not an object", false;
+    if (c.eat('}')) return true;
+    do {
+        std::string key;
+        if (!c.str(key) || !c.eat(':')) return err = "bad key", false;
+        if (key == "__metadata__") {
+            if (!c.skip_value()) return err = "bad metadata", false;
+            continue;
+        }
+        StEntry en;
+        if (!c.eat('{')) return err = "entry " + key + " is not an object", false;
+        if (!c.eat('}')) {
+            do {
+                std::string f;
+                if (!c.str(f) || !c.eat(':')) return err = "bad field in " + key, false;
+                if (f == "dtype") {
+                    if (!c.str(en.dtype)) return err = "bad dtype in " + key, false;
+                } else if (f == "shape") {
+                    if (!c.int_list(en.shape)) return err = "bad shape in " + key, false;
+                } else if (f == "data_offsets") {
+                    std::vector<int64_t> o;
+                    if (!c.int_list(o) || o.size() != 2) return err = "bad offsets in " + key, false;
+                    en.begin = o[0];
+                    en.end = o[1];
+                } else if (!c.skip_value()) {
+                    return err = "bad value in " + key, false;
+                }
+            } while (c.eat(','));
+            if (!c.eat('}')) return err = "unterminated entry " + key, false;
+        }
+        out[key] = en;
+    } while (c.eat(','));
+    return c.eat('}') ? true : (err = "unterminated header", false);
+}
+}  // namespace
+
+extern "C" int mimi_load_safetensors(mimi_engine* e, const char* path) {
+    if (!e || !path) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null argument");
+    if (e->finalized) return set_err(MIMI_ERR_STATE, "weights are frozen after mimi_finalize");
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return set_err(MIMI_ERR_IO, "cannot open %s", path);
+    uint64_t hlen = 0;
+    f.read(reinterpret_cast<char*>(&hlen), 8);
+    if (!f || hlen == 0 || hlen > (1ull << 30)) return set_err(MIMI_ERR_IO, "%s: bad safetensors header", path);
+    std::string hdr(hlen, '\0');
+    f.read(&hdr[0], (std::streamsize)hlen);
+    if (!f) return set_err(MIMI_ERR_IO, "%s: truncated header", path);
+    std::map<std::string, StEntry> entries;
+    std::string perr;
+    if (!parse_header(hdr, entries, perr)) return set_err(MIMI_ERR_IO, "%s: %s", path, perr.c_str());
+    const int64_t data0 = 8 + (int64_t)hlen;
+    std::lock_guard<std::mutex> lk(e->mu);
+    for (const auto& kv : entries) {
+        const std::string& name = kv.first;
+        const StEntry& en = kv.second;
+        const bool wanted = e->expected.count(name) || name.rfind("quantizer.", 0) == 0 ||
+                            name.find("weight_g") != std::string::npos || name.find("original0") != std::string::npos;
+        if (!wanted || name.rfind("decoder", 0) == 0) continue;
+        if (en.dtype != "F32") return set_err(MIMI_ERR_WEIGHTS, "%s: dtype %s (F32 required)", name.c_str(), en.dtype.c_str());
+        int64_t numel = 1;
+        for (int64_t d : en.shape) numel *= d;
+        if (en.end - en.begin != numel * 4) return set_err(MIMI_ERR_IO, "%s: size mismatch", name.c_str());
+        std::vector<float> buf(numel);
+        f.seekg(data0 + en.begin);
+        f.read(reinterpret_cast<char*>(buf.data()), numel * 4);
+        if (!f) return set_err(MIMI_ERR_IO, "%s: truncated data for %s", path, name.c_str());
+        e->host_w[name] = std::move(buf);
+    }
+    return MIMI_OK;
+}
+
+// weight-norm checkpoints store weight_g [cout,1,1] and weight_v [cout,cin,k]: w = g * v / ||v|| per cout
+static bool resolve_weight_norm(mimi_engine* e, const std::string& wname, const std::vector<int64_t>& shape) {
+    const std::string base = wname.substr(0, wname.size() - std::string("weight").size());
+    const std::string gk[] = {base + "weight_g", base + "parametrizations.weight.original0"};
+    const std::string vk[] = {base + "weight_v", base + "parametrizations.weight.original1"};
+    for (int i = 0; i < 2; ++i) {
+        auto g = e->host_w.find(gk[i]);
+        auto v = e->host_w.find(vk[i]);
+        if (g == e->host_w.end() || v == e->host_w.end()) continue;
+        const int64_t cout = shape[0];
+        const int64_t per = (int64_t)v->second.size() / cout;
+        std::vector<float> w(v->second.size());
+        for (int64_t o = 0; o < cout; ++o) {
+            double n2 = 0;
+            for (int64_t j = 0; j < per; ++j) n2 += (double)v->second[o * per + j] * v->second[o * per + j];
+            const float s = (float)(g->second[o] / std::sqrt(n2));
+            for (int64_t j = 0; j < per; ++j) w[o * per + j] = v->second[o * per + j] * s;
+        }
+        e->host_w[wname] = std::move(w);
+        return true;
+    }
+    return false;
+}
+
+static int get_w(mimi_engine* e, const std::string& name, std::vector<float>** out) {
+    auto it = e->host_w.find(name);
+    auto ex = e->expected.find(name);
+    if (it == e->host_w.end() && ex != e->expected.end() && resolve_weight_norm(e, name, ex->second))
+        it = e->host_w.find(name);
+    if (it == e->host_w.end()) return set_err(MIMI_ERR_WEIGHTS, "missing parameter %s", name.c_str());
+    if (ex != e->expected.end()) {
+        int64_t n = 1;
+        for (int64_t d : ex->second) n *= d;
+        if ((int64_t)it->second.size() != n)
+            return set_err(MIMI_ERR_WEIGHTS, "parameter %s has %zu elements, expected %lld", name.c_str(),
+                           it->second.size(), (long long)n);
+    }
+    *out = &it->second;
+    return MIMI_OK;
+}
+
+// W[co][ci][k] -> W'[co][k*cin + ci]
+static std::vector<float> relayout_conv(const std::vector<float>& w, int cout, int cin, int k) {
+    std::vector<float> o((size_t)cout * cin * k);
+    for (int co = 0; co < cout; ++co)
+        for (int ci = 0; ci < cin; ++ci)
+            for (int kk = 0; kk < k; ++kk) o[((size_t)co * k + kk) * cin + ci] = w[((size_t)co * cin + ci) * k + kk];
+    return o;
+}
+
+static int make_conv(mimi_engine* e, DevConv& dc, const std::string& prefix, int cin, int cout, int k, int stride,
+                     bool bias) {
+    std::vector<float>* w;
+    int rc = get_w(e, prefix + "weight", &w);
+    if (rc) return rc;
+    if ((int64_t)w->size() != (int64_t)cin * cout * k)
+        return set_err(MIMI_ERR_WEIGHTS, "%sweight: bad size", prefix.c_str());
+    dc.cin = cin;
+    dc.cout = cout;
+    dc.k = k;
+    dc.stride = stride;
+    rc = upload(e, &dc.w, cin == 1 ? *w : relayout_conv(*w, cout, cin, k));
+    if (rc) return rc;
+    if (bias) {
+        std::vector<float>* b;
+        rc = get_w(e, prefix + "bias", &b);
+        if (rc) return rc;
+        rc = upload(e, &dc.b, *b);
+        if (rc) return rc;
+    }
+    return MIMI_OK;
+}
+
+// sum of squares in torch's x.pow(2).sum(-1) order for rows of 8*m floats (see ops.hip)
+static float torch_sqsum_host(const float* r, int D) {
+    float lanes[8];
+    for (int l = 0; l < 8; ++l) {
+        float a[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int blk = 0; blk < D / 8; ++blk) {
+            volatile float sq = r[blk * 8 + l] * r[blk * 8 + l];
+            a[blk & 3] = a[blk & 3] + sq;
+        }
+        volatile float t = a[0] + a[1];
+        t = t + a[2];
+        t = t + a[3];
+        lanes[l] = t;
+    }
+    volatile float tot = lanes[0];
+    for (int l = 1; l < 8; ++l) tot = tot + lanes[l];
+    return tot;
+}
+
+extern "C" int mimi_finalize(mimi_engine* e) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (e->finalized) return MIMI_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    const mimi_config& c = e->cfg;
+    int rc = make_conv(e, e->conv0, "encoder.layers.0.conv.", 1, c.num_filters, c.kernel_size, 1, true);
+    if (rc) return rc;
+    int idx = 1, C = c.num_filters;
+    e->res3.resize(c.num_ratios);
+    e->res1.resize(c.num_ratios);
+    e->down.resize(c.num_ratios);
+    for (int s = 0; s < c.num_ratios; ++s) {
+        const int ratio = c.upsampling_ratios[c.num_ratios - 1 - s];
+        const std::string p = "encoder.layers." + std::to_string(idx) + ".block.";
+        if ((rc = make_conv(e, e->res3[s], p + "1.conv.", C, C / c.compress, c.residual_kernel_size, 1, true))) return rc;
+        if ((rc = make_conv(e, e->res1[s], p + "3.conv.", C / c.compress, C, 1, 1, true))) return rc;
+        idx += 2;
+        if ((rc = make_conv(e, e->down[s], "encoder.layers." + std::to_string(idx) + ".conv.", C, 2 * C, 2 * ratio,
+                            ratio, true)))
+            return rc;
+        idx += 1;
+        C *= 2;
+    }
+    idx += 1;
+    if ((rc = make_conv(e, e->final_conv, "encoder.layers." + std::to_string(idx) + ".conv.", C, c.hidden_size,
+                        c.last_kernel_size, 1, true)))
+        return rc;
+    const int h = c.hidden_size;
+    e->xf.resize(c.num_hidden_layers);
+    for (int l = 0; l < c.num_hidden_layers; ++l) {
+        const std::string p = "encoder_transformer.layers." + std::to_string(l) + ".";
+        DevXfmr& x = e->xf[l];
+        std::vector<float>*q, *k, *v, *t;
+        if ((rc = get_w(e, p + "self_attn.q_proj.weight", &q)) || (rc = get_w(e, p + "self_attn.k_proj.weight", &k)) ||
+            (rc = get_w(e, p + "self_attn.v_proj.weight", &v)))
+            return rc;
+        std::vector<float> qkv;
+        qkv.reserve(q->size() * 3);
+        qkv.insert(qkv.end(), q->begin(), q->end());
+        qkv.insert(qkv.end(), k->begin(), k->end());
+        qkv.insert(qkv.end(), v->begin(), v->end());
+        if ((rc = upload(e, &x.wqkv, qkv))) return rc;
+        struct {
+            const char* n;
+            float** d;
+        } simple[] = {{"self_attn.o_proj.weight", &x.wo},
+                      {"mlp.fc1.weight", &x.w1},
+                      {"mlp.fc2.weight", &x.w2},
+                      {"input_layernorm.weight", &x.ln1_w},
+                      {"input_layernorm.bias", &x.ln1_b},
+                      {"post_attention_layernorm.weight", &x.ln2_w},
+                      {"post_attention_layernorm.bias", &x.ln2_b},
+                      {"self_attn_layer_scale.scale", &x.ls1},
+                      {"mlp_layer_scale.scale", &x.ls2}};
+        for (auto& sp : simple) {
+            if ((rc = get_w(e, p + sp.n, &t))) return rc;
+            if ((rc = upload(e, sp.d, *t))) return rc;
+        }
+    }
+    if ((rc = make_conv(e, e->ds, "downsample.conv.", h, h, c.downsample_kernel, c.downsample_stride, false))) return rc;
+    {
+        std::vector<float>*ps, *pa;
+        if ((rc = get_w(e, "quantizer.semantic_residual_vector_quantizer.input_proj.weight", &ps)) ||
+            (rc = get_w(e, "quantizer.acoustic_residual_vector_quantizer.input_proj.weight", &pa)))
+            return rc;
+        std::vector<float> both(*ps);
+        both.insert(both.end(), pa->begin(), pa->end());
+        if ((rc = upload(e, &e->inproj, both))) return rc;
+    }
+    // codebooks: as many consecutive levels as the checkpoint provides (32 for kyutai/mimi)
+    const int n = c.codebook_size, D = c.codebook_dim;
+    int L = 0;
+    while (L < c.num_quantizers && e->host_w.count(codebook_prefix(c, L) + "embed_sum")) ++L;
+    if (L <= c.num_semantic_quantizers) return set_err(MIMI_ERR_WEIGHTS, "no acoustic codebooks found");
+    std::vector<float> rows((size_t)L * n * D), frag((size_t)L * n * D), norms((size_t)L * n);
+    for (int lv = 0; lv < L; ++lv) {
+        std::vector<float>*es, *us;
+        const std::string p = codebook_prefix(c, lv);
+        if ((rc = get_w(e, p + "embed_sum", &es)) || (rc = get_w(e, p + "cluster_usage", &us))) return rc;
+        if ((int64_t)es->size() != (int64_t)n * D || (int64_t)us->size() != n)
+            return set_err(MIMI_ERR_WEIGHTS, "%s: bad codebook shape", p.c_str());
+        float* R = rows.data() + (size_t)lv * n * D;
+        for (int j = 0; j < n; ++j) {
+            const float u = std::max((*us)[j], c.codebook_eps);
+            for (int d = 0; d < D; ++d) {
+                volatile float q = (*es)[(size_t)j * D + d] / u;
+                R[(size_t)j * D + d] = q;
+            }
+            norms[(size_t)lv * n + j] = torch_sqsum_host(R + (size_t)j * D, D);
+        }
+        // fragment layout: [jt][u][lane][s] = embed[32*jt + (lane&31)][8u + 2s + (lane>>5)]
+        float* F = frag.data() + (size_t)lv * n * D;
+        for (int jt = 0; jt < n / 32; ++jt)
+            for (int u = 0; u < D / 8; ++u)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int s = 0; s < 4; ++s)
+                        F[(((size_t)jt * (D / 8) + u) * 64 + lane) * 4 + s] =
+                            R[(size_t)(32 * jt + (lane & 31)) * D + 8 * u + 2 * s + (lane >> 5)];
+    }
+    if ((rc = upload(e, &e->cb_rows, rows)) || (rc = upload(e, &e->cb_frag, frag)) || (rc = upload(e, &e->cb_norm, norms)))
+        return rc;
+    e->levels_available = L;
+    e->host_w.clear();
+    e->finalized = true;
+    return MIMI_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// encode
+// ------------------------------------------------------------------------------------------------
+struct Workspace {
+    float *x, *h, *y;              // SEANet ping-pong
+    float *t0, *t1, *qkv, *att, *ff;  // transformer
+    float *dsout, *proj;
+};
+
+static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspace* w) {
+    const mimi_config& c = e->cfg;
+    size_t xmax = 0, hmax = 0;
+    int C = c.num_filters;
+    for (int s = 0; s < c.num_ratios; ++s) {
+        xmax = std::max(xmax, (size_t)p.T[s] * C);
+        hmax = std::max(hmax, (size_t)p.T[s] * (C / c.compress));
+        C *= 2;
+    }
+    xmax = std::max(xmax, (size_t)p.T[c.num_ratios] * C);
+    const size_t T = (size_t)p.frames25, Hd = (size_t)c.hidden_size;
+    const size_t sizes[] = {xmax * B,
+                            hmax * B,
+                            xmax * B,
+                            T * Hd * B,
+                            T * Hd * B,
+                            T * 3 * Hd * B,
+                            T * Hd * B,
+                            T * (size_t)c.intermediate_size * B,
+                            (size_t)p.frames12 * Hd * B,
+                            (size_t)p.frames12 * 2 * c.vq_hidden_dim * B};
+    size_t off = 0;
+    float** ptrs[] = {&w->x, &w->h, &w->y, &w->t0, &w->t1, &w->qkv, &w->att, &w->ff, &w->dsout, &w->proj};
+    char* base = reinterpret_cast<char*>(e->ws);
+    for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); ++i) {
+        if (w) *ptrs[i] = reinterpret_cast<float*>(base + off);
+        off += ((sizes[i] * sizeof(float) + 255) / 256) * 256;
+    }
+    return off;
+}
+
+extern "C" int64_t mimi_workspace_bytes(const mimi_engine* e, int32_t batch, int64_t length) {
+    if (!e || batch <= 0 || length <= 0) return -1;
+    return (int64_t)ws_layout(e, batch, plan_lengths(e->cfg, length), nullptr);
+}
+
+static int ensure_ws(mimi_engine* e, size_t bytes, hipStream_t s) {
+    if (bytes <= e->ws_bytes) return MIMI_OK;
+    HIP_TRY(hipStreamSynchronize(s));
+    if (e->ws) {
+        HIP_TRY(hipFree(e->ws));
+        e->ws = nullptr;
+        e->ws_bytes = 0;
+    }
+    hipError_t err = hipMalloc(&e->ws, bytes);
+    if (err != hipSuccess) {
+        e->ws = nullptr;
+        return set_err(err == hipErrorOutOfMemory ? MIMI_ERR_OUT_OF_MEMORY : MIMI_ERR_HIP,
+                       "workspace hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(err));
+    }
+    e->ws_bytes = bytes;
+    return MIMI_OK;
+}
+
+static int ensure_rope(mimi_engine* e, int64_t T) {
+    if (T <= e->rope_T) return MIMI_OK;
+    const int half = e->cfg.head_dim / 2;
+    const int64_t Tn = std::max<int64_t>(T, 256);
+    std::vector<float> cs((size_t)Tn * half), sn((size_t)Tn * half);
+    for (int d = 0; d < half; ++d) {
+        // inv_freq = 1 / theta^(2d / dim) in float32 (TF/modeling_mimi.py:546), freq = inv_freq * pos in float32
+        const float expo = (float)(2 * d) / (float)e->cfg.head_dim;
+        const float pw = (float)std::pow((double)e->cfg.rope_theta, (double)expo);
+        const float inv = 1.0f / pw;
+        for (int64_t t = 0; t < Tn; ++t) {
+            volatile float fr = inv * (float)t;
+            cs[(size_t)t * half + d] = (float)std::cos((double)fr);
+            sn[(size_t)t * half + d] = (float)std::sin((double)fr);
+        }
+    }
+    if (e->rope_cos) {
+        HIP_TRY(hipFree(e->rope_cos));
+        HIP_TRY(hipFree(e->rope_sin));
+    }
+    HIP_TRY(hipMalloc(&e->rope_cos, cs.size() * 4));
+    HIP_TRY(hipMalloc(&e->rope_sin, sn.size() * 4));
+    HIP_TRY(hipMemcpy(e->rope_cos, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->rope_sin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
+    e->rope_T = Tn;
+    return MIMI_OK;
+}
+
+static hipEvent_t pool_event(mimi_engine* e) {
+    if (!e->event_pool.empty()) {
+        hipEvent_t ev = e->event_pool.back();
+        e->event_pool.pop_back();
+        return ev;
+    }
+    hipEvent_t ev = nullptr;
+    (void)hipEventCreate(&ev);
+    return ev;
+}
+
+struct Recorder {
+    mimi_engine* e;
+    hipStream_t s;
+    void begin() {
+        if (!e->profiling) return;
+        ProfEvent pe{"", pool_event(e), 0, 0};
+        (void)hipEventRecord(pe.ev, s);
+        e->pending.push_back(pe);
+    }
+    void mark(const std::string& name, double flops, double bytes, const char* kernel) {
+        if (!e->profiling) return;
+        ProfEvent pe{name + "|" + kernel, pool_event(e), flops, bytes};
+        (void)hipEventRecord(pe.ev, s);
+        e->pending.push_back(pe);
+    }
+};
+
+static int save_tap(mimi_engine* e, const char* name, const float* src, int64_t b, int64_t t, int64_t ch,
+                    hipStream_t s) {
+    if (!e->taps) return MIMI_OK;
+    auto& tp = e->tapmap[name];
+    const size_t n = (size_t)(b * t * ch);
+    if (tp.cap < n) {
+        if (tp.d) HIP_TRY(hipFree(tp.d));
+        HIP_TRY(hipMalloc(&tp.d, n * 4));
+        tp.cap = n;
+    }
+    HIP_TRY(hipMemcpyAsync(tp.d, src, n * 4, hipMemcpyDeviceToDevice, s));
+    tp.dims[0] = b;
+    tp.dims[1] = t;
+    tp.dims[2] = ch;
+    return MIMI_OK;
+}
+
+static GemmArgs conv_args(const DevConv& cv, const float* in, int64_t Tin, float* out, int64_t Tout, int B) {
+    GemmArgs a{};
+    a.A = in;
+    a.a_bstride = Tin * cv.cin;
+    a.a_off = -(int64_t)(cv.k - cv.stride) * cv.cin;  // causal left pad
+    a.a_rs = cv.stride * cv.cin;
+    a.a_cin = cv.cin;
+    a.a_len = Tin * cv.cin;
+    a.W = cv.w;
+    a.M = (int)Tout;
+    a.N = cv.cout;
+    a.K = cv.k * cv.cin;
+    a.batch = B;
+    a.bias = cv.b;
+    a.C = out;
+    a.c_bstride = Tout * cv.cout;
+    a.ldc = cv.cout;
+    return a;
+}
+
+static GemmArgs linear_args(const float* in, int64_t rows, int K, const float* W, int N, float* out) {
+    GemmArgs a{};
+    a.A = in;
+    a.a_bstride = 0;
+    a.a_off = 0;
+    a.a_rs = K;
+    a.a_cin = K;
+    a.a_len = rows * K;
+    a.W = W;
+    a.M = (int)rows;
+    a.N = N;
+    a.K = K;
+    a.batch = 1;
+    a.C = out;
+    a.c_bstride = 0;
+    a.ldc = N;
+    return a;
+}
+
+#define LAUNCH_TRY(expr, what)                                                                           \
+    do {                                                                                                 \
+        hipError_t _e = (expr);                                                                          \
+        if (_e != hipSuccess) return set_err(MIMI_ERR_HIP, "launch %s: %s", what, hipGetErrorString(_e)); \
+    } while (0)
+
+static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int32_t* codes, int frames_per_item,
+                   hipStream_t s, Recorder& rec) {
+    RvqArgs r{};
+    r.proj = proj;
+    r.frames = frames;
+    r.D = e->cfg.codebook_dim;
+    r.ncodes = e->cfg.codebook_size;
+    r.levels = K;
+    r.nsem = e->cfg.num_semantic_quantizers;
+    r.cb_frag = e->cb_frag;
+    r.cb_rows = e->cb_rows;
+    r.cb_norm = e->cb_norm;
+    r.codes = codes;
+    r.frames_per_item = frames_per_item;
+    LAUNCH_TRY(launch_rvq(r, s), "rvq");
+    rec.mark("rvq", 2.0 * frames * r.D * r.ncodes * K, (double)frames * (2 * r.D) * 4 + (double)frames * K * 4,
+             "mimi::rvq_kernel<256, 8>");
+    return MIMI_OK;
+}
+
+static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s) {
+    const mimi_config& c = e->cfg;
+    const StagePlan p = plan_lengths(c, L);
+    Workspace w{};
+    int rc = ensure_ws(e, ws_layout(e, B, p, nullptr), s);
+    if (rc) return rc;
+    ws_layout(e, B, p, &w);
+    if ((rc = ensure_rope(e, p.frames25))) return rc;
+    Recorder rec{e, s};
+    const char* kname = "?";
+    HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));
+    rec.begin();
+    auto gemm_flops = [](const GemmArgs& a) { return 2.0 * a.batch * (double)a.M * a.N * a.K; };
+    auto gemm_bytes = [](const GemmArgs& a, bool res) {
+        // algorithmic: activation span read once, output written once (+ residual read), weights once
+        const double in = (double)a.batch * a.a_len * 4, out = (double)a.batch * a.M * a.N * 4;
+        return in + out * (res ? 2 : 1) + (double)a.N * a.K * 4;
+    };
+
+    // ---- SEANet encoder ----
+    LAUNCH_TRY(launch_conv0(audio, L, B, e->conv0.w, e->conv0.b, w.x, c.num_filters, c.kernel_size, s), "conv0");
+    rec.mark("conv0", 2.0 * B * L * c.num_filters * c.kernel_size, (double)B * L * 4 * (1 + c.num_filters),
+             "mimi::conv0_kernel<64, 7>");
+    if ((rc = save_tap(e, "conv0", w.x, B, p.T[0], c.num_filters, s))) return rc;
+    int C = c.num_filters;
+    char nm[64];
+    for (int si = 0; si < c.num_ratios; ++si) {
+        const int64_t T = p.T[si];
+        GemmArgs a3 = conv_args(e->res3[si], w.x, T, w.h, T, B);
+        LAUNCH_TRY(launch_gemm(ROLE_RES3, a3, s, &kname), "res3");
+        snprintf(nm, sizeof nm, "res3_s%d", si);
+        rec.mark(nm, gemm_flops(a3), gemm_bytes(a3, false), kname);
+        GemmArgs a1 = conv_args(e->res1[si], w.h, T, w.y, T, B);
+        a1.R = w.x;
+        LAUNCH_TRY(launch_gemm(ROLE_RES1, a1, s, &kname), "res1");
+        snprintf(nm, sizeof nm, "res1_s%d", si);
+        rec.mark(nm, gemm_flops(a1), gemm_bytes(a1, true), kname);
+        snprintf(nm, sizeof nm, "res%d_elu", si);
+        if ((rc = save_tap(e, nm, w.y, B, T, C, s))) return rc;
+        const bool last = si == c.num_ratios - 1;
+        GemmArgs ad = conv_args(e->down[si], w.y, T, w.x, p.T[si + 1], B);
+        LAUNCH_TRY(launch_gemm(last ? ROLE_DOWN_ELU : ROLE_DOWN, ad, s, &kname), "down");
+        snprintf(nm, sizeof nm, "down_s%d", si);
+        rec.mark(nm, gemm_flops(ad), gemm_bytes(ad, false), kname);
+        snprintf(nm, sizeof nm, last ? "down%d_elu" : "down%d", si);
+        if ((rc = save_tap(e, nm, w.x, B, p.T[si + 1], 2 * C, s))) return rc;
+        C *= 2;
+    }
+    const int64_t T = p.frames25;
+    const int Hd = c.hidden_size;
+    GemmArgs af = conv_args(e->final_conv, w.x, p.T[c.num_ratios], w.t0, T, B);
+    LAUNCH_TRY(launch_gemm(ROLE_FINAL, af, s, &kname), "final");
+    rec.mark("final", gemm_flops(af), gemm_bytes(af, false), kname);
+    if ((rc = save_tap(e, "encoder", w.t0, B, T, Hd, s))) return rc;
+
+    // ---- transformer (x in t0) ----
+    const int64_t rows = (int64_t)B * T;
+    const int H = c.num_attention_heads, Dh = c.head_dim;
+    double att_flops = 0;
+    for (int64_t i = 0; i < T; ++i) att_flops += 4.0 * Dh * std::min<int64_t>(i + 1, c.sliding_window);
+    att_flops *= (double)B * H;
+    for (int l = 0; l < c.num_hidden_layers; ++l) {
+        const DevXfmr& x = e->xf[l];
+        LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s), "ln1");
+        rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512>");
+        GemmArgs aq = linear_args(w.t1, T, Hd, x.wqkv, 3 * H * Dh, w.qkv);
+        aq.batch = B;
+        aq.a_bstride = T * Hd;
+        aq.c_bstride = T * 3 * H * Dh;
+        aq.rope_cos = e->rope_cos;
+        aq.rope_sin = e->rope_sin;
+        aq.rope_cols = 2 * H * Dh;
+        LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname), "qkv");
+        rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
+        LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh), s),
+                   "attention");
+        rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4, "mimi::attention_kernel");
+        GemmArgs ao = linear_args(w.att, rows, H * Dh, x.wo, Hd, w.t0);
+        ao.R = w.t0;
+        ao.scale = x.ls1;
+        LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname), "o_proj");
+        rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
+        LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s), "ln2");
+        rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512>");
+        GemmArgs a1 = linear_args(w.t1, rows, Hd, x.w1, c.intermediate_size, w.ff);
+        LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname), "fc1");
+        rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
+        GemmArgs a2 = linear_args(w.ff, rows, c.intermediate_size, x.w2, Hd, w.t0);
+        a2.R = w.t0;
+        a2.scale = x.ls2;
+        LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname), "fc2");
+        rec.mark("fc2", gemm_flops(a2), gemm_bytes(a2, true), kname);
+        snprintf(nm, sizeof nm, "xfmr%d", l);
+        if ((rc = save_tap(e, nm, w.t0, B, T, Hd, s))) return rc;
+    }
+
+    // ---- downsample (replicate pad) + input projections + RVQ ----
+    const int64_t T2 = p.frames12;
+    GemmArgs ad = conv_args(e->ds, w.t0, T, w.dsout, T2, B);
+    LAUNCH_TRY(launch_gemm(ROLE_DOWNSAMPLE, ad, s, &kname), "downsample");
+    rec.mark("downsample", gemm_flops(ad), gemm_bytes(ad, false), kname);
+    if ((rc = save_tap(e, "downsample", w.dsout, B, T2, Hd, s))) return rc;
+    const int Dq = c.vq_hidden_dim;
+    GemmArgs ap = linear_args(w.dsout, (int64_t)B * T2, Hd, e->inproj, 2 * Dq, w.proj);
+    LAUNCH_TRY(launch_gemm(ROLE_INPROJ, ap, s, &kname), "input_proj");
+    rec.mark("input_proj", gemm_flops(ap), gemm_bytes(ap, false), kname);
+    if ((rc = save_tap(e, "proj", w.proj, B, T2, 2 * Dq, s))) return rc;
+    if ((rc = run_rvq(e, w.proj, (int64_t)B * T2, K, codes, (int)T2, s, rec))) return rc;
+    HIP_TRY(hipEventRecord(e->ws_free, s));
+    return MIMI_OK;
+}
+
+extern "C" int mimi_encode(mimi_engine* e, const float* audio, int32_t batch, int64_t length, int32_t K,
+                           int32_t* codes, void* stream) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    if (!e->finalized) return set_err(MIMI_ERR_STATE, "mimi_finalize has not been called");
+    if (K <= 0) K = e->cfg.num_quantizers;
+    if (K > e->cfg.num_quantizers)
+        return set_err(MIMI_ERR_INVALID_ARGUMENT,
+                       "The number of quantizers (i.e codebooks) asked should be lower than the total number of "
+                       "quantizers %d, but is currently %d.",
+                       e->cfg.num_quantizers, K);
+    if (K < e->cfg.num_semantic_quantizers)
+        return set_err(MIMI_ERR_INVALID_ARGUMENT, "num_quantizers %d below the semantic quantizers %d", K,
+                       e->cfg.num_semantic_quantizers);
+    if (K > e->levels_available)
+        return set_err(MIMI_ERR_WEIGHTS, "num_quantizers %d but the checkpoint has %d codebooks", K, e->levels_available);
+    if (batch <= 0 || length <= 0 || !audio || !codes)
+        return set_err(MIMI_ERR_INVALID_ARGUMENT, "batch=%d length=%lld", batch, (long long)length);
+    if (length > (int64_t)1 << 31) return set_err(MIMI_ERR_INVALID_ARGUMENT, "length %lld too large", (long long)length);
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the HIP null stream, as in every HIP API
+    return encode_locked(e, audio, batch, length, K, codes, s);
+}
+
+extern "C" int mimi_rvq_encode(mimi_engine* e, const float* emb, int64_t frames, int32_t K, int32_t* codes,
+                               void* stream) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    if (!e->finalized) return set_err(MIMI_ERR_STATE, "mimi_finalize has not been called");
+    if (K <= 0) K = e->cfg.num_quantizers;
+    if (K > e->levels_available || K < e->cfg.num_semantic_quantizers)
+        return set_err(MIMI_ERR_INVALID_ARGUMENT, "num_quantizers %d out of range", K);
+    if (frames <= 0 || !emb || !codes) return set_err(MIMI_ERR_INVALID_ARGUMENT, "frames=%lld", (long long)frames);
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the HIP null stream, as in every HIP API
+    const int Hd = e->cfg.hidden_size, Dq = e->cfg.vq_hidden_dim;
+    const size_t need = (size_t)frames * 2 * Dq * sizeof(float);
+    int rc = ensure_ws(e, std::max(need, e->ws_bytes), s);
+    if (rc) return rc;
+    float* proj = reinterpret_cast<float*>(e->ws);
+    HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));
+    Recorder rec{e, s};
+    rec.begin();
+    GemmArgs ap = linear_args(emb, frames, Hd, e->inproj, 2 * Dq, proj);
+    const char* kname = "?";
+    LAUNCH_TRY(launch_gemm(ROLE_INPROJ, ap, s, &kname), "input_proj");
+    rec.mark("input_proj", 2.0 * frames * Hd * 2 * Dq, 0, kname);
+    if ((rc = run_rvq(e, proj, frames, K, codes, 0, s, rec))) return rc;
+    HIP_TRY(hipEventRecord(e->ws_free, s));
+    return MIMI_OK;
+}
+
+extern "C" void mimi_destroy(mimi_engine* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    (void)hipDeviceSynchronize();
+    for (void* p : e->allocations) (void)hipFree(p);
+    if (e->ws) (void)hipFree(e->ws);
+    if (e->rope_cos) (void)hipFree(e->rope_cos);
+    if (e->rope_sin) (void)hipFree(e->rope_sin);
+    for (auto& kv : e->tapmap)
+        if (kv.second.d) (void)hipFree(kv.second.d);
+    for (auto& pe : e->pending) (void)hipEventDestroy(pe.ev);
+    for (auto ev : e->event_pool) (void)hipEventDestroy(ev);
+    if (e->ws_free) (void)hipEventDestroy(e->ws_free);
+    delete e;
+}
+
+// ------------------------------------------------------------------------------------------------
+// instrumentation
+// ------------------------------------------------------------------------------------------------
+extern "C" int mimi_set_profiling(mimi_engine* e, int enable) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->profiling = enable != 0;
+    return MIMI_OK;
+}
+
+static int resolve_pending(mimi_engine* e) {
+    HIP_TRY(hipSetDevice(e->device));
+    hipEvent_t prev = nullptr;
+    for (auto& pe : e->pending) {
+        HIP_TRY(hipEventSynchronize(pe.ev));
+        if (pe.name.empty()) {
+            prev = pe.ev;
+            continue;
+        }
+        float ms = 0;
+        if (prev) HIP_TRY(hipEventElapsedTime(&ms, prev, pe.ev));
+        if (!e->prof.count(pe.name)) e->prof_order.push_back(pe.name);
+        ProfStat& st = e->prof[pe.name];
+        st.ms += ms;
+        st.flops += pe.flops;
+        st.bytes += pe.bytes;
+        st.launches += 1;
+        prev = pe.ev;
+    }
+    for (auto& pe : e->pending) e->event_pool.push_back(pe.ev);
+    e->pending.clear();
+    return MIMI_OK;
+}
+
+extern "C" int mimi_profile_read(mimi_engine* e, int32_t max_stages, char* names, double* total_ms, int64_t* launches,
+                                 double* flops, int32_t* n_stages) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    int rc = resolve_pending(e);
+    if (rc) return rc;
+    int i = 0;
+    for (const auto& n : e->prof_order) {
+        if (i >= max_stages) break;
+        const ProfStat& st = e->prof[n];
+        if (names) {
+            std::strncpy(names + 128 * i, n.c_str(), 127);
+            names[128 * i + 127] = 0;
+        }
+        if (total_ms) total_ms[i] = st.ms;
+        if (launches) launches[i] = st.launches;
+        if (flops) flops[2 * i] = st.flops, flops[2 * i + 1] = st.bytes;
+        ++i;
+    }
+    if (n_stages) *n_stages = i;
+    return MIMI_OK;
+}
+
+extern "C" int mimi_profile_reset(mimi_engine* e) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    int rc = resolve_pending(e);
+    e->prof.clear();
+    e->prof_order.clear();
+    return rc;
+}
+
+extern "C" int mimi_set_taps(mimi_engine* e, int enable) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->taps = enable != 0;
+    return MIMI_OK;
+}
+
+extern "C" int mimi_get_tap(mimi_engine* e, const char* name, float* dst, int64_t cap, int64_t* numel, int64_t dims[3]) {
+    if (!e || !name) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    auto it = e->tapmap.find(name);
+    if (it == e->tapmap.end()) return set_err(MIMI_ERR_INVALID_ARGUMENT, "no tap named %s", name);
+    const auto& tp = it->second;
+    const int64_t n = tp.dims[0] * tp.dims[1] * tp.dims[2];
+    if (numel) *numel = n;
+    if (dims) std::memcpy(dims, tp.dims, sizeof(tp.dims));
+    if (dst) {
+        if (cap < n) return set_err(MIMI_ERR_INVALID_ARGUMENT, "tap %s needs %lld floats", name, (long long)n);
+        HIP_TRY(hipSetDevice(e->device));
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(dst, tp.d, n * 4, hipMemcpyDeviceToHost));
+    }
+    return MIMI_OK;
+}

@@ -1,0 +1,96 @@
+// Internal launcher interface between the engine (engine.cpp) and the HIP kernels (gemm.hip, ops.hip).
+// Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace mimi {
+
+// Epilogues of the implicit-GEMM conv / linear kernel.
+enum Epi : int {
+    EPI_NONE = 0,          // C = acc                                  (input_proj, downsample)
+    EPI_BIAS = 1,          // C = acc + bias                           (down convs 0-2)
+    EPI_BIAS_ELU = 2,      // C = ELU(acc + bias)                      (res conv k3, down conv 3)
+    EPI_BIAS_RES_ELU = 3,  // C = ELU(R + (acc + bias))                (res conv k1 + identity skip)
+    EPI_GELU = 4,          // C = GELU_erf(acc)                        (fc1)
+    EPI_SCALE_RES = 5,     // C = R + scale * acc                      (o_proj, fc2 with layer scale)
+    EPI_ROPE = 6,          // C = RoPE(acc) on columns < rope_cols      (fused q/k/v projection)
+    EPI_BIAS_OUT = 7,      // C = acc + bias  (final conv, channel-last output = transformer input)
+};
+
+enum Pad : int { PAD_ZERO = 0, PAD_REPLICATE = 1 };
+
+// C[b][m][n] = epi( sum_k A(b, m, k) * W[n][k] ) with the im2col view of a channels-last activation:
+//   A(b, m, k) = Aptr[b*a_bstride + a_off + m*a_rs + k]      (k in [0, K), K = ksize*Cin)
+// Elements outside [0, a_len) of a batch item read as 0 (causal / extra zero padding) or, for
+// PAD_REPLICATE, as the nearest valid time step (torch 'replicate' pad).  Cin % 4 == 0 is required.
+struct GemmArgs {
+    const float* A;
+    long long a_bstride;
+    long long a_off;
+    int a_rs;
+    int a_cin;
+    long long a_len;
+    const float* W;
+    int M, N, K;
+    int batch;
+    const float* bias;
+    const float* R;
+    const float* scale;
+    const float* rope_cos;  // [T][head_dim/2]
+    const float* rope_sin;
+    int rope_cols;
+    float* C;
+    long long c_bstride;
+    int ldc;
+};
+
+// Launch the GEMM for a given conv/linear role (the role picks tile shape and template flags).
+enum GemmRole : int {
+    ROLE_RES3 = 0,   // ELU-on-load, bias + ELU epilogue
+    ROLE_RES1,       // bias + residual + ELU
+    ROLE_DOWN,       // bias (raw output; next res block needs it for the skip)
+    ROLE_DOWN_ELU,   // bias + ELU (last down conv: only the final conv reads it, through ELU)
+    ROLE_FINAL,      // bias
+    ROLE_QKV,        // RoPE
+    ROLE_OPROJ,      // scale + residual
+    ROLE_FC1,        // GELU
+    ROLE_FC2,        // scale + residual
+    ROLE_DOWNSAMPLE, // replicate pad, no bias
+    ROLE_INPROJ,     // plain
+    ROLE_COUNT
+};
+// *kname (optional) receives the kernel symbol as rocprofv3 prints it, for per-kernel profile aggregation.
+hipError_t launch_gemm(int role, const GemmArgs& a, hipStream_t s, const char** kname = nullptr);
+
+// conv0: Cin = 1, k = 7 causal conv, channels-last output [B][T][64].
+hipError_t launch_conv0(const float* x, long long L, int batch, const float* w /*[64][7]*/,
+                        const float* b, float* y, int cout, int ksize, hipStream_t s);
+
+// LayerNorm over the last dim (C = 512) of rows.
+hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* y, long long rows,
+                            int C, float eps, hipStream_t s);
+
+// Sliding-window causal attention on the fused qkv tensor [B][T][3*H*D] (q, k already rotated);
+// output [B][T][H*D].
+hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window,
+                            float scale, hipStream_t s);
+
+// Split RVQ: proj [F][2*Dq] (semantic | acoustic projections), codebooks in fragment layout, codes
+// out[level][F] int32 (or [b][level][t] when frames_per_item > 0).
+struct RvqArgs {
+    const float* proj;      // [F][2*D]
+    long long frames;
+    int D;                  // codebook dim (256)
+    int ncodes;             // 2048
+    int levels;             // K
+    int nsem;               // semantic levels (1)
+    const float* cb_frag;   // [level][ncodes/32][D/8][64 lanes][4]
+    const float* cb_rows;   // [level][ncodes][D]
+    const float* cb_norm;   // [level][ncodes]
+    int32_t* codes;
+    int frames_per_item;    // T (for [b][level][t] output); 0 -> [level][frame]
+};
+hipError_t launch_rvq(const RvqArgs& a, hipStream_t s);
+
+}  // namespace mimi

@@ -1,0 +1,394 @@
+// Non-GEMM kernels of the Mimi encode path for gfx950: the Cin = 1 input conv, LayerNorm, the
+// sliding-window attention and the split residual-VQ argmin.
+#include "kernels.h"
+
+namespace mimi {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------------------------------------
+// conv0: causal Conv1d(1 -> 64, k = 7) (TF/modeling_mimi.py:455), channels-last output [B][L][64].
+// HBM-bound (7 MACs per 4-byte output): each workgroup stages its 128 + 6 input samples in LDS and
+// writes 128 x 64 outputs as coalesced float4 rows.
+// ------------------------------------------------------------------------------------------------
+template <int COUT, int KS>
+__global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, long long L,
+                                                    const float* __restrict__ w, const float* __restrict__ bias,
+                                                    float* __restrict__ y) {
+    constexpr int TT = 128;
+    constexpr int CG = COUT / 4;        // channel groups of 4
+    constexpr int TG = 256 / CG;        // time lanes
+    __shared__ float xs[TT + KS - 1];
+    __shared__ float ws[COUT * KS];
+    __shared__ float bs[COUT];
+    const int b = blockIdx.y;
+    const long long t0 = (long long)blockIdx.x * TT;
+    const float* xb = x + (long long)b * L;
+    for (int i = threadIdx.x; i < TT + KS - 1; i += 256) {
+        const long long t = t0 - (KS - 1) + i;
+        xs[i] = (t >= 0 && t < L) ? xb[t] : 0.0f;
+    }
+    for (int i = threadIdx.x; i < COUT * KS; i += 256) ws[i] = w[i];
+    for (int i = threadIdx.x; i < COUT; i += 256) bs[i] = bias[i];
+    __syncthreads();
+    const int cg = threadIdx.x % CG;
+    const int tl = threadIdx.x / CG;
+    float* yb = y + (long long)b * L * COUT;
+    for (int tt = tl; tt < TT; tt += TG) {
+        const long long t = t0 + tt;
+        if (t >= L) break;
+        float out[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int co = cg * 4 + c;
+            float acc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < KS; ++k) acc = fmaf(ws[co * KS + k], xs[tt + k], acc);
+            out[c] = acc + bs[co];
+        }
+        *reinterpret_cast<f32x4*>(yb + t * COUT + cg * 4) = f32x4{out[0], out[1], out[2], out[3]};
+    }
+}
+
+hipError_t launch_conv0(const float* x, long long L, int batch, const float* w, const float* b, float* y,
+                        int cout, int ksize, hipStream_t s) {
+    if (cout != 64 || ksize != 7) return hipErrorInvalidValue;
+    dim3 grid((unsigned)((L + 127) / 128), batch);
+    hipLaunchKernelGGL((conv0_kernel<64, 7>), grid, dim3(256), 0, s, x, L, w, b, y);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// LayerNorm(512) (TF/modeling_mimi.py:737-738): one wave per row, two-pass mean / variance in fp32,
+// y = (x * rstd + (-mean * rstd)) * gamma + beta as the torch CPU kernel forms it.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                        const float* __restrict__ bta, float* __restrict__ y,
+                                                        long long rows, float eps) {
+    constexpr int PER = C / 64;  // floats per lane
+    static_assert(PER % 4 == 0, "C multiple of 256");
+    const int lane = threadIdx.x & 63;
+    const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float* xr = x + row * C;
+    float v[PER];
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) {
+        f32x4 t = *reinterpret_cast<const f32x4*>(xr + q * 256 + lane * 4);
+        v[q * 4 + 0] = t.x; v[q * 4 + 1] = t.y; v[q * 4 + 2] = t.z; v[q * 4 + 3] = t.w;
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) s += v[i];
+    const float mean = wave_sum(s) / (float)C;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const float d = v[i] - mean;
+        s2 += d * d;
+    }
+    const float var = wave_sum(s2) / (float)C;
+    const float rstd = 1.0f / sqrtf(var + eps);
+    const float sc = rstd;
+    const float bi = -rstd * mean;
+    float* yr = y + row * C;
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) {
+        const int c0 = q * 256 + lane * 4;
+        const f32x4 gg = *reinterpret_cast<const f32x4*>(g + c0);
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(bta + c0);
+        f32x4 o;
+        o.x = (v[q * 4 + 0] * sc + bi) * gg.x + bb.x;
+        o.y = (v[q * 4 + 1] * sc + bi) * gg.y + bb.y;
+        o.z = (v[q * 4 + 2] * sc + bi) * gg.z + bb.z;
+        o.w = (v[q * 4 + 3] * sc + bi) * gg.w + bb.w;
+        *reinterpret_cast<f32x4*>(yr + c0) = o;
+    }
+}
+
+hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* y, long long rows, int C,
+                            float eps, hipStream_t s) {
+    if (C != 512) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((layernorm_kernel<512>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, g, b, y,
+                       rows, eps);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Sliding-window causal attention (window W incl. self: masking_utils.py:76-101), head_dim 64.
+// One workgroup = 64 queries of one (batch, head); 4 lanes per query each take every 4th key of a
+// 64-key LDS chunk with an online (running max / sum) softmax, merged across the 4 lanes at the end.
+// ~1 % of the encode FLOPs, so this is VALU code.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attention_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                        int T, int H, int window, float scale) {
+    constexpr int D = 64;
+    constexpr int QB = 64;
+    constexpr int KC = 64;
+    __shared__ float Ks[KC][D + 1];
+    __shared__ float Vs[KC][D + 1];
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int q0 = blockIdx.x * QB;
+    const int sub = threadIdx.x & 3;
+    const int qi = q0 + (threadIdx.x >> 2);
+    const long long ld = 3LL * H * D;
+    const float* base = qkv + (long long)b * T * ld;
+    float q[D];
+    const bool qvalid = qi < T;
+    if (qvalid) {
+#pragma unroll
+        for (int d = 0; d < D; d += 4) {
+            f32x4 t = *reinterpret_cast<const f32x4*>(base + (long long)qi * ld + h * D + d);
+            q[d] = t.x; q[d + 1] = t.y; q[d + 2] = t.z; q[d + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int d = 0; d < D; ++d) q[d] = 0.f;
+    }
+    float o[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) o[d] = 0.f;
+    float m = -INFINITY, l = 0.f;
+
+    int kstart = q0 - window + 1;
+    if (kstart < 0) kstart = 0;
+    const int kend = min(T - 1, q0 + QB - 1);
+    for (int c0 = kstart; c0 <= kend; c0 += KC) {
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < KC * (D / 4); idx += 256) {
+            const int r = idx / (D / 4);
+            const int c = (idx % (D / 4)) * 4;
+            const int j = c0 + r;
+            f32x4 kv = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
+            if (j <= kend) {
+                kv = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + H * D + h * D + c);
+                vv = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + 2 * H * D + h * D + c);
+            }
+            Ks[r][c] = kv.x; Ks[r][c + 1] = kv.y; Ks[r][c + 2] = kv.z; Ks[r][c + 3] = kv.w;
+            Vs[r][c] = vv.x; Vs[r][c + 1] = vv.y; Vs[r][c + 2] = vv.z; Vs[r][c + 3] = vv.w;
+        }
+        __syncthreads();
+        if (!qvalid) continue;
+        for (int r = sub; r < KC; r += 4) {
+            const int j = c0 + r;
+            if (j > qi || j <= qi - window || j > kend) continue;
+            float sdot = 0.f;
+#pragma unroll
+            for (int d = 0; d < D; ++d) sdot = fmaf(q[d], Ks[r][d], sdot);
+            const float sc = sdot * scale;
+            if (sc > m) {
+                const float corr = expf(m - sc);
+                l = l * corr;
+#pragma unroll
+                for (int d = 0; d < D; ++d) o[d] = o[d] * corr;
+                m = sc;
+            }
+            const float pexp = expf(sc - m);
+            l = l + pexp;
+#pragma unroll
+            for (int d = 0; d < D; ++d) o[d] = fmaf(pexp, Vs[r][d], o[d]);
+        }
+    }
+    // merge the 4 partial softmaxes of a query (lanes 4q .. 4q+3 of the same wave)
+    float mt = m;
+    mt = fmaxf(mt, __shfl_xor(mt, 1));
+    mt = fmaxf(mt, __shfl_xor(mt, 2));
+    const float f = (m == -INFINITY) ? 0.f : expf(m - mt);
+    float lt = l * f;
+    lt += __shfl_xor(lt, 1);
+    lt += __shfl_xor(lt, 2);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        float v = o[d] * f;
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        o[d] = v;
+    }
+    if (qvalid) {
+        float* orow = out + ((long long)b * T + qi) * (H * D) + h * D;
+        const float inv = 1.0f / lt;
+#pragma unroll
+        for (int d = 0; d < D; d += 4) {
+            if ((d / 16) != sub) continue;
+            *reinterpret_cast<f32x4*>(orow + d) = f32x4{o[d] * inv, o[d + 1] * inv, o[d + 2] * inv, o[d + 3] * inv};
+        }
+    }
+}
+
+hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window, float scale,
+                            hipStream_t s) {
+    if (D != 64) return hipErrorInvalidValue;
+    dim3 grid((T + 63) / 64, H, batch);
+    hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, qkv, out, T, H, window, scale);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Split residual VQ (TF/modeling_mimi.py:964-1126) on fp32 MFMA, bit-exact with the reference:
+//   dist = sqrt(clamp_min( sum_k(-2 r_k) e_k  (+ |r|^2) (+ |e|^2), 0 ))
+// is torch's cdist 'mm' form (torch/_decomp/decompositions.py:691-703), whose CPU matmul is ONE in-order
+// FMA chain over k = 0..255, then + |r|^2, then + |e|^2 (verified bitwise in the survey container).
+// v_mfma_f32_32x32x2_f32 is an in-order fmaf chain over its two k (k0 then k1), so feeding k = 2t (lane
+// half 0) and 2t+1 (half 1) at step t reproduces the chain exactly.  |r|^2 follows torch's
+// x.pow(2).sum(-1) order (4 accumulators x 8 lanes, then lanes in order).  argmin keeps the first index.
+// One workgroup = 32 frames; its 8 waves split the 2048 codes; levels are chained in LDS.
+// ------------------------------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ float torch_sqsum(const float* r) {
+    // 4 vector accumulators of 8 lanes over blocks of 8, combined acc0+acc1+acc2+acc3, lanes summed in order
+    float tot = 0.f;
+    float lanes[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        float a[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int blk = 0; blk < D / 8; ++blk) {
+            const float v = r[blk * 8 + l];
+            a[blk & 3] = a[blk & 3] + v * v;
+        }
+        lanes[l] = ((a[0] + a[1]) + a[2]) + a[3];
+    }
+    tot = lanes[0];
+#pragma unroll
+    for (int l = 1; l < 8; ++l) tot = tot + lanes[l];
+    return tot;
+}
+
+template <int D, int NW>
+__global__ __launch_bounds__(NW * 64) void rvq_kernel(RvqArgs p) {
+    constexpr int FR = 32;
+    constexpr int LDH = D / 2 + 4;  // half-image row (even or odd k), +4 pad
+    __shared__ __attribute__((aligned(16))) float res[FR][D];
+    __shared__ __attribute__((aligned(16))) float img[2][FR][LDH];  // -2*r split by k parity
+    __shared__ float xn[FR];
+    __shared__ float redd[NW][FR];
+    __shared__ int redi[NW][FR];
+    __shared__ int best[FR];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5;
+    const long long f0 = (long long)blockIdx.x * FR;
+    const int ntile = p.ncodes / 32;
+    const int tiles_per_wave = ntile / NW;
+    const int nu = D / 8;
+
+    for (int level = 0; level < p.levels; ++level) {
+        if (level == 0 || level == p.nsem) {
+            // (re)load the projection this quantizer works on: semantic half, then acoustic half
+            const int coff = (level == 0) ? 0 : D;
+            for (int idx = tid; idx < FR * D; idx += NW * 64) {
+                const int i = idx / D, k = idx % D;
+                const long long f = f0 + i;
+                res[i][k] = (f < p.frames) ? p.proj[f * (2 * D) + coff + k] : 0.0f;
+            }
+            __syncthreads();
+        }
+        // A image and |r|^2
+        for (int idx = tid; idx < FR * D; idx += NW * 64) {
+            const int i = idx / D, k = idx % D;
+            img[k & 1][i][k >> 1] = -2.0f * res[i][k];
+        }
+        if (tid < FR) xn[tid] = torch_sqsum<D>(res[tid]);
+        __syncthreads();
+
+        const float* cbf = p.cb_frag + (long long)level * ntile * nu * 256;
+        const float* cbn = p.cb_norm + (long long)level * p.ncodes;
+        float bd[16];
+        int bi[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { bd[r] = INFINITY; bi[r] = 0x7fffffff; }
+        float xr[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xr[r] = xn[(r & 3) + 8 * (r >> 2) + 4 * h];
+
+        for (int tt = 0; tt < tiles_per_wave; ++tt) {
+            const int jt = wave * tiles_per_wave + tt;
+            const f32x4* bsrc = reinterpret_cast<const f32x4*>(cbf + (long long)jt * nu * 256) + lane;
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+            const float* arow = &img[h][lane & 31][0];
+#pragma unroll 8
+            for (int u = 0; u < D / 8; ++u) {
+                const f32x4 bv = bsrc[u * 64];
+                const f32x4 av = *reinterpret_cast<const f32x4*>(arow + u * 4);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0], bv[0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1], bv[1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[2], bv[2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[3], bv[3], acc, 0, 0, 0);
+            }
+            const int j = jt * 32 + (lane & 31);
+            const float yn = cbn[j];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float d2 = acc[r] + xr[r];
+                d2 = d2 + yn;
+                const float d = __builtin_sqrtf(fmaxf(d2, 0.0f));
+                if (d < bd[r]) { bd[r] = d; bi[r] = j; }
+            }
+        }
+        // reduce over the 32 lanes of each half (same rows), ties -> lower index
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float d = bd[r];
+            int ix = bi[r];
+#pragma unroll
+            for (int o = 16; o >= 1; o >>= 1) {
+                const float od = __shfl_xor(d, o);
+                const int oi = __shfl_xor(ix, o);
+                if (od < d || (od == d && oi < ix)) { d = od; ix = oi; }
+            }
+            if ((lane & 31) == 0) {
+                const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
+                redd[wave][i] = d;
+                redi[wave][i] = ix;
+            }
+        }
+        __syncthreads();
+        if (tid < FR) {
+            float d = redd[0][tid];
+            int ix = redi[0][tid];
+            for (int w = 1; w < NW; ++w) {
+                const float od = redd[w][tid];
+                const int oi = redi[w][tid];
+                if (od < d || (od == d && oi < ix)) { d = od; ix = oi; }
+            }
+            if (ix < 0 || ix >= p.ncodes) ix = 0;  // all-NaN row: torch would return a NaN index; keep in range
+            best[tid] = ix;
+            const long long f = f0 + tid;
+            if (f < p.frames) {
+                if (p.frames_per_item > 0) {
+                    const long long bb = f / p.frames_per_item, t = f % p.frames_per_item;
+                    p.codes[(bb * p.levels + level) * p.frames_per_item + t] = ix;
+                } else {
+                    p.codes[(long long)level * p.frames + f] = ix;
+                }
+            }
+        }
+        __syncthreads();
+        // residual -= embed[idx]
+        const float* rows = p.cb_rows + (long long)level * p.ncodes * D;
+        for (int idx = tid; idx < FR * D; idx += NW * 64) {
+            const int i = idx / D, k = idx % D;
+            res[i][k] = res[i][k] - rows[(long long)best[i] * D + k];
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_rvq(const RvqArgs& a, hipStream_t s) {
+    if (a.D != 256 || a.ncodes % (32 * 8) != 0) return hipErrorInvalidValue;
+    if (a.frames <= 0) return hipSuccess;
+    dim3 grid((unsigned)((a.frames + 31) / 32));
+    hipLaunchKernelGGL((rvq_kernel<256, 8>), grid, dim3(512), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace mimi
