@@ -188,7 +188,16 @@ def main():
             achieved = dom["bytes"] / dom["launches"] / t_launch / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4)}
-        roof.update({"traffic": None, "kernel": dom_name, "stages": dom["stages"],
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            k = pmc.get("kernels", {}).get(dom_name, {})
+            if "traffic_bytes" in k:
+                traffic = {"bytes_per_launch": round(k["traffic_bytes"]), "source": f"profiles/{pmc['tag']}_pmc_summary.json",
+                           "fetch_bytes": round(k["fetch_bytes"]), "write_bytes": round(k["write_bytes"])}
+        roof.update({"traffic": traffic, "kernel": dom_name, "stages": dom["stages"],
                      "avg_launch_ms": round(1000 * t_launch, 4), "launches": dom["launches"],
                      "algorithmic_per_launch": dom["flops"] / dom["launches"] if gemm_like
                      else dom["bytes"] / dom["launches"]})

@@ -905,23 +905,38 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
     };
 
     // ---- SEANet encoder ----
-    LAUNCH_TRY(launch_conv0(audio, L, B, e->conv0.w, e->conv0.b, w.x, c.num_filters, c.kernel_size, s), "conv0");
-    rec.mark("conv0", 2.0 * B * L * c.num_filters * c.kernel_size, (double)B * L * 4 * (1 + c.num_filters),
-             "mimi::conv0_kernel<64, 7>");
-    if ((rc = save_tap(e, "conv0", w.x, B, p.T[0], c.num_filters, s))) return rc;
+    // conv0 is fused into the stage-0 residual block (x0 is recomputed per tile from the audio); the standalone
+    // conv0 kernel only runs to materialise the "conv0" tap for per-stage parity tests.
+    if (e->taps) {
+        LAUNCH_TRY(launch_conv0(audio, L, B, e->conv0.w, e->conv0.b, w.x, c.num_filters, c.kernel_size, s), "conv0");
+        if ((rc = save_tap(e, "conv0", w.x, B, p.T[0], c.num_filters, s))) return rc;
+    }
     int C = c.num_filters;
     char nm[64];
     for (int si = 0; si < c.num_ratios; ++si) {
         const int64_t T = p.T[si];
-        GemmArgs a3 = conv_args(e->res3[si], w.x, T, w.h, T, B);
-        LAUNCH_TRY(launch_gemm(ROLE_RES3, a3, s, &kname), "res3");
-        snprintf(nm, sizeof nm, "res3_s%d", si);
-        rec.mark(nm, gemm_flops(a3), gemm_bytes(a3, false), kname);
-        GemmArgs a1 = conv_args(e->res1[si], w.h, T, w.y, T, B);
-        a1.R = w.x;
-        LAUNCH_TRY(launch_gemm(ROLE_RES1, a1, s, &kname), "res1");
-        snprintf(nm, sizeof nm, "res1_s%d", si);
-        rec.mark(nm, gemm_flops(a1), gemm_bytes(a1, true), kname);
+        ResArgs ra{};
+        ra.x = w.x;
+        if (si == 0) {
+            ra.audio = audio;
+            ra.w0 = e->conv0.w;
+            ra.b0 = e->conv0.b;
+        }
+        ra.T = T;
+        ra.batch = B;
+        ra.w3 = e->res3[si].w;
+        ra.b3 = e->res3[si].b;
+        ra.w1 = e->res1[si].w;
+        ra.b1 = e->res1[si].b;
+        ra.y = w.y;
+        LAUNCH_TRY(launch_resblock(C, ra, s, &kname), "resblock");
+        snprintf(nm, sizeof nm, "res_s%d", si);
+        {
+            const double H = C / c.compress;
+            const double fl = 2.0 * B * T * (3.0 * C * H + H * C) + (si == 0 ? 2.0 * B * T * C * c.kernel_size : 0.0);
+            const double by = (double)B * T * 4 * (si == 0 ? 1 + C : 2 * C) + (3.0 * C * H + H * C) * 4;
+            rec.mark(nm, fl, by, kname);
+        }
         snprintf(nm, sizeof nm, "res%d_elu", si);
         if ((rc = save_tap(e, nm, w.y, B, T, C, s))) return rc;
         const bool last = si == c.num_ratios - 1;

@@ -63,6 +63,22 @@ enum GemmRole : int {
 // *kname (optional) receives the kernel symbol as rocprofv3 prints it, for per-kernel profile aggregation.
 hipError_t launch_gemm(int role, const GemmArgs& a, hipStream_t s, const char** kname = nullptr);
 
+// Fused residual block + trailing ELU: y = ELU(x + b1 + W1 . ELU(b3 + W3 (*) ELU(x))), [B][T][C].
+struct ResArgs {
+    const float* x;       // [B][T][C] raw input (unused when audio != null)
+    const float* audio;   // stage 0 only: [B][T] waveform; x = conv0(audio) is recomputed in-kernel
+    const float* w0;      // conv0 weight [64][7]
+    const float* b0;      // conv0 bias [64]
+    long long T;
+    int batch;
+    const float* w3;  // [C/2][3*C]  (W'[n][kk*C + ci])
+    const float* b3;
+    const float* w1;  // [C][C/2]
+    const float* b1;
+    float* y;
+};
+hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** kname);
+
 // conv0: Cin = 1, k = 7 causal conv, channels-last output [B][T][64].
 hipError_t launch_conv0(const float* x, long long L, int batch, const float* w /*[64][7]*/,
                         const float* b, float* y, int cout, int ksize, hipStream_t s);

@@ -123,110 +123,132 @@ hipError_t launch_layernorm(const float* x, const float* g, const float* b, floa
 }
 
 // ------------------------------------------------------------------------------------------------
-// Sliding-window causal attention (window W incl. self: masking_utils.py:76-101), head_dim 64.
-// One workgroup = 64 queries of one (batch, head); 4 lanes per query each take every 4th key of a
-// 64-key LDS chunk with an online (running max / sum) softmax, merged across the 4 lanes at the end.
-// ~1 % of the encode FLOPs, so this is VALU code.
+// Sliding-window causal attention (window W incl. self: masking_utils.py:76-101), head_dim 64, on fp32 MFMA.
+// Workgroup = 128 queries of one (batch, head), 4 waves x 32 queries; 32-key K/V chunks staged in LDS.
+// Each wave computes S^T = K . Q^T (keys on rows, queries on lanes), so a query's softmax statistics sit in
+// one lane (16 registers + the other lane half), then O^T += V^T . P^T reuses the probabilities straight
+// from the S^T accumulator registers as the B operand (no shuffles, no LDS round trip).  Q is pre-scaled
+// by 1/sqrt(64) = 1/8 (exact).  Online softmax with running max / sum per query, fp32 throughout.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict__ qkv, float* __restrict__ out,
                                                         int T, int H, int window, float scale) {
     constexpr int D = 64;
-    constexpr int QB = 64;
-    constexpr int KC = 64;
-    __shared__ float Ks[KC][D + 1];
-    __shared__ float Vs[KC][D + 1];
+    constexpr int KC = 32;
+    constexpr int LDKS = D + 4;
+    constexpr int LDO = D + 1;
+    __shared__ __attribute__((aligned(16))) float Ks[KC * LDKS];
+    __shared__ __attribute__((aligned(16))) float Vs[KC * D];
+    __shared__ float Os[4][32 * LDO];
     const int b = blockIdx.z, h = blockIdx.y;
-    const int q0 = blockIdx.x * QB;
-    const int sub = threadIdx.x & 3;
-    const int qi = q0 + (threadIdx.x >> 2);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hf = lane >> 5, col = lane & 31;
+    const int q0 = blockIdx.x * 128;
+    const int qw = q0 + wave * 32;
+    const int qi = qw + col;  // this lane's query (B operand column / S^T column)
     const long long ld = 3LL * H * D;
     const float* base = qkv + (long long)b * T * ld;
-    float q[D];
-    const bool qvalid = qi < T;
-    if (qvalid) {
+
+    // Q fragment (B operand): lane (q, hf) holds q[8kq + 4hf + s], kq = 0..7, pre-scaled
+    f32x4 qf[8];
 #pragma unroll
-        for (int d = 0; d < D; d += 4) {
-            f32x4 t = *reinterpret_cast<const f32x4*>(base + (long long)qi * ld + h * D + d);
-            q[d] = t.x; q[d + 1] = t.y; q[d + 2] = t.z; q[d + 3] = t.w;
-        }
-    } else {
-#pragma unroll
-        for (int d = 0; d < D; ++d) q[d] = 0.f;
+    for (int kq = 0; kq < 8; ++kq) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (qi < T) v = *reinterpret_cast<const f32x4*>(base + (long long)qi * ld + h * D + kq * 8 + hf * 4);
+        qf[kq] = v * scale;
     }
-    float o[D];
+    f32x16 o[2];
 #pragma unroll
-    for (int d = 0; d < D; ++d) o[d] = 0.f;
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
     float m = -INFINITY, l = 0.f;
 
-    int kstart = q0 - window + 1;
-    if (kstart < 0) kstart = 0;
-    const int kend = min(T - 1, q0 + QB - 1);
+    const int kstart = max(0, q0 - window + 1);
+    const int kend = min(T - 1, q0 + 127);
     for (int c0 = kstart; c0 <= kend; c0 += KC) {
         __syncthreads();
-        for (int idx = threadIdx.x; idx < KC * (D / 4); idx += 256) {
-            const int r = idx / (D / 4);
-            const int c = (idx % (D / 4)) * 4;
+        for (int idx = tid; idx < KC * (D / 4); idx += 256) {
+            const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
             const int j = c0 + r;
             f32x4 kv = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
             if (j <= kend) {
                 kv = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + H * D + h * D + c);
                 vv = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + 2 * H * D + h * D + c);
             }
-            Ks[r][c] = kv.x; Ks[r][c + 1] = kv.y; Ks[r][c + 2] = kv.z; Ks[r][c + 3] = kv.w;
-            Vs[r][c] = vv.x; Vs[r][c + 1] = vv.y; Vs[r][c + 2] = vv.z; Vs[r][c + 3] = vv.w;
+            *reinterpret_cast<f32x4*>(Ks + r * LDKS + c) = kv;
+            *reinterpret_cast<f32x4*>(Vs + r * D + c) = vv;
         }
         __syncthreads();
-        if (!qvalid) continue;
-        for (int r = sub; r < KC; r += 4) {
-            const int j = c0 + r;
-            if (j > qi || j <= qi - window || j > kend) continue;
-            float sdot = 0.f;
+        // skip chunks entirely outside this wave's band [qw - W + 1, qw + 31]
+        if (c0 > qw + 31 || c0 + KC - 1 < qw - window + 1) continue;
+        // S^T[key][query]
+        f32x16 st;
 #pragma unroll
-            for (int d = 0; d < D; ++d) sdot = fmaf(q[d], Ks[r][d], sdot);
-            const float sc = sdot * scale;
-            if (sc > m) {
-                const float corr = expf(m - sc);
-                l = l * corr;
+        for (int r = 0; r < 16; ++r) st[r] = 0.f;
 #pragma unroll
-                for (int d = 0; d < D; ++d) o[d] = o[d] * corr;
-                m = sc;
+        for (int kq = 0; kq < 8; ++kq) {
+            const f32x4 kf = *reinterpret_cast<const f32x4*>(Ks + col * LDKS + kq * 8 + hf * 4);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) st = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[s], qf[kq][s], st, 0, 0, 0);
+        }
+        // mask + online softmax for this lane's query
+        float cmax = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = c0 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            const bool ok = key <= qi && key > qi - window && key <= kend;
+            st[r] = ok ? st[r] : -INFINITY;
+            cmax = fmaxf(cmax, st[r]);
+        }
+        cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
+        const float mnew = fmaxf(m, cmax);
+        const float corr = (m == -INFINITY) ? 0.f : expf(m - mnew);
+        float psum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float pv = (st[r] == -INFINITY) ? 0.f : expf(st[r] - mnew);
+            st[r] = pv;
+            psum += pv;
+        }
+        psum += __shfl_xor(psum, 32);
+        l = l * corr + psum;
+        m = mnew;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[t][r] *= corr;
+        // O^T[d][query] += V^T . P^T : step r pairs key (r&3)+8(r>>2) (half 0) with +4 (half 1)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = (r & 3) + 8 * (r >> 2) + 4 * hf;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const float va = Vs[key * D + t * 32 + col];
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(va, st[r], o[t], 0, 0, 0);
             }
-            const float pexp = expf(sc - m);
-            l = l + pexp;
-#pragma unroll
-            for (int d = 0; d < D; ++d) o[d] = fmaf(pexp, Vs[r][d], o[d]);
         }
     }
-    // merge the 4 partial softmaxes of a query (lanes 4q .. 4q+3 of the same wave)
-    float mt = m;
-    mt = fmaxf(mt, __shfl_xor(mt, 1));
-    mt = fmaxf(mt, __shfl_xor(mt, 2));
-    const float f = (m == -INFINITY) ? 0.f : expf(m - mt);
-    float lt = l * f;
-    lt += __shfl_xor(lt, 1);
-    lt += __shfl_xor(lt, 2);
+    // O^T -> LDS (per wave) -> coalesced rows of out[b][q][h*64 + d]
+    const float inv = (l > 0.f) ? 1.0f / l : 0.f;
+    float* ow = Os[wave];
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-        float v = o[d] * f;
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        o[d] = v;
-    }
-    if (qvalid) {
-        float* orow = out + ((long long)b * T + qi) * (H * D) + h * D;
-        const float inv = 1.0f / lt;
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int d = 0; d < D; d += 4) {
-            if ((d / 16) != sub) continue;
-            *reinterpret_cast<f32x4*>(orow + d) = f32x4{o[d] * inv, o[d + 1] * inv, o[d + 2] * inv, o[d + 3] * inv};
+        for (int r = 0; r < 16; ++r) {
+            const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            ow[col * LDO + d] = o[t][r] * inv;
         }
+    __syncthreads();
+    for (int qq = 0; qq < 32; ++qq) {
+        const int q = qw + qq;
+        if (q < T) out[((long long)b * T + q) * (H * D) + h * D + lane] = ow[qq * LDO + lane];
     }
 }
 
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window, float scale,
                             hipStream_t s) {
     if (D != 64) return hipErrorInvalidValue;
-    dim3 grid((T + 63) / 64, H, batch);
+    dim3 grid((T + 127) / 128, H, batch);
     hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, qkv, out, T, H, window, scale);
     return hipGetLastError();
 }

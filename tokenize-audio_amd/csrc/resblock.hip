@@ -1,0 +1,333 @@
+// Fused SEANet residual block (TF/modeling_mimi.py:408-447, with the ELU that precedes the next down conv):
+//   y = ELU( x + b1 + W1 . ELU( b3 + W3 (*) ELU(x) ) )          x, y: [B][T][C] channels-last
+// W3: causal k=3 conv C -> C/2 (W'[n][kk*C + ci]), W1: k=1 conv C/2 -> C.  One workgroup owns BM time rows:
+//   GEMM1  h[BM][C/2] = ELU(x) window (*) W3   -> ELU(h + b3) kept in LDS (never written to HBM)
+//   GEMM2  y[BM][C]   = h . W1^T, in column passes of NP, epilogue + b1 + x (residual), ELU -> HBM
+// so the block reads x once and writes y once (the unfused pair moved x, h, h, x, y).
+// WINDOW: the (BM+2) x C slab of ELU(x) (rows m0-2 .. m0+BM-1, causal zeros before t=0) is staged in LDS once
+//   and GEMM1's im2col rows are overlapping windows of it (row i, tap kk = slab row i+kk): one ELU per element.
+// STREAM (large C, where the slab does not fit): GEMM1's A is streamed in 32-wide K slices with ELU on load.
+// All MFMAs are v_mfma_f32_32x32x2_f32; LDS rows are padded by 4 floats (row stride = 4 mod 64 dwords), which
+// keeps the ds_read_b128 fragment reads conflict-free.
+#include "kernels.h"
+
+namespace mimi {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float elu_f(float x) { return x > 0.0f ? x : expm1f(x); }
+__device__ __forceinline__ f32x4 elu4(f32x4 v) {
+    v.x = elu_f(v.x); v.y = elu_f(v.y); v.z = elu_f(v.z); v.w = elu_f(v.w);
+    return v;
+}
+
+// acc[TM][TN] += A[rows][32] . B[cols][32]^T for one 32-wide K slice.  A / B point at the wave's first row /
+// first column (row r at A + r*lda); lane (i, h) feeds k = 8*kq + 4*h + s at step s of quad kq.
+template <int TM, int TN>
+__device__ __forceinline__ void mma_k32(f32x16 (&acc)[TM][TN], const float* A, int lda, const float* B, int ldb,
+                                        int lane) {
+    const int r = lane & 31;
+    const int kh = (lane >> 5) * 4;
+#pragma unroll
+    for (int kq = 0; kq < 4; ++kq) {
+        f32x4 af[TM], bf[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f32x4*>(A + (i * 32 + r) * lda + kq * 8 + kh);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bf[j] = *reinterpret_cast<const f32x4*>(B + (j * 32 + r) * ldb + kq * 8 + kh);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    }
+}
+
+template <int C, int BM, bool WINDOW, bool FIRST, int W1M, int W1N, int W2M, int W2N, int NP>
+__global__ __launch_bounds__(256) void resblock_kernel(ResArgs p) {
+    constexpr int H = C / 2;
+    constexpr int K1 = 3 * C;
+    constexpr int LDK = 36;
+    constexpr int LDX = C + 4;
+    constexpr int LDH = H + 4;
+    constexpr int TM1 = BM / W1M / 32, TN1 = H / W1N / 32;
+    constexpr int TM2 = BM / W2M / 32, TN2 = NP / W2N / 32;
+    static_assert(W1M * W1N == 4 && W2M * W2N == 4, "4 waves");
+    static_assert(TM1 >= 1 && TN1 >= 1 && TM2 >= 1 && TN2 >= 1, "tiles");
+    static_assert(C % NP == 0 && H % 32 == 0, "shapes");
+    constexpr int XS = WINDOW ? (BM + 2) * LDX : BM * LDK;
+    constexpr int BST = (H > NP ? H : NP) * LDK;
+    constexpr int A_F4 = WINDOW ? 1 : BM * 8 / 256;  // streamed A slice: float4 per thread
+    constexpr int B1_F4 = H * 8 / 256 > 0 ? H * 8 / 256 : 1;
+    constexpr int B2_F4 = NP * 8 / 256 > 0 ? NP * 8 / 256 : 1;
+    static_assert(WINDOW || A_F4 * 256 == BM * 8, "A loader");
+    static_assert(!FIRST || (WINDOW && C == 64), "conv0 fusion is for the 64-channel first stage");
+    constexpr int AUD = FIRST ? BM + 8 + 64 * 8 : 0;  // audio window + conv0 weights/bias (FIRST)
+
+    __shared__ __attribute__((aligned(16))) float lds[XS + BM * LDH + BST + AUD];
+    float* Xs = lds;
+    float* Hs = lds + XS;
+    float* Bs = Hs + BM * LDH;
+    float* Aud = Bs + BST;  // FIRST: audio[m0-8 .. m0+BM), then w0[64][7] (stride 8), b0[64]
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long T = p.T;
+    const long long m0 = (long long)blockIdx.x * BM;
+    const int b = blockIdx.y;
+    const float* __restrict__ xb = p.x + (long long)b * T * C;
+
+    // ---------------- GEMM1: h = ELU(x) (*) W3 ----------------
+    if (FIRST) {
+        // conv0 (Cin = 1, k = 7, TF/modeling_mimi.py:455) recomputed per tile from the audio: the 24 kHz x0
+        // tensor never exists in HBM.  Same arithmetic as conv0_kernel: fmaf chain over taps, then + bias.
+        const float* ab = p.audio + (long long)b * T;
+        for (int i = tid; i < BM + 8; i += 256) {
+            const long long pos = m0 - 8 + i;
+            Aud[i] = (pos >= 0 && pos < T) ? ab[pos] : 0.0f;
+        }
+        for (int i = tid; i < 64 * 7; i += 256) Aud[BM + 8 + (i / 7) * 8 + (i % 7)] = p.w0[i];
+        for (int i = tid; i < 64; i += 256) Aud[BM + 8 + i * 8 + 7] = p.b0[i];
+        __syncthreads();
+        for (int idx = tid; idx < (BM + 2) * 64; idx += 256) {
+            const int r = idx >> 6, c = idx & 63;
+            const long long pos = m0 - 2 + r;
+            float v = 0.0f;  // causal zero padding of x0 before t = 0
+            if (pos >= 0) {
+                const float* wr = Aud + BM + 8 + c * 8;
+                float acc = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 7; ++k) acc = fmaf(wr[k], Aud[r + k], acc);  // audio[pos - 6 + k]
+                v = elu_f(acc + wr[7]);
+            }
+            Xs[r * LDX + c] = v;
+        }
+    } else if (WINDOW) {
+        constexpr int TOT = (BM + 2) * (C / 4);
+        constexpr int NPRO = (TOT + 255) / 256;
+        f32x4 pre[NPRO];
+#pragma unroll
+        for (int i = 0; i < NPRO; ++i) {  // all loads in flight before the first use
+            const int idx = tid + i * 256;
+            const int r = idx / (C / 4), c = (idx % (C / 4)) * 4;
+            const long long pos = m0 - 2 + r;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (idx < TOT && pos >= 0 && pos < T) v = *reinterpret_cast<const f32x4*>(xb + pos * C + c);
+            pre[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < NPRO; ++i) {
+            const int idx = tid + i * 256;
+            const int r = idx / (C / 4), c = (idx % (C / 4)) * 4;
+            if (idx < TOT) *reinterpret_cast<f32x4*>(Xs + r * LDX + c) = elu4(pre[i]);
+        }
+    }
+    f32x4 ra[A_F4], rb[B1_F4 > B2_F4 ? B1_F4 : B2_F4];
+    auto load1 = [&](int k0) {
+        if (!WINDOW) {
+#pragma unroll
+            for (int i = 0; i < A_F4; ++i) {
+                const int idx = tid + i * 256;
+                const int r = idx >> 3, c = (idx & 7) * 4;
+                const long long e = (m0 + r - 2) * C + k0 + c;  // causal pad 2 rows; rows >= T never read
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                if (m0 + r < T && e >= 0) v = *reinterpret_cast<const f32x4*>(xb + e);
+                ra[i] = v;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < B1_F4; ++i) {
+            const int idx = tid + i * 256;
+            const int r = idx >> 3, c = (idx & 7) * 4;
+            if (r < H) rb[i] = *reinterpret_cast<const f32x4*>(p.w3 + (long long)r * K1 + k0 + c);
+        }
+    };
+    auto store1 = [&]() {
+        if (!WINDOW) {
+#pragma unroll
+            for (int i = 0; i < A_F4; ++i) {
+                const int idx = tid + i * 256;
+                const int r = idx >> 3, c = (idx & 7) * 4;
+                *reinterpret_cast<f32x4*>(Xs + r * LDK + c) = elu4(ra[i]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < B1_F4; ++i) {
+            const int idx = tid + i * 256;
+            const int r = idx >> 3, c = (idx & 7) * 4;
+            if (r < H) *reinterpret_cast<f32x4*>(Bs + r * LDK + c) = rb[i];
+        }
+    };
+
+    const int w1m = wave / W1N, w1n = wave % W1N;
+    f32x16 acc1[TM1][TN1];
+#pragma unroll
+    for (int i = 0; i < TM1; ++i)
+#pragma unroll
+        for (int j = 0; j < TN1; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc1[i][j][r] = 0.f;
+
+    constexpr int NK1 = K1 / 32;
+    load1(0);
+    store1();
+    __syncthreads();
+    for (int kc = 0; kc < NK1; ++kc) {
+        if (kc + 1 < NK1) load1((kc + 1) * 32);
+        const float* Ab;
+        int lda;
+        if (WINDOW) {
+            const int k0 = kc * 32;
+            const int kk = k0 / C, ci0 = k0 % C;
+            Ab = Xs + (w1m * TM1 * 32 + kk) * LDX + ci0;
+            lda = LDX;
+        } else {
+            Ab = Xs + (w1m * TM1 * 32) * LDK;
+            lda = LDK;
+        }
+        mma_k32<TM1, TN1>(acc1, Ab, lda, Bs + (w1n * TN1 * 32) * LDK, LDK, lane);
+        if (kc + 1 < NK1) {
+            __syncthreads();
+            store1();
+            __syncthreads();
+        }
+    }
+    // residual x for the GEMM2 epilogue: FIRST recomputes raw x0 into the (now dead) window slab; the other
+    // stages prefetch it from global (L2-hot: just read) into registers so the loads fly under GEMM2
+    constexpr int TM2P = BM / W2M / 32, TN2P = NP / W2N / 32;
+    const int w2m = wave / W2N, w2n = wave % W2N;
+    if (FIRST) {
+        __syncthreads();  // every wave is done reading the ELU slab
+        for (int idx = tid; idx < BM * 64; idx += 256) {
+            const int r = idx >> 6, c = idx & 63;
+            const float* wr = Aud + BM + 8 + c * 8;
+            float acc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) acc = fmaf(wr[k], Aud[r + 2 + k], acc);
+            Xs[r * LDX + c] = acc + wr[7];
+        }
+    }
+    float xres[TM2P][TN2P][16];
+    auto prefetch_res = [&](int n0) {
+        if (FIRST) return;
+        const int rb0 = w2m * TM2P * 32 + 4 * (lane >> 5);
+        const int cb0 = n0 + w2n * TN2P * 32 + (lane & 31);
+#pragma unroll
+        for (int j = 0; j < TN2P; ++j)
+#pragma unroll
+            for (int i = 0; i < TM2P; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const long long row = m0 + rb0 + i * 32 + (r & 3) + 8 * (r >> 2);
+                    xres[i][j][r] = row < T ? xb[row * C + cb0 + j * 32] : 0.0f;
+                }
+    };
+    prefetch_res(0);
+    // epilogue 1: Hs = ELU(h + b3)
+    {
+        const int rb0 = w1m * TM1 * 32 + 4 * (lane >> 5);
+        const int cb0 = w1n * TN1 * 32 + (lane & 31);
+#pragma unroll
+        for (int j = 0; j < TN1; ++j) {
+            const int col = cb0 + j * 32;
+            const float bias = p.b3[col];
+#pragma unroll
+            for (int i = 0; i < TM1; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = rb0 + i * 32 + (r & 3) + 8 * (r >> 2);
+                    Hs[row * LDH + col] = elu_f(acc1[i][j][r] + bias);
+                }
+        }
+    }
+
+    // ---------------- GEMM2: y = ELU(x + b1 + h . W1^T), NP columns per pass ----------------
+    float* __restrict__ yb = p.y + (long long)b * T * C;
+    for (int n0 = 0; n0 < C; n0 += NP) {
+        auto load2 = [&](int k0) {
+#pragma unroll
+            for (int i = 0; i < B2_F4; ++i) {
+                const int idx = tid + i * 256;
+                const int r = idx >> 3, c = (idx & 7) * 4;
+                if (r < NP) rb[i] = *reinterpret_cast<const f32x4*>(p.w1 + (long long)(n0 + r) * H + k0 + c);
+            }
+        };
+        auto store2 = [&]() {
+#pragma unroll
+            for (int i = 0; i < B2_F4; ++i) {
+                const int idx = tid + i * 256;
+                const int r = idx >> 3, c = (idx & 7) * 4;
+                if (r < NP) *reinterpret_cast<f32x4*>(Bs + r * LDK + c) = rb[i];
+            }
+        };
+        f32x16 acc2[TM2][TN2];
+#pragma unroll
+        for (int i = 0; i < TM2; ++i)
+#pragma unroll
+            for (int j = 0; j < TN2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc2[i][j][r] = 0.f;
+        constexpr int NK2 = H / 32;
+        load2(0);
+        __syncthreads();  // Hs complete; previous readers of Bs done
+        store2();
+        __syncthreads();
+        for (int kc = 0; kc < NK2; ++kc) {
+            if (kc + 1 < NK2) load2((kc + 1) * 32);
+            mma_k32<TM2, TN2>(acc2, Hs + (w2m * TM2 * 32) * LDH + kc * 32, LDH, Bs + (w2n * TN2 * 32) * LDK, LDK,
+                              lane);
+            if (kc + 1 < NK2) {
+                __syncthreads();
+                store2();
+                __syncthreads();
+            }
+        }
+        const int rb0 = w2m * TM2 * 32 + 4 * (lane >> 5);
+        const int cb0 = n0 + w2n * TN2 * 32 + (lane & 31);
+#pragma unroll
+        for (int j = 0; j < TN2; ++j) {
+            const int col = cb0 + j * 32;
+            const float bias = p.b1[col];
+#pragma unroll
+            for (int i = 0; i < TM2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const long long row = m0 + rb0 + i * 32 + (r & 3) + 8 * (r >> 2);
+                    if (row < T) {
+                        const float xr = FIRST ? Xs[(row - m0) * LDX + col] : xres[i][j][r];
+                        yb[row * C + col] = elu_f(xr + (acc2[i][j][r] + bias));
+                    }
+                }
+        }
+        if (n0 + NP < C) prefetch_res(n0 + NP);
+    }
+}
+
+template <int C, int BM, bool WINDOW, bool FIRST, int W1M, int W1N, int W2M, int W2N, int NP>
+static hipError_t run_res(const ResArgs& a, hipStream_t s, const char** kname) {
+    static char name[160];
+    if (!name[0])
+        snprintf(name, sizeof(name), "mimi::resblock_kernel<%d, %d, %s, %s, %d, %d, %d, %d, %d>", C, BM,
+                 WINDOW ? "true" : "false", FIRST ? "true" : "false", W1M, W1N, W2M, W2N, NP);
+    if (kname) *kname = name;
+    dim3 grid((unsigned)((a.T + BM - 1) / BM), a.batch);
+    hipLaunchKernelGGL((resblock_kernel<C, BM, WINDOW, FIRST, W1M, W1N, W2M, W2N, NP>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** kname) {
+    if (a.T <= 0 || a.batch <= 0) return hipErrorInvalidValue;
+    switch (C) {
+        case 64:
+            if (a.audio) return run_res<64, 128, true, true, 4, 1, 4, 1, 64>(a, s, kname);
+            return run_res<64, 128, true, false, 4, 1, 4, 1, 64>(a, s, kname);
+        case 128: return run_res<128, 64, true, false, 2, 2, 2, 2, 128>(a, s, kname);
+        case 256: return run_res<256, 64, false, false, 2, 2, 2, 2, 128>(a, s, kname);
+        case 512: return run_res<512, 32, false, false, 1, 4, 1, 4, 256>(a, s, kname);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace mimi

@@ -1,0 +1,58 @@
+"""Copy the judged rocprofv3 evidence of a profiling round from gpurun_out/prof_<tag>/ into profiles/.
+
+    python tools/summarize_profile.py r1
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats summary, verbatim),
+profiles/<tag>_pmc_summary.json (per-kernel mean FETCH_SIZE / WRITE_SIZE per launch from the two separate
+--pmc passes, with the gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md §HBM applied) and
+profiles/pmc_summary.json (the latest, read by bench.py to fill roofline.traffic).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(tag):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    bj = os.path.join(src, "bench_under_trace.json")
+    if os.path.exists(bj):
+        shutil.copy(bj, os.path.join(dst, f"{tag}_bench_under_trace.json"))
+    out = {"tag": tag, "units": "bytes per launch", "fetch_correction": 2.0,
+           "note": "FETCH_SIZE (KB) x 1024 x 2 (gfx950 reports half of wide streaming reads), WRITE_SIZE (KB) x 1024;"
+                   " separate --pmc passes of `bench.py --steps 2 --warmup 1`", "kernels": {}}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        p = os.path.join(src, f"pmc_{counter}", "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(p)):
+            agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+        for k, v in agg.items():
+            name = k.replace("void ", "", 1).split("(")[0].strip()
+            d = out["kernels"].setdefault(name, {})
+            mean_kb = sum(v) / len(v)
+            if counter == "FETCH_SIZE":
+                d["fetch_bytes"] = mean_kb * 1024 * 2.0
+                d["fetch_raw_kb"] = mean_kb
+            else:
+                d["write_bytes"] = mean_kb * 1024
+            d["launches_" + counter] = len(v)
+    for d in out["kernels"].values():
+        if "fetch_bytes" in d and "write_bytes" in d:
+            d["traffic_bytes"] = d["fetch_bytes"] + d["write_bytes"]
+    for name in (f"{tag}_pmc_summary.json", "pmc_summary.json"):
+        with open(os.path.join(dst, name), "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
+    print("wrote profiles for", tag, len(out["kernels"]), "kernels")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r1")
