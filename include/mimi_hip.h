@@ -106,6 +106,17 @@ int mimi_encode(mimi_engine* e, const float* dev_audio, int32_t batch, int64_t l
 int mimi_rvq_encode(mimi_engine* e, const float* dev_embedding, int64_t frames, int32_t num_quantizers,
                     int32_t* dev_codes, void* stream);
 
+/*
+ * Arithmetic of the conv / linear GEMMs (the residual VQ distances are always exact fp32):
+ *   MIMI_PRECISION_F32     v_mfma_f32_32x32x2_f32 (fp32 MFMA)
+ *   MIMI_PRECISION_BF16X6  fp32 emulated on the bf16 matrix cores: both operands split into 3 bf16 planes,
+ *                          6 plane products accumulated in fp32 (default; ~fp32 accuracy, 2.7x MFMA rate)
+ *   MIMI_PRECISION_BF16X3  2 planes, 3 products (~1e-5 relative, 5.3x MFMA rate)
+ */
+enum { MIMI_PRECISION_F32 = 0, MIMI_PRECISION_BF16X6 = 1, MIMI_PRECISION_BF16X3 = 2 };
+int mimi_set_precision(mimi_engine* e, int32_t mode);
+int mimi_get_precision(const mimi_engine* e);
+
 /* Frames produced for `length` samples with the default config (reference float32 length math). */
 int64_t mimi_encoded_length(int64_t length);
 int64_t mimi_encoded_length_cfg(const mimi_config* cfg, int64_t length);

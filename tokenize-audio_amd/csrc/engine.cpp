@@ -141,12 +141,14 @@ extern "C" int64_t mimi_encoded_length(int64_t length) { return mimi_encoded_len
 // ------------------------------------------------------------------------------------------------
 struct DevConv {
     int cin = 0, cout = 0, k = 0, stride = 1;
-    float* w = nullptr;  // [cout][k*cin]
-    float* b = nullptr;  // [cout] or null
+    float* w = nullptr;      // [cout][k*cin]
+    void* wsplit = nullptr;  // bf16 planes [3][cout][k*cin] of w (split-bf16 precision modes)
+    float* b = nullptr;      // [cout] or null
 };
 
 struct DevXfmr {
     float *ln1_w, *ln1_b, *wqkv, *wo, *ls1, *ln2_w, *ln2_b, *w1, *w2, *ls2;
+    void *wqkv_s, *wo_s, *w1_s, *w2_s;  // bf16 planes
 };
 
 struct ProfEvent {
@@ -168,6 +170,7 @@ struct mimi_engine {
     std::mutex mu;
     bool finalized = false;
     int levels_available = 0;
+    int precision = PREC_BF16X6;
 
     std::unordered_map<std::string, std::vector<float>> host_w;
     std::unordered_map<std::string, std::vector<int64_t>> expected;  // name -> shape
@@ -219,6 +222,37 @@ static int upload(mimi_engine* e, float** dst, const std::vector<float>& host) {
     int rc = dev_alloc(e, reinterpret_cast<void**>(dst), host.size() * sizeof(float));
     if (rc) return rc;
     HIP_TRY(hipMemcpy(*dst, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+    return MIMI_OK;
+}
+
+// x = x0 + x1 + x2 with x_p = bf16_rne(x - x0 - ... - x_{p-1}) (each subtraction exact in fp32)
+static uint16_t f2bf_rne(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    u += 0x7FFF + ((u >> 16) & 1);
+    return (uint16_t)(u >> 16);
+}
+static float bf2f(uint16_t h) {
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+static int upload_split(mimi_engine* e, void** dst, const std::vector<float>& host) {
+    const size_t n = host.size();
+    std::vector<uint16_t> planes(3 * n);
+    for (size_t i = 0; i < n; ++i) {
+        float r = host[i];
+        for (int p = 0; p < 3; ++p) {
+            const uint16_t h = f2bf_rne(r);
+            planes[p * n + i] = h;
+            r = r - bf2f(h);
+        }
+    }
+    int rc = dev_alloc(e, dst, planes.size() * sizeof(uint16_t));
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(*dst, planes.data(), planes.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     return MIMI_OK;
 }
 
@@ -545,8 +579,10 @@ static int make_conv(mimi_engine* e, DevConv& dc, const std::string& prefix, int
     dc.cout = cout;
     dc.k = k;
     dc.stride = stride;
-    rc = upload(e, &dc.w, cin == 1 ? *w : relayout_conv(*w, cout, cin, k));
+    const std::vector<float> wl = cin == 1 ? *w : relayout_conv(*w, cout, cin, k);
+    rc = upload(e, &dc.w, wl);
     if (rc) return rc;
+    if (cin % 4 == 0 && (k * cin) % 32 == 0 && (rc = upload_split(e, &dc.wsplit, wl))) return rc;
     if (bias) {
         std::vector<float>* b;
         rc = get_w(e, prefix + "bias", &b);
@@ -618,7 +654,7 @@ extern "C" int mimi_finalize(mimi_engine* e) {
         qkv.insert(qkv.end(), q->begin(), q->end());
         qkv.insert(qkv.end(), k->begin(), k->end());
         qkv.insert(qkv.end(), v->begin(), v->end());
-        if ((rc = upload(e, &x.wqkv, qkv))) return rc;
+        if ((rc = upload(e, &x.wqkv, qkv)) || (rc = upload_split(e, &x.wqkv_s, qkv))) return rc;
         struct {
             const char* n;
             float** d;
@@ -634,6 +670,8 @@ extern "C" int mimi_finalize(mimi_engine* e) {
         for (auto& sp : simple) {
             if ((rc = get_w(e, p + sp.n, &t))) return rc;
             if ((rc = upload(e, sp.d, *t))) return rc;
+            void** sd = sp.d == &x.wo ? &x.wo_s : sp.d == &x.w1 ? &x.w1_s : sp.d == &x.w2 ? &x.w2_s : nullptr;
+            if (sd && (rc = upload_split(e, sd, *t))) return rc;
         }
     }
     if ((rc = make_conv(e, e->ds, "downsample.conv.", h, h, c.downsample_kernel, c.downsample_stride, false))) return rc;
@@ -829,6 +867,7 @@ static GemmArgs conv_args(const DevConv& cv, const float* in, int64_t Tin, float
     a.a_cin = cv.cin;
     a.a_len = Tin * cv.cin;
     a.W = cv.w;
+    a.Wsplit = cv.wsplit;
     a.M = (int)Tout;
     a.N = cv.cout;
     a.K = cv.k * cv.cin;
@@ -941,7 +980,7 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
         if ((rc = save_tap(e, nm, w.y, B, T, C, s))) return rc;
         const bool last = si == c.num_ratios - 1;
         GemmArgs ad = conv_args(e->down[si], w.y, T, w.x, p.T[si + 1], B);
-        LAUNCH_TRY(launch_gemm(last ? ROLE_DOWN_ELU : ROLE_DOWN, ad, s, &kname), "down");
+        LAUNCH_TRY(launch_gemm(last ? ROLE_DOWN_ELU : ROLE_DOWN, ad, s, &kname, e->precision), "down");
         snprintf(nm, sizeof nm, "down_s%d", si);
         rec.mark(nm, gemm_flops(ad), gemm_bytes(ad, false), kname);
         snprintf(nm, sizeof nm, last ? "down%d_elu" : "down%d", si);
@@ -951,7 +990,7 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
     const int64_t T = p.frames25;
     const int Hd = c.hidden_size;
     GemmArgs af = conv_args(e->final_conv, w.x, p.T[c.num_ratios], w.t0, T, B);
-    LAUNCH_TRY(launch_gemm(ROLE_FINAL, af, s, &kname), "final");
+    LAUNCH_TRY(launch_gemm(ROLE_FINAL, af, s, &kname, e->precision), "final");
     rec.mark("final", gemm_flops(af), gemm_bytes(af, false), kname);
     if ((rc = save_tap(e, "encoder", w.t0, B, T, Hd, s))) return rc;
 
@@ -966,31 +1005,35 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
         LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s), "ln1");
         rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512>");
         GemmArgs aq = linear_args(w.t1, T, Hd, x.wqkv, 3 * H * Dh, w.qkv);
+        aq.Wsplit = x.wqkv_s;
         aq.batch = B;
         aq.a_bstride = T * Hd;
         aq.c_bstride = T * 3 * H * Dh;
         aq.rope_cos = e->rope_cos;
         aq.rope_sin = e->rope_sin;
         aq.rope_cols = 2 * H * Dh;
-        LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname), "qkv");
+        LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, e->precision), "qkv");
         rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
         LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh), s),
                    "attention");
         rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4, "mimi::attention_kernel");
         GemmArgs ao = linear_args(w.att, rows, H * Dh, x.wo, Hd, w.t0);
+        ao.Wsplit = x.wo_s;
         ao.R = w.t0;
         ao.scale = x.ls1;
-        LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname), "o_proj");
+        LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, e->precision), "o_proj");
         rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
         LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s), "ln2");
         rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512>");
         GemmArgs a1 = linear_args(w.t1, rows, Hd, x.w1, c.intermediate_size, w.ff);
-        LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname), "fc1");
+        a1.Wsplit = x.w1_s;
+        LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, e->precision), "fc1");
         rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
         GemmArgs a2 = linear_args(w.ff, rows, c.intermediate_size, x.w2, Hd, w.t0);
+        a2.Wsplit = x.w2_s;
         a2.R = w.t0;
         a2.scale = x.ls2;
-        LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname), "fc2");
+        LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname, e->precision), "fc2");
         rec.mark("fc2", gemm_flops(a2), gemm_bytes(a2, true), kname);
         snprintf(nm, sizeof nm, "xfmr%d", l);
         if ((rc = save_tap(e, nm, w.t0, B, T, Hd, s))) return rc;
@@ -999,7 +1042,7 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
     // ---- downsample (replicate pad) + input projections + RVQ ----
     const int64_t T2 = p.frames12;
     GemmArgs ad = conv_args(e->ds, w.t0, T, w.dsout, T2, B);
-    LAUNCH_TRY(launch_gemm(ROLE_DOWNSAMPLE, ad, s, &kname), "downsample");
+    LAUNCH_TRY(launch_gemm(ROLE_DOWNSAMPLE, ad, s, &kname, e->precision), "downsample");
     rec.mark("downsample", gemm_flops(ad), gemm_bytes(ad, false), kname);
     if ((rc = save_tap(e, "downsample", w.dsout, B, T2, Hd, s))) return rc;
     const int Dq = c.vq_hidden_dim;
@@ -1083,6 +1126,17 @@ extern "C" void mimi_destroy(mimi_engine* e) {
 // ------------------------------------------------------------------------------------------------
 // instrumentation
 // ------------------------------------------------------------------------------------------------
+extern "C" int mimi_set_precision(mimi_engine* e, int32_t mode) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    if (mode < MIMI_PRECISION_F32 || mode > MIMI_PRECISION_BF16X3)
+        return set_err(MIMI_ERR_INVALID_ARGUMENT, "precision mode %d", mode);
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->precision = mode;
+    return MIMI_OK;
+}
+
+extern "C" int mimi_get_precision(const mimi_engine* e) { return e ? e->precision : -1; }
+
 extern "C" int mimi_set_profiling(mimi_engine* e, int enable) {
     if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
     std::lock_guard<std::mutex> lk(e->mu);

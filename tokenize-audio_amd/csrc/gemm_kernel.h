@@ -1,0 +1,452 @@
+// The implicit-GEMM Conv1d / Linear kernel template (included by gemm.hip and by tools/gemm_bench.hip).
+#pragma once
+#include "kernels.h"
+
+namespace mimi {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float elu1(float x) { return x > 0.0f ? x : expm1f(x); }
+
+// torch CPU GELU(approximate='none'): (x * 0.5) * (1 + erf(x * M_SQRT1_2))
+__device__ __forceinline__ float gelu_erf(float x) {
+    return (x * 0.5f) * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+template <int BM, int BN, int WM, int WN, int BK, int NBUF, bool NFAST, bool ELU_IN, int PAD, int EPI, int TAG>
+__global__ __launch_bounds__(WM* WN * 64) void gemm_f32_kernel(GemmArgs p) {
+    constexpr int NT = WM * WN * 64;
+    constexpr int LDK = BK + 4;
+    constexpr int TM = BM / WM / 32;
+    constexpr int TN = BN / WN / 32;
+    constexpr int KQ = BK / 4;  // float4 per LDS row
+    constexpr int A_F4 = BM * KQ / NT;
+    constexpr int B_F4 = BN * KQ / NT;
+    static_assert(NBUF == 1 || NBUF == 2, "buffers");
+    static_assert(TM >= 1 && TN >= 1, "tile");
+    static_assert(A_F4 * NT == BM * (BK / 4) && B_F4 * NT == BN * (BK / 4), "loader");
+    static_assert(EPI != EPI_ROPE || (TN % 2 == 0), "rope pairs need even TN");
+
+    __shared__ __attribute__((aligned(16))) float lds[NBUF * (BM + BN) * LDK];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN;
+    const int wn = wave % WN;
+    const int b = blockIdx.z;
+    // NFAST: consecutive workgroups walk the N tiles of one M tile, so an activation tile is re-read by the
+    // other N tiles while it is still in L2 / the Infinity Cache instead of one full pass over M later.
+    int mt, nt;
+    if (NFAST) {
+        const int ntn = gridDim.y;
+        const int lin = blockIdx.x * ntn + blockIdx.y;
+        mt = lin / ntn;
+        nt = lin % ntn;
+        (void)ntn;
+    } else {
+        mt = blockIdx.x;
+        nt = blockIdx.y;
+    }
+    const int m0 = mt * BM;
+    const int n0 = nt * BN;
+    const int M = p.M, N = p.N, K = p.K;
+
+    const float* __restrict__ Ab = p.A + (long long)b * p.a_bstride;
+    const float* __restrict__ W = p.W;
+
+    f32x4 ra[A_F4];
+    f32x4 rb[B_F4];
+
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i) {
+            const int idx = tid + i * NT;
+            const int r = idx / KQ;
+            const int c = (idx % KQ) * 4;
+            const int m = m0 + r;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (m < M) {
+                long long e = p.a_off + (long long)m * p.a_rs + k0 + c;
+                if (PAD == PAD_ZERO) {
+                    if (e >= 0 && e < p.a_len) v = *reinterpret_cast<const f32x4*>(Ab + e);
+                } else {
+                    const long long cin = p.a_cin;
+                    long long t = e >= 0 ? e / cin : -((-e + cin - 1) / cin);
+                    const long long ch = e - t * cin;
+                    const long long tmax = p.a_len / cin - 1;
+                    t = t < 0 ? 0 : (t > tmax ? tmax : t);
+                    v = *reinterpret_cast<const f32x4*>(Ab + t * cin + ch);
+                }
+            }
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < B_F4; ++i) {
+            const int idx = tid + i * NT;
+            const int r = idx / KQ;
+            const int c = (idx % KQ) * 4;
+            const int n = n0 + r;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (n < N) v = *reinterpret_cast<const f32x4*>(W + (long long)n * K + k0 + c);
+            rb[i] = v;
+        }
+    };
+    auto sstore = [&](int buf) {
+        float* As = lds + buf * (BM + BN) * LDK;
+        float* Bs = As + BM * LDK;
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i) {
+            const int idx = tid + i * NT;
+            const int r = idx / KQ;
+            const int c = (idx % KQ) * 4;
+            f32x4 v = ra[i];
+            if (ELU_IN) {
+                v.x = elu1(v.x); v.y = elu1(v.y); v.z = elu1(v.z); v.w = elu1(v.w);
+            }
+            *reinterpret_cast<f32x4*>(As + r * LDK + c) = v;
+        }
+#pragma unroll
+        for (int i = 0; i < B_F4; ++i) {
+            const int idx = tid + i * NT;
+            const int r = idx / KQ;
+            const int c = (idx % KQ) * 4;
+            *reinterpret_cast<f32x4*>(Bs + r * LDK + c) = rb[i];
+        }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    const int KT = K / BK;
+    const int arow = wm * TM * 32 + (lane & 31);
+    const int brow = wn * TN * 32 + (lane & 31);
+    const int kh = (lane >> 5) * 4;
+
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < KT; ++kt) {
+        const int cur = NBUF == 2 ? (kt & 1) : 0;
+        const float* As = lds + cur * (BM + BN) * LDK;
+        const float* Bs = As + BM * LDK;
+        if (kt + 1 < KT) gload((kt + 1) * BK);
+#pragma unroll
+        for (int kq = 0; kq < BK / 8; ++kq) {
+            f32x4 af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                af[i] = *reinterpret_cast<const f32x4*>(As + (arow + i * 32) * LDK + kq * 8 + kh);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                bf[j] = *reinterpret_cast<const f32x4*>(Bs + (brow + j * 32) * LDK + kq * 8 + kh);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < KT) {
+            if (NBUF == 1) __syncthreads();  // single buffer: every wave is done reading before the overwrite
+            sstore(NBUF == 2 ? (cur ^ 1) : 0);
+            __syncthreads();
+        }
+    }
+
+    // ---- epilogue: lane holds col (lane&31), rows (r&3) + 8*(r>>2) + 4*(lane>>5) of each 32x32 tile
+    float* __restrict__ Cb = p.C + (long long)b * p.c_bstride;
+    const float* __restrict__ Rb = p.R ? p.R + (long long)b * p.c_bstride : nullptr;
+    const int rbase = m0 + wm * TM * 32 + 4 * (lane >> 5);
+    const int cbase = n0 + wn * TN * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = cbase + j * 32;
+            float bias = 0.0f, scale = 0.0f;
+            if (col < N) {
+                if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU || EPI == EPI_BIAS_RES_ELU || EPI == EPI_BIAS_OUT)
+                    bias = p.bias[col];
+                if (EPI == EPI_SCALE_RES) scale = p.scale[col];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
+                if (row >= M || col >= N) continue;
+                float v = acc[i][j][r];
+                const long long off = (long long)row * p.ldc + col;
+                if (EPI == EPI_BIAS || EPI == EPI_BIAS_OUT) {
+                    v = v + bias;
+                } else if (EPI == EPI_BIAS_ELU) {
+                    v = elu1(v + bias);
+                } else if (EPI == EPI_BIAS_RES_ELU) {
+                    v = elu1(Rb[off] + (v + bias));
+                } else if (EPI == EPI_GELU) {
+                    v = gelu_erf(v);
+                } else if (EPI == EPI_SCALE_RES) {
+                    v = Rb[off] + scale * v;
+                } else if (EPI == EPI_ROPE) {
+                    // pair (j even -> first half d, j+1 -> second half d+32) of one head
+                    const int hd2 = 32;
+                    if (col < p.rope_cols) {
+                        const int d = (col % 64);  // head_dim = 64
+                        const float c = p.rope_cos[(long long)row * hd2 + (d & 31)];
+                        const float sn = p.rope_sin[(long long)row * hd2 + (d & 31)];
+                        if ((j & 1) == 0) {
+                            const float x2 = acc[i][j + 1][r];
+                            v = v * c + (-x2) * sn;
+                        } else {
+                            const float x1 = acc[i][j - 1][r];
+                            v = v * c + x1 * sn;
+                        }
+                    }
+                }
+                Cb[off] = v;
+            }
+        }
+    }
+}
+
+
+// ================================================================================================
+// Split-bf16 variant: fp32 accuracy from the bf16 matrix cores.
+//
+// gfx950 has no xf32/tf32; its bf16 MFMA (v_mfma_f32_32x32x16_bf16) runs 16x the f32-MFMA rate.  Each fp32
+// operand is split exactly into NS bf16 planes (x = x0 + x1 [+ x2], x_p = bf16(x - x0 - ... - x_{p-1})) and
+// the product is the sum of the plane products whose plane indices add to < NS:
+//   NS = 3: a0b0 + a0b1 + a1b0 + a0b2 + a1b1 + a2b0  (6 MFMAs, ~24-bit operands: fp32-level error, 2.7x f32 rate)
+//   NS = 2: a0b0 + a0b1 + a1b0                       (3 MFMAs, ~16-bit operands: ~1e-5 rel error, 5.3x)
+// bf16 x bf16 products are exact in fp32 and accumulate in fp32, so what is dropped is only the plane
+// truncation (2^-24 resp. 2^-16 relative).  Activations are split as they are staged into LDS (after the
+// optional ELU); weights are split once at load time and read from global as NS bf16 planes [NS][N][K].
+// ================================================================================================
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <int NS>
+__device__ __forceinline__ void split_bf16x4(f32x4 v, bf16x4 (&out)[NS]) {
+#pragma unroll
+    for (int p = 0; p < NS; ++p) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const __bf16 h = (__bf16)v[i];
+            out[p][i] = h;
+            v[i] = v[i] - (float)h;  // exact in fp32
+        }
+    }
+}
+
+template <int NS, int TM, int TN>
+__device__ __forceinline__ void mma_split(f32x16 (&acc)[TM][TN], const bf16x8 (&a)[NS][TM],
+                                          const bf16x8 (&b)[NS][TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            // small terms first, the leading product last
+            if (NS == 3) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2 % NS][i], b[0][j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2 % NS][j], acc[i][j], 0, 0, 0);
+            }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+        }
+}
+
+template <int BM, int BN, int WM, int WN, int NS, bool ELU_IN, int PAD, int EPI, int TAG>
+__global__ __launch_bounds__(WM* WN * 64) void gemm_bf16x_kernel(GemmArgs p) {
+    constexpr int NT = WM * WN * 64;
+    constexpr int BK = 32;
+    constexpr int LDB = BK + 8;  // bf16 per LDS row: 80 B stride keeps ds_read_b128 fragments conflict-free
+    constexpr int TM = BM / WM / 32;
+    constexpr int TN = BN / WN / 32;
+    constexpr int A_F4 = BM * (BK / 4) / NT;      // fp32 float4 per thread
+    constexpr int B_C = NS * BN * (BK / 8) / NT;  // 16-byte bf16 chunks per thread
+    static_assert(NS == 2 || NS == 3, "planes");
+    static_assert(TM >= 1 && TN >= 1, "tile");
+    static_assert(A_F4 * NT == BM * (BK / 4) && B_C * NT == NS * BN * (BK / 8), "loader");
+    static_assert(EPI != EPI_ROPE || (TN % 2 == 0), "rope pairs need even TN");
+
+    __shared__ __attribute__((aligned(16))) __bf16 lds[NS * (BM + BN) * LDB];
+    __bf16* As = lds;                 // plane p at As + p*BM*LDB
+    __bf16* Bs = lds + NS * BM * LDB; // plane p at Bs + p*BN*LDB
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN;
+    const int wn = wave % WN;
+    const int b = blockIdx.z;
+    const int m0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int M = p.M, N = p.N, K = p.K;
+    const float* __restrict__ Ab = p.A + (long long)b * p.a_bstride;
+    const __bf16* __restrict__ Wp = reinterpret_cast<const __bf16*>(p.Wsplit);
+
+    f32x4 ra[A_F4];
+    uint4 rb[B_C];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i) {
+            const int idx = tid + i * NT;
+            const int r = idx >> 3;
+            const int c = (idx & 7) * 4;
+            const int m = m0 + r;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (m < M) {
+                long long e = p.a_off + (long long)m * p.a_rs + k0 + c;
+                if (PAD == PAD_ZERO) {
+                    if (e >= 0 && e < p.a_len) v = *reinterpret_cast<const f32x4*>(Ab + e);
+                } else {
+                    const long long cin = p.a_cin;
+                    long long t = e >= 0 ? e / cin : -((-e + cin - 1) / cin);
+                    const long long ch = e - t * cin;
+                    const long long tmax = p.a_len / cin - 1;
+                    t = t < 0 ? 0 : (t > tmax ? tmax : t);
+                    v = *reinterpret_cast<const f32x4*>(Ab + t * cin + ch);
+                }
+            }
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < B_C; ++i) {
+            const int idx = tid + i * NT;
+            const int pl = idx / (BN * 4);
+            const int rem = idx % (BN * 4);
+            const int r = rem >> 2;
+            const int c = (rem & 3) * 8;
+            const int n = n0 + r;
+            uint4 v = {0u, 0u, 0u, 0u};
+            if (n < N) v = *reinterpret_cast<const uint4*>(Wp + ((long long)pl * N + n) * K + k0 + c);
+            rb[i] = v;
+        }
+    };
+    auto sstore = [&]() {
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i) {
+            const int idx = tid + i * NT;
+            const int r = idx >> 3;
+            const int c = (idx & 7) * 4;
+            f32x4 v = ra[i];
+            if (ELU_IN) {
+                v.x = elu1(v.x); v.y = elu1(v.y); v.z = elu1(v.z); v.w = elu1(v.w);
+            }
+            bf16x4 h[NS];
+            split_bf16x4<NS>(v, h);
+#pragma unroll
+            for (int pl = 0; pl < NS; ++pl) *reinterpret_cast<bf16x4*>(As + pl * BM * LDB + r * LDB + c) = h[pl];
+        }
+#pragma unroll
+        for (int i = 0; i < B_C; ++i) {
+            const int idx = tid + i * NT;
+            const int pl = idx / (BN * 4);
+            const int rem = idx % (BN * 4);
+            const int r = rem >> 2;
+            const int c = (rem & 3) * 8;
+            *reinterpret_cast<uint4*>(Bs + pl * BN * LDB + r * LDB + c) = rb[i];
+        }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    const int KT = K / BK;
+    const int arow = wm * TM * 32 + (lane & 31);
+    const int brow = wn * TN * 32 + (lane & 31);
+    const int kh = (lane >> 5) * 8;
+
+    gload(0);
+    sstore();
+    __syncthreads();
+    for (int kt = 0; kt < KT; ++kt) {
+        if (kt + 1 < KT) gload((kt + 1) * BK);
+#pragma unroll
+        for (int kk = 0; kk < BK / 16; ++kk) {
+            bf16x8 af[NS][TM], bf[NS][TN];
+#pragma unroll
+            for (int pl = 0; pl < NS; ++pl) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    af[pl][i] = *reinterpret_cast<const bf16x8*>(As + pl * BM * LDB + (arow + i * 32) * LDB + kk * 16 + kh);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    bf[pl][j] = *reinterpret_cast<const bf16x8*>(Bs + pl * BN * LDB + (brow + j * 32) * LDB + kk * 16 + kh);
+            }
+            mma_split<NS, TM, TN>(acc, af, bf);
+        }
+        if (kt + 1 < KT) {
+            __syncthreads();
+            sstore();
+            __syncthreads();
+        }
+    }
+    // ---- epilogue: lane holds col (lane&31), rows (r&3) + 8*(r>>2) + 4*(lane>>5) of each 32x32 tile
+    float* __restrict__ Cb = p.C + (long long)b * p.c_bstride;
+    const float* __restrict__ Rb = p.R ? p.R + (long long)b * p.c_bstride : nullptr;
+    const int rbase = m0 + wm * TM * 32 + 4 * (lane >> 5);
+    const int cbase = n0 + wn * TN * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = cbase + j * 32;
+            float bias = 0.0f, scale = 0.0f;
+            if (col < N) {
+                if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU || EPI == EPI_BIAS_RES_ELU || EPI == EPI_BIAS_OUT)
+                    bias = p.bias[col];
+                if (EPI == EPI_SCALE_RES) scale = p.scale[col];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
+                if (row >= M || col >= N) continue;
+                float v = acc[i][j][r];
+                const long long off = (long long)row * p.ldc + col;
+                if (EPI == EPI_BIAS || EPI == EPI_BIAS_OUT) {
+                    v = v + bias;
+                } else if (EPI == EPI_BIAS_ELU) {
+                    v = elu1(v + bias);
+                } else if (EPI == EPI_BIAS_RES_ELU) {
+                    v = elu1(Rb[off] + (v + bias));
+                } else if (EPI == EPI_GELU) {
+                    v = gelu_erf(v);
+                } else if (EPI == EPI_SCALE_RES) {
+                    v = Rb[off] + scale * v;
+                } else if (EPI == EPI_ROPE) {
+                    // pair (j even -> first half d, j+1 -> second half d+32) of one head
+                    const int hd2 = 32;
+                    if (col < p.rope_cols) {
+                        const int d = (col % 64);  // head_dim = 64
+                        const float c = p.rope_cos[(long long)row * hd2 + (d & 31)];
+                        const float sn = p.rope_sin[(long long)row * hd2 + (d & 31)];
+                        if ((j & 1) == 0) {
+                            const float x2 = acc[i][j + 1][r];
+                            v = v * c + (-x2) * sn;
+                        } else {
+                            const float x1 = acc[i][j - 1][r];
+                            v = v * c + x1 * sn;
+                        }
+                    }
+                }
+                Cb[off] = v;
+            }
+        }
+    }
+}
+
+}  // namespace mimi

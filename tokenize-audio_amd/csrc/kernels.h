@@ -31,7 +31,8 @@ struct GemmArgs {
     int a_rs;
     int a_cin;
     long long a_len;
-    const float* W;
+    const float* W;       // fp32 [N][K]
+    const void* Wsplit;   // bf16 planes [3][N][K] of W (x = x0 + x1 + x2), for the split-bf16 modes
     int M, N, K;
     int batch;
     const float* bias;
@@ -60,8 +61,13 @@ enum GemmRole : int {
     ROLE_INPROJ,     // plain
     ROLE_COUNT
 };
+// Arithmetic of the GEMMs: fp32 MFMA, or fp32 emulated on the bf16 matrix cores with 3 (6 products) or
+// 2 (3 products) bf16 planes per operand (gemm_kernel.h).
+enum Precision : int { PREC_F32 = 0, PREC_BF16X6 = 1, PREC_BF16X3 = 2 };
+
 // *kname (optional) receives the kernel symbol as rocprofv3 prints it, for per-kernel profile aggregation.
-hipError_t launch_gemm(int role, const GemmArgs& a, hipStream_t s, const char** kname = nullptr);
+hipError_t launch_gemm(int role, const GemmArgs& a, hipStream_t s, const char** kname = nullptr,
+                       int precision = PREC_F32);
 
 // Fused residual block + trailing ELU: y = ELU(x + b1 + W1 . ELU(b3 + W3 (*) ELU(x))), [B][T][C].
 struct ResArgs {

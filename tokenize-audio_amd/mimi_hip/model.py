@@ -220,6 +220,16 @@ class MimiHipModel:
         return codes.view(num_quantizers, B, T).permute(1, 0, 2).long()
 
     # ---- instrumentation ------------------------------------------------------------------------
+    def set_precision(self, mode: str):
+        """'bf16x6' (default: fp32 emulated on the bf16 matrix cores, 3 planes), 'f32' (fp32 MFMA) or
+        'bf16x3' (2 planes, ~1e-5)."""
+        _lib.check(self._lib.mimi_set_precision(self._h, _lib.PRECISIONS[mode]))
+
+    @property
+    def precision(self) -> str:
+        v = self._lib.mimi_get_precision(self._h)
+        return {i: k for k, i in _lib.PRECISIONS.items()}[v]
+
     def set_profiling(self, enable: bool = True):
         _lib.check(self._lib.mimi_set_profiling(self._h, int(enable)))
 

@@ -1,0 +1,188 @@
+// Microbenchmark of gemm_f32_kernel variants on the encode's real GEMM shapes (tuning aid, not shipped).
+//   hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I tokenize-audio_amd/csrc tools/gemm_bench.hip -o tools/bin/gemm_bench
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "gemm_kernel.h"
+
+using namespace mimi;
+
+#define CK(x)                                                                          \
+    do {                                                                               \
+        hipError_t e = (x);                                                            \
+        if (e != hipSuccess) {                                                         \
+            fprintf(stderr, "%s: %s (line %d)\n", #x, hipGetErrorString(e), __LINE__); \
+            exit(1);                                                                   \
+        }                                                                              \
+    } while (0)
+
+struct Shape {
+    const char* name;
+    int cin, k, s;
+    long long tin, tout;
+    int batch, N;
+};
+
+typedef void (*LaunchFn)(const GemmArgs&, hipStream_t);
+
+template <int BM, int BN, int WM, int WN, int BK, int NBUF, bool NFAST>
+void launch(const GemmArgs& a, hipStream_t s) {
+    dim3 grid((a.M + BM - 1) / BM, (a.N + BN - 1) / BN, a.batch);
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, BK, NBUF, NFAST, false, PAD_ZERO, EPI_BIAS, 0>), grid,
+                       dim3(WM * WN * 64), 0, s, a);
+}
+
+template <int BM, int BN, int WM, int WN, int NS>
+void launch_bf(const GemmArgs& a, hipStream_t s) {
+    dim3 grid((a.M + BM - 1) / BM, (a.N + BN - 1) / BN, a.batch);
+    hipLaunchKernelGGL((gemm_bf16x_kernel<BM, BN, WM, WN, NS, false, PAD_ZERO, EPI_BIAS, 0>), grid,
+                       dim3(WM * WN * 64), 0, s, a);
+}
+
+struct Variant {
+    const char* name;
+    LaunchFn fn;
+    int bk;
+    int ns;  // 0 = fp32 weights, else bf16 planes
+};
+
+static uint16_t f2bf(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    u += 0x7FFF + ((u >> 16) & 1);
+    return (uint16_t)(u >> 16);
+}
+static float bf2f(uint16_t h) {
+    uint32_t u = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+int main(int argc, char** argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 10;
+    Shape shapes[] = {
+        {"down_s0", 64, 8, 4, 240000, 60000, 32, 128},  {"down_s1", 128, 10, 5, 60000, 12000, 32, 256},
+        {"down_s2", 256, 12, 6, 12000, 2000, 32, 512},  {"down_s3", 512, 16, 8, 2000, 250, 32, 1024},
+        {"final", 1024, 3, 1, 250, 250, 32, 512},        {"fc1", 512, 1, 1, 8000, 8000, 1, 2048},
+        {"fc2", 2048, 1, 1, 8000, 8000, 1, 512},         {"qkv", 512, 1, 1, 250, 250, 32, 1536},
+        {"o_proj", 512, 1, 1, 8000, 8000, 1, 512},
+    };
+    Variant vars[] = {
+        {"f32 128x128 bk32 nb1", launch<128, 128, 2, 2, 32, 1, false>, 32, 0},
+        {"f32 256x128 8w", launch<256, 128, 4, 2, 32, 1, false>, 32, 0},
+        {"bf16x3p 128x128", launch_bf<128, 128, 2, 2, 3>, 32, 3},
+        {"bf16x3p 256x128 8w", launch_bf<256, 128, 4, 2, 3>, 32, 3},
+        {"bf16x3p 128x256 8w", launch_bf<128, 256, 2, 4, 3>, 32, 3},
+        {"bf16x3p 64x128", launch_bf<64, 128, 1, 2, 3>, 32, 3},
+        {"bf16x3p 256x256 8w", launch_bf<256, 256, 4, 2, 3>, 32, 3},
+        {"bf16x2p 128x128", launch_bf<128, 128, 2, 2, 2>, 32, 2},
+        {"bf16x2p 256x128 8w", launch_bf<256, 128, 4, 2, 2>, 32, 2},
+        {"bf16x2p 256x256 8w", launch_bf<256, 256, 4, 2, 2>, 32, 2},
+    };
+    const int nv = sizeof(vars) / sizeof(vars[0]);
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (const Shape& sh : shapes) {
+        const long long K = (long long)sh.k * sh.cin;
+        const size_t nA = (size_t)sh.batch * sh.tin * sh.cin, nW = (size_t)sh.N * K,
+                     nC = (size_t)sh.batch * sh.tout * sh.N;
+        std::vector<float> hA(nA), hW(nW), hb(sh.N);
+        unsigned long long x = 0x9E3779B97F4A7C15ull;
+        auto rnd = [&]() {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            return (float)((x >> 40) * (1.0 / (1ull << 24)) - 0.5);
+        };
+        for (auto& v : hA) v = rnd();
+        for (auto& v : hW) v = rnd() * 0.1f;
+        for (auto& v : hb) v = rnd();
+        float *A, *W, *bias, *C, *Cref;
+        uint16_t* Wp;
+        CK(hipMalloc(&Wp, 3 * nW * 2));
+        {
+            std::vector<uint16_t> hp(3 * nW);
+            for (size_t i = 0; i < nW; ++i) {
+                float r = hW[i];
+                for (int pl = 0; pl < 3; ++pl) {
+                    const uint16_t h = f2bf(r);
+                    hp[pl * nW + i] = h;
+                    r -= bf2f(h);
+                }
+            }
+            // planes for NS = 2 are the first two planes of the NS = 3 split (same leading terms)
+            CK(hipMemcpy(Wp, hp.data(), 3 * nW * 2, hipMemcpyHostToDevice));
+        }
+        CK(hipMalloc(&A, nA * 4));
+        CK(hipMalloc(&W, nW * 4));
+        CK(hipMalloc(&bias, sh.N * 4));
+        CK(hipMalloc(&C, nC * 4));
+        CK(hipMalloc(&Cref, nC * 4));
+        CK(hipMemcpy(A, hA.data(), nA * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(W, hW.data(), nW * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(bias, hb.data(), sh.N * 4, hipMemcpyHostToDevice));
+        GemmArgs a{};
+        a.A = A;
+        a.a_bstride = sh.tin * sh.cin;
+        a.a_off = -(long long)(sh.k - sh.s) * sh.cin;
+        a.a_rs = sh.s * sh.cin;
+        a.a_cin = sh.cin;
+        a.a_len = sh.tin * sh.cin;
+        a.W = W;
+        a.M = (int)sh.tout;
+        a.N = sh.N;
+        a.K = (int)K;
+        a.batch = sh.batch;
+        a.bias = bias;
+        a.c_bstride = sh.tout * sh.N;
+        a.ldc = sh.N;
+        const double flops = 2.0 * sh.batch * sh.tout * sh.N * K;
+        std::vector<float> ref(nC), out(nC);
+        for (int v = 0; v < nv; ++v) {
+            if (K % vars[v].bk) continue;
+            a.C = v == 0 ? Cref : C;
+            a.W = W;
+            a.Wsplit = Wp;
+            if (vars[v].ns == 2) {
+                // NS = 2 reads planes [2][N][K]: the first two planes of the 3-plane buffer are exactly that
+            }
+            vars[v].fn(a, st);
+            CK(hipGetLastError());
+            CK(hipStreamSynchronize(st));
+            float best = 1e30f, tot = 0;
+            for (int r = 0; r < reps; ++r) {
+                CK(hipEventRecord(e0, st));
+                vars[v].fn(a, st);
+                CK(hipEventRecord(e1, st));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                best = fminf(best, ms);
+                tot += ms;
+            }
+            double maxrel = 0;
+            if (v > 0) {
+                CK(hipMemcpy(out.data(), C, nC * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(ref.data(), Cref, nC * 4, hipMemcpyDeviceToHost));
+                double mx = 0, md = 0;
+                for (size_t i = 0; i < nC; ++i) {
+                    mx = fmax(mx, fabs((double)ref[i]));
+                    md = fmax(md, fabs((double)out[i] - (double)ref[i]));
+                }
+                maxrel = md / (mx + 1e-30);
+            }
+            printf("%-8s %-22s best %8.3f ms  mean %8.3f ms  %7.1f TF/s(f32-equiv)  max|d|/max|ref| %.2e\n", sh.name,
+                   vars[v].name, best, tot / reps, flops / (best * 1e-3) / 1e12, maxrel);
+            fflush(stdout);
+        }
+        CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(Wp)); CK(hipFree(bias)); CK(hipFree(C)); CK(hipFree(Cref));
+    }
+    return 0;
+}
