@@ -143,6 +143,7 @@ struct DevConv {
     int cin = 0, cout = 0, k = 0, stride = 1;
     float* w = nullptr;      // [cout][k*cin]
     void* wsplit = nullptr;  // bf16 planes [3][cout][k*cin] of w (split-bf16 precision modes)
+    float* wfrag = nullptr;  // w in 32x32x2-MFMA fragment order [cout/32][k*cin/8][64][4] (stage-0 block)
     float* b = nullptr;      // [cout] or null
 };
 
@@ -254,6 +255,19 @@ static int upload_split(mimi_engine* e, void** dst, const std::vector<float>& ho
     if (rc) return rc;
     HIP_TRY(hipMemcpy(*dst, planes.data(), planes.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     return MIMI_OK;
+}
+
+// W [N][K] -> Wf[nt][kq][lane][s] = W[32*nt + (lane & 31)][8*kq + 4*(lane >> 5) + s]: a wave's B fragment
+// for one 8-wide K quad of one 32-column tile is one contiguous 1 KB load.
+static std::vector<float> frag_layout(const std::vector<float>& w, int N, int K) {
+    std::vector<float> f((size_t)N * K);
+    for (int nt = 0; nt < N / 32; ++nt)
+        for (int kq = 0; kq < K / 8; ++kq)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int s = 0; s < 4; ++s)
+                    f[(((size_t)nt * (K / 8) + kq) * 64 + lane) * 4 + s] =
+                        w[(size_t)(32 * nt + (lane & 31)) * K + 8 * kq + 4 * (lane >> 5) + s];
+    return f;
 }
 
 static std::string conv_name_first() { return "encoder.layers.0.conv"; }
@@ -583,6 +597,7 @@ static int make_conv(mimi_engine* e, DevConv& dc, const std::string& prefix, int
     rc = upload(e, &dc.w, wl);
     if (rc) return rc;
     if (cin % 4 == 0 && (k * cin) % 32 == 0 && (rc = upload_split(e, &dc.wsplit, wl))) return rc;
+    if (cout % 32 == 0 && (k * cin) % 8 == 0 && (rc = upload(e, &dc.wfrag, frag_layout(wl, cout, k * cin)))) return rc;
     if (bias) {
         std::vector<float>* b;
         rc = get_w(e, prefix + "bias", &b);
@@ -960,6 +975,8 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
             ra.audio = audio;
             ra.w0 = e->conv0.w;
             ra.b0 = e->conv0.b;
+            ra.w3frag = e->res3[0].wfrag;
+            ra.w1frag = e->res1[0].wfrag;
         }
         ra.T = T;
         ra.batch = B;

@@ -7,7 +7,7 @@ namespace mimi {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ float elu1(float x) { return x > 0.0f ? x : expm1f(x); }
+__device__ __forceinline__ float elu1(float x) { return elu_fast(x); }
 
 // torch CPU GELU(approximate='none'): (x * 0.5) * (1 + erf(x * M_SQRT1_2))
 __device__ __forceinline__ float gelu_erf(float x) {

@@ -6,6 +6,22 @@
 
 namespace mimi {
 
+// ELU(x) = x (x > 0), expm1(x) (x <= 0), branchless: degree-8 Taylor on [-0.5, 0] (truncation < 2e-8
+// relative), exp(x) - 1 below it (v_exp_f32; |error| ~1e-7 on a value in [-1, -0.39]).  ~14 VALU instead of
+// ocml expm1f's ~24 plus exec-mask branches; the SEANet applies it to every conv input.
+__device__ __forceinline__ float elu_fast(float x) {
+    float p = x * (1.0f / 40320.0f) + (1.0f / 5040.0f);
+    p = p * x + (1.0f / 720.0f);
+    p = p * x + (1.0f / 120.0f);
+    p = p * x + (1.0f / 24.0f);
+    p = p * x + (1.0f / 6.0f);
+    p = p * x + 0.5f;
+    p = (p * x) * x + x;
+    const float e = __expf(x) - 1.0f;
+    const float n = x > -0.5f ? p : e;
+    return x > 0.0f ? x : n;
+}
+
 // Epilogues of the implicit-GEMM conv / linear kernel.
 enum Epi : int {
     EPI_NONE = 0,          // C = acc                                  (input_proj, downsample)
@@ -82,6 +98,8 @@ struct ResArgs {
     const float* w1;  // [C][C/2]
     const float* b1;
     float* y;
+    const float* w3frag;  // optional: W3 / W1 in MFMA-fragment order [ntile][kquad][64 lanes][4] (stage 0)
+    const float* w1frag;
 };
 hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** kname);
 

@@ -16,7 +16,7 @@ namespace mimi {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ float elu_f(float x) { return x > 0.0f ? x : expm1f(x); }
+__device__ __forceinline__ float elu_f(float x) { return elu_fast(x); }
 __device__ __forceinline__ f32x4 elu4(f32x4 v) {
     v.x = elu_f(v.x); v.y = elu_f(v.y); v.z = elu_f(v.z); v.w = elu_f(v.w);
     return v;
@@ -305,6 +305,131 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs p) {
     }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Stage 0, wave-autonomous: conv0 (1 -> 64, k7) + residual block (64 -> 32 -> 64) + ELU, one WAVE per 32 rows.
+// Every wave builds its own 34-row ELU(x0) slab from the audio (lane = channel, 7 taps in registers), runs
+// both GEMMs with the weights read straight from L2 in MFMA-fragment order (Wf[ntile][kquad][lane][4]),
+// and keeps h in its private LDS: no __syncthreads anywhere, so the two waves sharing a SIMD drift apart
+// and overlap one's VALU work (conv0, ELU) with the other's MFMAs.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void resblock0_wave_kernel(ResArgs p) {
+    constexpr int C = 64, H = 32;
+    constexpr int LDX = C + 4, LDH = H + 4;
+    constexpr int AW = 48;  // audio window floats per wave (32 rows + 2 halo + 6 taps, padded)
+    constexpr int PERW = 34 * LDX + AW;
+    __shared__ __attribute__((aligned(16))) float lds[4 * PERW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float* Xw = lds + wave * PERW;  // [34][LDX]: ELU(x0) rows r0-2 .. r0+31, then h [32][LDH] aliased on it
+    float* Hw = Xw;
+    float* Aw = Xw + 34 * LDX;      // audio[r0 - 8 .. r0 + 40)
+    const long long T = p.T;
+    const long long r0 = ((long long)blockIdx.x * 4 + wave) * 32;
+    const int b = blockIdx.y;
+    if (r0 >= T) return;  // whole wave idle (no barriers in this kernel)
+    const float* ab = p.audio + (long long)b * T;
+    const f32x4* __restrict__ w3f = reinterpret_cast<const f32x4*>(p.w3);  // [24 kq][64][4]
+    const f32x4* __restrict__ w1f = reinterpret_cast<const f32x4*>(p.w1);  // [2 nt][4 kq][64][4]
+
+    // conv0 weights of this lane's channel; the first GEMM1 B fragments fly under the slab work
+    float w0[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) w0[k] = p.w0[lane * 7 + k];
+    const float b0 = p.b0[lane];
+    f32x4 bq[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bq[q] = w3f[q * 64 + lane];
+    if (lane < AW) {
+        const long long pos = r0 - 8 + lane;
+        Aw[lane] = (pos >= 0 && pos < T) ? ab[pos] : 0.0f;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's audio stores are visible to its reads
+    // slab: row i = position r0 - 2 + i; causal zero padding of x0 before t = 0
+    const int zero_rows = r0 >= 2 ? 0 : (int)(2 - r0);
+#pragma unroll 2
+    for (int i = 0; i < 34; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) acc = fmaf(w0[k], Aw[i + k], acc);  // audio[pos - 6 + k]
+        const float v = elu_fast(acc + b0);
+        Xw[i * LDX + lane] = i < zero_rows ? 0.0f : v;
+    }
+    // ---- GEMM1: h[32][32] = slab (*) W3, K = 192 (24 quads of 8)
+    f32x16 acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc1[r] = 0.f;
+    const int ar = lane & 31;
+    const int kh = (lane >> 5) * 4;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        f32x4 nq[8];
+        if (g < 2) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) nq[q] = w3f[((g + 1) * 8 + q) * 64 + lane];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int kq = g * 8 + q;  // k = 8*kq + kh + s; tap kk = k / 64, channel = k % 64
+            const int kk = (kq * 8) / C, ci = (kq * 8) % C;
+            const f32x4 af = *reinterpret_cast<const f32x4*>(Xw + (ar + kk) * LDX + ci + kh);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bq[q][s], acc1, 0, 0, 0);
+        }
+        if (g < 2) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) bq[q] = nq[q];
+        }
+    }
+    f32x4 b1q[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) b1q[q] = w1f[q * 64 + lane];
+    // epilogue 1: ELU(h + b3) over the consumed slab (the wave's own LDS; reads precede writes in order)
+    {
+        const float bias = p.b3[lane & 31];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            Hw[row * LDH + (lane & 31)] = elu_fast(acc1[r] + bias);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    // ---- GEMM2: y[32][64] = h . W1^T (K = 32), 2 column tiles
+    f32x16 acc2[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
+#pragma unroll
+    for (int kq = 0; kq < 4; ++kq) {
+        const f32x4 af = *reinterpret_cast<const f32x4*>(Hw + ar * LDH + kq * 8 + kh);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], b1q[j * 4 + kq][s], acc2[j], 0, 0, 0);
+    }
+    // epilogue 2: y = ELU(x0 + (acc + b1)); x0 (the identity skip) recomputed from the audio window
+    float* __restrict__ yb = p.y + (long long)b * T * C;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int col = j * 32 + (lane & 31);
+        const float bias = p.b1[col];
+        float wc[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) wc[k] = p.w0[col * 7 + k];
+        const float bc = p.b0[col];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            float x0 = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) x0 = fmaf(wc[k], Aw[row + 2 + k], x0);
+            x0 = x0 + bc;
+            if (r0 + row < T) yb[(r0 + row) * C + col] = elu_fast(x0 + (acc2[j][r] + bias));
+        }
+    }
+}
+
 template <int C, int BM, bool WINDOW, bool FIRST, int W1M, int W1N, int W2M, int W2N, int NP>
 static hipError_t run_res(const ResArgs& a, hipStream_t s, const char** kname) {
     static char name[160];
@@ -321,6 +446,16 @@ hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** 
     if (a.T <= 0 || a.batch <= 0) return hipErrorInvalidValue;
     switch (C) {
         case 64:
+            if (a.audio && a.w3frag && a.w1frag) {
+                static const char* nm = "mimi::resblock0_wave_kernel(mimi::ResArgs)";
+                if (kname) *kname = nm;
+                ResArgs f = a;
+                f.w3 = a.w3frag;
+                f.w1 = a.w1frag;
+                hipLaunchKernelGGL(resblock0_wave_kernel, dim3((unsigned)((a.T + 127) / 128), a.batch), dim3(256), 0, s,
+                                   f);
+                return hipGetLastError();
+            }
             if (a.audio) return run_res<64, 128, true, true, 4, 1, 4, 1, 64>(a, s, kname);
             return run_res<64, 128, true, false, 4, 1, 4, 1, 64>(a, s, kname);
         case 128: return run_res<128, 64, true, false, 2, 2, 2, 2, 128>(a, s, kname);
