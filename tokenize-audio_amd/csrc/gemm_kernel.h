@@ -266,20 +266,24 @@ __device__ __forceinline__ void mma_split(f32x16 (&acc)[TM][TN], const bf16x8 (&
 template <int BM, int BN, int WM, int WN, int NS, bool ELU_IN, int PAD, int EPI, int TAG>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_bf16x_kernel(GemmArgs p) {
     constexpr int NT = WM * WN * 64;
+    constexpr int NW = WM * WN;
     constexpr int BK = 32;
-    constexpr int LDB = BK + 8;  // bf16 per LDS row: 80 B stride keeps ds_read_b128 fragments conflict-free
+    constexpr int LDB = BK + 8;  // A image: bf16 per row (80 B stride keeps ds_read_b128 conflict-free)
     constexpr int TM = BM / WM / 32;
     constexpr int TN = BN / WN / 32;
-    constexpr int A_F4 = BM * (BK / 4) / NT;      // fp32 float4 per thread
-    constexpr int B_C = NS * BN * (BK / 8) / NT;  // 16-byte bf16 chunks per thread
+    constexpr int A_F4 = BM * (BK / 4) / NT;  // fp32 float4 per thread
+    constexpr int BPL = BN * BK;              // B image plane: [BN][32] bf16, 16-B chunks XOR-swizzled
+    constexpr int BCH = NS * BN / 16;         // 1 KB LDS-DMA pieces per K slice
     static_assert(NS == 2 || NS == 3, "planes");
     static_assert(TM >= 1 && TN >= 1, "tile");
-    static_assert(A_F4 * NT == BM * (BK / 4) && B_C * NT == NS * BN * (BK / 8), "loader");
+    static_assert(A_F4 * NT == BM * (BK / 4), "loader");
     static_assert(EPI != EPI_ROPE || (TN % 2 == 0), "rope pairs need even TN");
 
-    __shared__ __attribute__((aligned(16))) __bf16 lds[NS * (BM + BN) * LDB];
-    __bf16* As = lds;                 // plane p at As + p*BM*LDB
-    __bf16* Bs = lds + NS * BM * LDB; // plane p at Bs + p*BN*LDB
+    // A: activations split in registers, written as NS padded planes; B: weight planes streamed by LDS-DMA
+    // (global_load_lds, no VGPRs, no ds_write) into a double-buffered swizzled image.
+    __shared__ __attribute__((aligned(16))) __bf16 lds[NS * BM * LDB + 2 * NS * BPL];
+    __bf16* As = lds;
+    __bf16* Bs0 = lds + NS * BM * LDB;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -293,70 +297,30 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_bf16x_kernel(GemmArgs p) {
     const float* __restrict__ Ab = p.A + (long long)b * p.a_bstride;
     const __bf16* __restrict__ Wp = reinterpret_cast<const __bf16*>(p.Wsplit);
 
+    const int a_len = (int)p.a_len;
+    int aoff[A_F4];
+    bool aok[A_F4];
+#pragma unroll
+    for (int i = 0; i < A_F4; ++i) {
+        const int idx = tid + i * NT;
+        const int m = m0 + (idx >> 3);
+        aok[i] = m < M;
+        aoff[i] = (int)(p.a_off + (long long)m * p.a_rs) + (idx & 7) * 4;
+    }
+    // this lane's LDS-DMA source rows: piece j = wave + q*NW covers 16 rows of one plane
+    constexpr int NQ = (BCH + NW - 1) / NW;
+    int bsrc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int j = wave + q * NW;
+        const int pl = j / (BN / 16), rb = j % (BN / 16);
+        const int row = rb * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ ((row >> 2) & 3);  // logical 16-B chunk stored at physical chunk lane&3
+        int n = n0 + row;
+        n = n < N ? n : N - 1;  // rows past N only feed columns that are never stored
+        bsrc[q] = (pl * N + n) * K + c * 8;
+    }
     f32x4 ra[A_F4];
-    uint4 rb[B_C];
-    auto gload = [&](int k0) {
-#pragma unroll
-        for (int i = 0; i < A_F4; ++i) {
-            const int idx = tid + i * NT;
-            const int r = idx >> 3;
-            const int c = (idx & 7) * 4;
-            const int m = m0 + r;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (m < M) {
-                long long e = p.a_off + (long long)m * p.a_rs + k0 + c;
-                if (PAD == PAD_ZERO) {
-                    if (e >= 0 && e < p.a_len) v = *reinterpret_cast<const f32x4*>(Ab + e);
-                } else {
-                    const long long cin = p.a_cin;
-                    long long t = e >= 0 ? e / cin : -((-e + cin - 1) / cin);
-                    const long long ch = e - t * cin;
-                    const long long tmax = p.a_len / cin - 1;
-                    t = t < 0 ? 0 : (t > tmax ? tmax : t);
-                    v = *reinterpret_cast<const f32x4*>(Ab + t * cin + ch);
-                }
-            }
-            ra[i] = v;
-        }
-#pragma unroll
-        for (int i = 0; i < B_C; ++i) {
-            const int idx = tid + i * NT;
-            const int pl = idx / (BN * 4);
-            const int rem = idx % (BN * 4);
-            const int r = rem >> 2;
-            const int c = (rem & 3) * 8;
-            const int n = n0 + r;
-            uint4 v = {0u, 0u, 0u, 0u};
-            if (n < N) v = *reinterpret_cast<const uint4*>(Wp + ((long long)pl * N + n) * K + k0 + c);
-            rb[i] = v;
-        }
-    };
-    auto sstore = [&]() {
-#pragma unroll
-        for (int i = 0; i < A_F4; ++i) {
-            const int idx = tid + i * NT;
-            const int r = idx >> 3;
-            const int c = (idx & 7) * 4;
-            f32x4 v = ra[i];
-            if (ELU_IN) {
-                v.x = elu1(v.x); v.y = elu1(v.y); v.z = elu1(v.z); v.w = elu1(v.w);
-            }
-            bf16x4 h[NS];
-            split_bf16x4<NS>(v, h);
-#pragma unroll
-            for (int pl = 0; pl < NS; ++pl) *reinterpret_cast<bf16x4*>(As + pl * BM * LDB + r * LDB + c) = h[pl];
-        }
-#pragma unroll
-        for (int i = 0; i < B_C; ++i) {
-            const int idx = tid + i * NT;
-            const int pl = idx / (BN * 4);
-            const int rem = idx % (BN * 4);
-            const int r = rem >> 2;
-            const int c = (rem & 3) * 8;
-            *reinterpret_cast<uint4*>(Bs + pl * BN * LDB + r * LDB + c) = rb[i];
-        }
-    };
-
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -370,11 +334,61 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_bf16x_kernel(GemmArgs p) {
     const int brow = wn * TN * 32 + (lane & 31);
     const int kh = (lane >> 5) * 8;
 
-    gload(0);
-    sstore();
+#define MIMI_SPLIT_LOAD_A(k0)                                                                  \
+    _Pragma("unroll") for (int i = 0; i < A_F4; ++i) {                                         \
+        const int e = aoff[i] + (k0);                                                          \
+        f32x4 v;                                                                               \
+        if (PAD == PAD_ZERO) {                                                                 \
+            const bool ok = aok[i] && e >= 0 && e < a_len;                                     \
+            v = *reinterpret_cast<const f32x4*>(Ab + (ok ? e : 0));                            \
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};                                              \
+            v = ok ? v : z;                                                                    \
+        } else {                                                                               \
+            const int cin = p.a_cin;                                                           \
+            int t = e >= 0 ? e / cin : -((-e + cin - 1) / cin);                                \
+            const int ch = e - t * cin;                                                        \
+            const int tmax = a_len / cin - 1;                                                  \
+            t = t < 0 ? 0 : (t > tmax ? tmax : t);                                             \
+            v = *reinterpret_cast<const f32x4*>(Ab + t * cin + ch);                            \
+        }                                                                                      \
+        ra[i] = v;                                                                             \
+    }
+#define MIMI_SPLIT_DMA_B(k0, buf)                                                              \
+    _Pragma("unroll") for (int q = 0; q < NQ; ++q) {                                           \
+        const int j = wave + q * NW;                                                           \
+        if (j < BCH) {                                                                         \
+            const int pl = j / (BN / 16), rb = j % (BN / 16);                                  \
+            __bf16* dst = Bs0 + (buf) * NS * BPL + pl * BPL + rb * 16 * BK;                    \
+            __builtin_amdgcn_global_load_lds((const void*)(Wp + bsrc[q] + (k0)),               \
+                (__attribute__((address_space(3))) void*)dst, 16, 0, 0);                       \
+        }                                                                                      \
+    }
+#define MIMI_SPLIT_STORE_A()                                                                   \
+    _Pragma("unroll") for (int i = 0; i < A_F4; ++i) {                                         \
+        const int idx = tid + i * NT;                                                          \
+        f32x4 v = ra[i];                                                                       \
+        if (ELU_IN) {                                                                          \
+            v.x = elu1(v.x); v.y = elu1(v.y); v.z = elu1(v.z); v.w = elu1(v.w);                \
+        }                                                                                      \
+        bf16x4 h[NS];                                                                          \
+        split_bf16x4<NS>(v, h);                                                                \
+        __bf16* dst = As + (idx >> 3) * LDB + (idx & 7) * 4;                                   \
+        _Pragma("unroll") for (int pl = 0; pl < NS; ++pl)                                      \
+            *reinterpret_cast<bf16x4*>(dst + pl * BM * LDB) = h[pl];                           \
+    }
+
+    MIMI_SPLIT_LOAD_A(0)
+    MIMI_SPLIT_DMA_B(0, 0)
+    MIMI_SPLIT_STORE_A()
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int kt = 0; kt < KT; ++kt) {
-        if (kt + 1 < KT) gload((kt + 1) * BK);
+        const int cur = kt & 1;
+        if (kt + 1 < KT) {
+            MIMI_SPLIT_LOAD_A((kt + 1) * BK)
+            MIMI_SPLIT_DMA_B((kt + 1) * BK, cur ^ 1)
+        }
+        const __bf16* Bs = Bs0 + cur * NS * BPL;
 #pragma unroll
         for (int kk = 0; kk < BK / 16; ++kk) {
             bf16x8 af[NS][TM], bf[NS][TN];
@@ -384,17 +398,25 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_bf16x_kernel(GemmArgs p) {
                 for (int i = 0; i < TM; ++i)
                     af[pl][i] = *reinterpret_cast<const bf16x8*>(As + pl * BM * LDB + (arow + i * 32) * LDB + kk * 16 + kh);
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    bf[pl][j] = *reinterpret_cast<const bf16x8*>(Bs + pl * BN * LDB + (brow + j * 32) * LDB + kk * 16 + kh);
+                for (int j = 0; j < TN; ++j) {
+                    const int row = brow + j * 32;
+                    const int phys = ((kk * 2 + (lane >> 5)) ^ ((row >> 2) & 3)) * 8;
+                    bf[pl][j] = *reinterpret_cast<const bf16x8*>(Bs + pl * BPL + row * BK + phys);
+                }
             }
             mma_split<NS, TM, TN>(acc, af, bf);
         }
         if (kt + 1 < KT) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            sstore();
+            MIMI_SPLIT_STORE_A()
             __syncthreads();
         }
     }
+#undef MIMI_SPLIT_LOAD_A
+#undef MIMI_SPLIT_DMA_B
+#undef MIMI_SPLIT_STORE_A
+
     // ---- epilogue: lane holds col (lane&31), rows (r&3) + 8*(r>>2) + 4*(lane>>5) of each 32x32 tile
     float* __restrict__ Cb = p.C + (long long)b * p.c_bstride;
     const float* __restrict__ Rb = p.R ? p.R + (long long)b * p.c_bstride : nullptr;
