@@ -11,8 +11,8 @@ per-GPU work is fixed as N grows ("weak").  The timed region is bracketed by bar
 max over ranks is reported.  Rank 0 prints ONE JSON line.
 
 roofline: per-kernel device time from HIP events recorded by the engine on its launch stream during the
-timed steps, aggregated per kernel symbol; the dominant kernel's algorithmic FLOPs / its time vs the fp32
-MFMA peak.  cpu_baseline: the oracle (torch CPU restatement of MimiModel.encode) on a bounded sample.
+timed steps, aggregated per kernel symbol; the dominant kernel's algorithmic FLOPs / its time vs the MFMA
+peak of the arithmetic it runs on (see ``mfma_peak_for``).  cpu_baseline: the oracle (torch CPU restatement of MimiModel.encode) on a bounded sample.
 """
 import argparse
 import json
@@ -27,6 +27,20 @@ for _p in (os.path.join(ROOT, "tokenize-audio_amd"), ROOT):
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 MFMA/vector peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec
+BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak
+
+
+def mfma_peak_for(kernel: str):
+    """Peak that bounds a GEMM kernel, in fp32-equivalent TFLOP/s of the algorithmic (fp32) FLOPs it does.
+
+    fp32 kernels run on v_mfma_f32_32x32x2_f32: 157.3 TF.  The split-bf16 kernels compute the same fp32 GEMM
+    as P bf16 products per fp32 multiply-add (NS = 3 planes -> 6 products, NS = 2 -> 3) on the dense bf16
+    MFMA, so their ceiling is 2.5 PF / P (416.7 TF for bf16x6, 833.3 TF for bf16x3)."""
+    if "gemm_bf16x_kernel<" in kernel:
+        ns = int(kernel.split("<", 1)[1].split(",")[4])
+        products = {3: 6, 2: 3}[ns]
+        return BF16_PEAK_TFLOPS / products, f"bf16 MFMA dense peak / {products} products (split-bf16, {ns} planes)"
+    return FP32_PEAK_TFLOPS, "fp32 MFMA peak"
 
 
 def parse():
@@ -182,22 +196,24 @@ def main():
         gemm_like = dom["flops"] > 0
         if gemm_like:
             achieved = dom["flops"] / dom["launches"] / t_launch / 1e12
-            roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / FP32_PEAK_TFLOPS, 4)}
+            peak, peak_note = mfma_peak_for(dom_name)
+            roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                    "frac": round(achieved / peak, 4), "peak_basis": peak_note}
         else:
             achieved = dom["bytes"] / dom["launches"] / t_launch / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4)}
-        traffic = None
+        traffic, traffic_src = None, None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 pmc = json.load(f)
             k = pmc.get("kernels", {}).get(dom_name, {})
             if "traffic_bytes" in k:
-                traffic = {"bytes_per_launch": round(k["traffic_bytes"]), "source": f"profiles/{pmc['tag']}_pmc_summary.json",
-                           "fetch_bytes": round(k["fetch_bytes"]), "write_bytes": round(k["write_bytes"])}
-        roof.update({"traffic": traffic, "kernel": dom_name, "stages": dom["stages"],
+                traffic = round(k["traffic_bytes"])
+                traffic_src = {"source": f"profiles/{pmc['tag']}_pmc_summary.json", "unit": "bytes per launch",
+                               "fetch_bytes": round(k["fetch_bytes"]), "write_bytes": round(k["write_bytes"])}
+        roof.update({"traffic": traffic, "traffic_detail": traffic_src, "kernel": dom_name, "stages": dom["stages"],
                      "avg_launch_ms": round(1000 * t_launch, 4), "launches": dom["launches"],
                      "algorithmic_per_launch": dom["flops"] / dom["launches"] if gemm_like
                      else dom["bytes"] / dom["launches"]})

@@ -741,24 +741,22 @@ extern "C" int mimi_finalize(mimi_engine* e) {
 // encode
 // ------------------------------------------------------------------------------------------------
 struct Workspace {
-    float *x, *h, *y;              // SEANet ping-pong
+    float *x, *y;                  // SEANet ping-pong (the residual blocks keep their hidden tile on chip)
     float *t0, *t1, *qkv, *att, *ff;  // transformer
     float *dsout, *proj;
 };
 
 static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspace* w) {
     const mimi_config& c = e->cfg;
-    size_t xmax = 0, hmax = 0;
+    size_t xmax = 0;
     int C = c.num_filters;
     for (int s = 0; s < c.num_ratios; ++s) {
         xmax = std::max(xmax, (size_t)p.T[s] * C);
-        hmax = std::max(hmax, (size_t)p.T[s] * (C / c.compress));
         C *= 2;
     }
     xmax = std::max(xmax, (size_t)p.T[c.num_ratios] * C);
     const size_t T = (size_t)p.frames25, Hd = (size_t)c.hidden_size;
     const size_t sizes[] = {xmax * B,
-                            hmax * B,
                             xmax * B,
                             T * Hd * B,
                             T * Hd * B,
@@ -768,7 +766,7 @@ static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspa
                             (size_t)p.frames12 * Hd * B,
                             (size_t)p.frames12 * 2 * c.vq_hidden_dim * B};
     size_t off = 0;
-    float** ptrs[] = {&w->x, &w->h, &w->y, &w->t0, &w->t1, &w->qkv, &w->att, &w->ff, &w->dsout, &w->proj};
+    float** ptrs[] = {&w->x, &w->y, &w->t0, &w->t1, &w->qkv, &w->att, &w->ff, &w->dsout, &w->proj};
     char* base = reinterpret_cast<char*>(e->ws);
     for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); ++i) {
         if (w) *ptrs[i] = reinterpret_cast<float*>(base + off);
