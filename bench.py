@@ -36,7 +36,7 @@ def mfma_peak_for(kernel: str):
     fp32 kernels run on v_mfma_f32_32x32x2_f32: 157.3 TF.  The split-bf16 kernels compute the same fp32 GEMM
     as P bf16 products per fp32 multiply-add (NS = 3 planes -> 6 products, NS = 2 -> 3) on the dense bf16
     MFMA, so their ceiling is 2.5 PF / P (416.7 TF for bf16x6, 833.3 TF for bf16x3)."""
-    if "gemm_bf16x_kernel<" in kernel:
+    if "gemm_bf16x_kernel<" in kernel or "gemm_planes_kernel<" in kernel:
         ns = int(kernel.split("<", 1)[1].split(",")[4])
         products = {3: 6, 2: 3}[ns]
         return BF16_PEAK_TFLOPS / products, f"bf16 MFMA dense peak / {products} products (split-bf16, {ns} planes)"

@@ -746,23 +746,44 @@ struct Workspace {
     float *dsout, *proj;
 };
 
+// Planes of the split-bf16 path: activations consumed only by GEMMs (resblock outputs, the last down conv's
+// output, LayerNorm / attention / GELU outputs) are stored as NS bf16 planes instead of fp32 so the GEMMs
+// only move bytes (gemm_planes.h).  0 = fp32 activations (f32 mode, or a clip so long that a batch item's
+// plane exceeds the 2 GiB buffer-resource range).
+static int act_planes(const mimi_engine* e, const StagePlan& p) {
+    const int ns = e->precision == PREC_BF16X6 ? 3 : e->precision == PREC_BF16X3 ? 2 : 0;
+    if (ns == 0) return 0;
+    const mimi_config& c = e->cfg;
+    int C = c.num_filters;
+    for (int si = 0; si <= c.num_ratios; ++si) {
+        if ((double)p.T[si] * C * 2 * 2 >= 2147483647.0) return 0;  // k*Cin span of the last row included
+        C *= 2;
+    }
+    if ((double)p.frames25 * c.intermediate_size * 2 >= 2147483647.0) return 0;
+    return ns;
+}
+
 static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspace* w) {
     const mimi_config& c = e->cfg;
-    size_t xmax = 0;
+    const int ns = act_planes(e, p);
+    // a plane-format buffer of n values takes ns * n bf16 = ns * n / 2 floats
+    auto act = [&](size_t n) { return ns ? (n * ns + 1) / 2 : n; };
+    size_t xmax = 0, ymax = 0;
     int C = c.num_filters;
     for (int s = 0; s < c.num_ratios; ++s) {
         xmax = std::max(xmax, (size_t)p.T[s] * C);
+        ymax = std::max(ymax, (size_t)p.T[s] * C);
         C *= 2;
     }
-    xmax = std::max(xmax, (size_t)p.T[c.num_ratios] * C);
+    xmax = std::max(xmax, act((size_t)p.T[c.num_ratios] * C));  // last down conv's (planes) output
     const size_t T = (size_t)p.frames25, Hd = (size_t)c.hidden_size;
     const size_t sizes[] = {xmax * B,
-                            xmax * B,
+                            act(ymax * B),
                             T * Hd * B,
-                            T * Hd * B,
+                            act(T * Hd * B),
                             T * 3 * Hd * B,
-                            T * Hd * B,
-                            T * (size_t)c.intermediate_size * B,
+                            act(T * Hd * B),
+                            act(T * (size_t)c.intermediate_size * B),
                             (size_t)p.frames12 * Hd * B,
                             (size_t)p.frames12 * 2 * c.vq_hidden_dim * B};
     size_t off = 0;
@@ -871,6 +892,31 @@ static int save_tap(mimi_engine* e, const char* name, const float* src, int64_t 
     return MIMI_OK;
 }
 
+// tap of a plane-format activation (materialised as fp32 only when taps are on)
+static int save_tap_planes(mimi_engine* e, const char* name, const void* planes, int ns, int64_t b, int64_t t,
+                           int64_t ch, hipStream_t s) {
+    if (!e->taps) return MIMI_OK;
+    if (ns == 0) return save_tap(e, name, reinterpret_cast<const float*>(planes), b, t, ch, s);
+    auto& tp = e->tapmap[name];
+    const size_t n = (size_t)(b * t * ch);
+    if (tp.cap < n) {
+        if (tp.d) HIP_TRY(hipFree(tp.d));
+        HIP_TRY(hipMalloc(&tp.d, n * 4));
+        tp.cap = n;
+    }
+    HIP_TRY(launch_planes_to_f32(planes, (long long)n, ns, tp.d, (long long)n, s));
+    tp.dims[0] = b;
+    tp.dims[1] = t;
+    tp.dims[2] = ch;
+    return MIMI_OK;
+}
+
+// A operand of a GEMM read from plane-format activations (plane stride = the activation's element count)
+static void planes_in(GemmArgs& a, const void* planes, long long n) {
+    a.Ap = planes;
+    a.a_pstride = n;
+}
+
 static GemmArgs conv_args(const DevConv& cv, const float* in, int64_t Tin, float* out, int64_t Tout, int B) {
     GemmArgs a{};
     a.A = in;
@@ -945,6 +991,7 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
     if (rc) return rc;
     ws_layout(e, B, p, &w);
     if ((rc = ensure_rope(e, p.frames25))) return rc;
+    const int ns = act_planes(e, p);  // 0: fp32 activations; 2/3: plane-format GEMM inputs
     Recorder rec{e, s};
     const char* kname = "?";
     HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));
@@ -983,6 +1030,9 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
         ra.w1 = e->res1[si].w;
         ra.b1 = e->res1[si].b;
         ra.y = w.y;
+        ra.yp = w.y;
+        ra.y_pstride = (long long)B * T * C;
+        ra.yns = ns;
         LAUNCH_TRY(launch_resblock(C, ra, s, &kname), "resblock");
         snprintf(nm, sizeof nm, "res_s%d", si);
         {
@@ -992,19 +1042,28 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
             rec.mark(nm, fl, by, kname);
         }
         snprintf(nm, sizeof nm, "res%d_elu", si);
-        if ((rc = save_tap(e, nm, w.y, B, T, C, s))) return rc;
+        if ((rc = save_tap_planes(e, nm, w.y, ns, B, T, C, s))) return rc;
         const bool last = si == c.num_ratios - 1;
         GemmArgs ad = conv_args(e->down[si], w.y, T, w.x, p.T[si + 1], B);
+        if (ns) {
+            planes_in(ad, w.y, (long long)B * T * C);
+            if (last) {  // only the final conv reads it: planes out
+                ad.Cp = w.x;
+                ad.c_pstride = (long long)B * p.T[si + 1] * 2 * C;
+                ad.C = nullptr;
+            }
+        }
         LAUNCH_TRY(launch_gemm(last ? ROLE_DOWN_ELU : ROLE_DOWN, ad, s, &kname, e->precision), "down");
         snprintf(nm, sizeof nm, "down_s%d", si);
         rec.mark(nm, gemm_flops(ad), gemm_bytes(ad, false), kname);
         snprintf(nm, sizeof nm, last ? "down%d_elu" : "down%d", si);
-        if ((rc = save_tap(e, nm, w.x, B, p.T[si + 1], 2 * C, s))) return rc;
+        if ((rc = save_tap_planes(e, nm, w.x, last ? ns : 0, B, p.T[si + 1], 2 * C, s))) return rc;
         C *= 2;
     }
     const int64_t T = p.frames25;
     const int Hd = c.hidden_size;
     GemmArgs af = conv_args(e->final_conv, w.x, p.T[c.num_ratios], w.t0, T, B);
+    if (ns) planes_in(af, w.x, (long long)B * p.T[c.num_ratios] * C);
     LAUNCH_TRY(launch_gemm(ROLE_FINAL, af, s, &kname, e->precision), "final");
     rec.mark("final", gemm_flops(af), gemm_bytes(af, false), kname);
     if ((rc = save_tap(e, "encoder", w.t0, B, T, Hd, s))) return rc;
@@ -1017,7 +1076,8 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
     att_flops *= (double)B * H;
     for (int l = 0; l < c.num_hidden_layers; ++l) {
         const DevXfmr& x = e->xf[l];
-        LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s), "ln1");
+        const long long nact = rows * Hd;
+        LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns), "ln1");
         rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512>");
         GemmArgs aq = linear_args(w.t1, T, Hd, x.wqkv, 3 * H * Dh, w.qkv);
         aq.Wsplit = x.wqkv_s;
@@ -1027,27 +1087,37 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
         aq.rope_cos = e->rope_cos;
         aq.rope_sin = e->rope_sin;
         aq.rope_cols = 2 * H * Dh;
+        if (ns) planes_in(aq, w.t1, nact);
         LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, e->precision), "qkv");
         rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
-        LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh), s),
+        LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh), s,
+                                    w.att, nact, ns),
                    "attention");
         rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4, "mimi::attention_kernel");
         GemmArgs ao = linear_args(w.att, rows, H * Dh, x.wo, Hd, w.t0);
         ao.Wsplit = x.wo_s;
         ao.R = w.t0;
         ao.scale = x.ls1;
+        if (ns) planes_in(ao, w.att, nact);
         LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, e->precision), "o_proj");
         rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
-        LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s), "ln2");
+        LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns), "ln2");
         rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512>");
         GemmArgs a1 = linear_args(w.t1, rows, Hd, x.w1, c.intermediate_size, w.ff);
         a1.Wsplit = x.w1_s;
+        if (ns) {
+            planes_in(a1, w.t1, nact);
+            a1.Cp = w.ff;  // only fc2 reads it: planes out
+            a1.c_pstride = rows * c.intermediate_size;
+            a1.C = nullptr;
+        }
         LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, e->precision), "fc1");
         rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
         GemmArgs a2 = linear_args(w.ff, rows, c.intermediate_size, x.w2, Hd, w.t0);
         a2.Wsplit = x.w2_s;
         a2.R = w.t0;
         a2.scale = x.ls2;
+        if (ns) planes_in(a2, w.ff, rows * (long long)c.intermediate_size);
         LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname, e->precision), "fc2");
         rec.mark("fc2", gemm_flops(a2), gemm_bytes(a2, true), kname);
         snprintf(nm, sizeof nm, "xfmr%d", l);

@@ -17,7 +17,7 @@
 #include <cstdio>
 
 
-#include "gemm_kernel.h"
+#include "gemm_planes.h"
 
 namespace mimi {
 
@@ -59,6 +59,36 @@ static hipError_t run_split(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int BM, int BN, int WM, int WN, int NS, int ST, int EPI, int OUTP, int TAG>
+static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
+    static char name[160];
+    if (!name[0])
+        snprintf(name, sizeof(name), "mimi::gemm_planes_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d>", BM, BN, WM, WN, NS,
+                 ST, EPI, OUTP, TAG);
+    g_last_kernel = name;
+    if (a.K % 32 != 0 || !a.Wsplit || !a.Ap || (OUTP && !a.Cp) || (!OUTP && !a.C)) return hipErrorInvalidValue;
+    if (a.a_len * 2 > 0x7fffffffLL) return hipErrorInvalidValue;  // buffer-resource byte offsets are 32-bit
+    const long long nwg = (long long)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.batch;
+    if (nwg > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG>), dim3((unsigned)nwg),
+                       dim3(WM * WN * 64), 0, s, a);
+    return hipGetLastError();
+}
+
+// Tiles of the planes kernel (tools/gemm_bench.hip, profiles/r1_gemm_bench_planes.log): 256x128 (8 waves,
+// 2 stages at NS = 3 / 3 stages at NS = 2, 144 KiB LDS) where M x N is large, 128x128 (4 waves, 3 stages)
+// where a 256-row tile would leave CUs idle (final conv, o_proj, fc2: M = B*250 rows, N = 512).
+template <int EPI, int OUTP3, int OUTP2, int TAG>
+static hipError_t run_planes_big(const GemmArgs& a, hipStream_t s, int prec) {
+    if (prec == PREC_BF16X6) return run_planes<256, 128, 4, 2, 3, 2, EPI, OUTP3, TAG>(a, s);
+    return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP2, TAG>(a, s);
+}
+template <int EPI, int TAG>
+static hipError_t run_planes_small(const GemmArgs& a, hipStream_t s, int prec) {
+    if (prec == PREC_BF16X6) return run_planes<128, 128, 2, 2, 3, 3, EPI, 0, TAG>(a, s);
+    return run_planes<128, 128, 2, 2, 2, 3, EPI, 0, TAG>(a, s);
+}
+
 template <bool ELU_IN, int PAD, int EPI, int TAG>
 static hipError_t run_prec(const GemmArgs& a, hipStream_t s, int prec);
 
@@ -86,6 +116,7 @@ static hipError_t run_prec(const GemmArgs& a, hipStream_t s, int prec) {
 hipError_t launch_gemm(int role, const GemmArgs& a, hipStream_t s, const char** kname, int precision) {
     if (a.K % 32 != 0 || a.a_cin % 4 != 0 || a.a_rs % 4 != 0 || a.M <= 0 || a.N <= 0 || a.batch <= 0)
         return hipErrorInvalidValue;
+    if (a.Ap && (a.a_cin % 8 != 0 || a.a_rs % 8 != 0 || a.a_off % 8 != 0)) return hipErrorInvalidValue;  // 16-B chunks
     g_last_kernel = nullptr;
     g_prec = precision;
     hipError_t e = dispatch(role, a, s);
@@ -93,7 +124,23 @@ hipError_t launch_gemm(int role, const GemmArgs& a, hipStream_t s, const char** 
     return e;
 }
 
+static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
+    const int prec = g_prec;
+    if (prec != PREC_BF16X6 && prec != PREC_BF16X3) return hipErrorInvalidValue;
+    switch (role) {
+        case ROLE_DOWN: return run_planes_big<EPI_BIAS, 0, 0, 2>(a, s, prec);
+        case ROLE_DOWN_ELU: return run_planes_big<EPI_BIAS_ELU, 3, 2, 3>(a, s, prec);  // planes out: final conv
+        case ROLE_FINAL: return run_planes_small<EPI_BIAS_OUT, 4>(a, s, prec);
+        case ROLE_QKV: return run_planes_big<EPI_ROPE, 0, 0, 5>(a, s, prec);
+        case ROLE_OPROJ: return run_planes_small<EPI_SCALE_RES, 6>(a, s, prec);
+        case ROLE_FC1: return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);  // planes out: fc2
+        case ROLE_FC2: return run_planes_small<EPI_SCALE_RES, 8>(a, s, prec);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 static hipError_t dispatch(int role, const GemmArgs& a, hipStream_t s) {
+    if (a.Ap) return dispatch_planes(role, a, s);
     switch (role) {
         case ROLE_DOWN: return run_prec<false, PAD_ZERO, EPI_BIAS, 2>(a, s, g_prec);
         case ROLE_DOWN_ELU: return run_prec<false, PAD_ZERO, EPI_BIAS_ELU, 3>(a, s, g_prec);

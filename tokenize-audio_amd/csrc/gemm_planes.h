@@ -1,0 +1,240 @@
+// Split-bf16 GEMM over pre-split operands ("planes"): both A (activations) and W are stored in HBM as NS
+// bf16 planes (x = x0 + x1 [+ x2], see gemm_kernel.h), so the main loop moves bytes only with LDS-DMA and
+// does no VALU conversion work.  Included by gemm.hip and tools/gemm_bench.hip.
+//
+// Structure (MI355X_MICROARCH.md / cdna_hip_programming.md "pipelining across barriers"):
+//   * one LDS array holding a STAGES-deep ring of {A planes, B planes} images; per stage the workgroup
+//     issues (NS*BM + NS*BN)/16 1-KiB `buffer_load_dwordx4 ... lds` / `global_load_lds_dwordx4` pieces,
+//     split evenly over the waves;
+//   * per K step: counted `s_waitcnt vmcnt(N)` (never 0 while later stages are in flight), ONE barrier,
+//     refill of the stage consumed in the previous step, then the MFMAs of this step;
+//   * each image row is BK = 32 bf16 = 64 B = four 16-B chunks, stored at chunk (c ^ ((row >> 2) & 3)) so the
+//     MFMA fragment reads (ds_read_b128, 16 rows x one chunk per quarter-wave) are conflict-free; the swizzle
+//     is applied on the SOURCE address of each DMA lane (the LDS destination of a DMA is lane-linear);
+//   * A rows come from the implicit im2col view of a channels-last activation (row m = span
+//     a_off + m*a_rs); causal zero padding and the right edge come from the buffer resource's range check
+//     (an out-of-range offset, including a negative one, loads 0) -- no per-element branches;
+//   * workgroup -> tile map is XCD-aware: the 8 XCDs each take a contiguous run of the (m, n) tile order
+//     with n fastest, so the N tiles sharing an A tile hit the same L2.
+#pragma once
+#include "gemm_kernel.h"
+
+namespace mimi {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
+    const long long lim = bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)lim, 0x00020000);
+}
+#endif
+
+// (XCD-aware) linear workgroup index -> logical tile index; bijective for any count.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int STAGES, int EPI, int OUTP, int TAG>
+__global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
+#if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
+    constexpr int NW = WM * WN;
+    constexpr int BK = 32;
+    constexpr int TM = BM / WM / 32;
+    constexpr int TN = BN / WN / 32;
+    constexpr int APL = BM * BK, BPL = BN * BK;  // bf16 per plane image
+    constexpr int STG = NS * (APL + BPL);        // bf16 per stage
+    constexpr int APW = NS * BM / 16 / NW;       // A pieces per wave per stage
+    constexpr int BPW = NS * BN / 16 / NW;       // B pieces per wave per stage
+    constexpr int PPW = APW + BPW;
+    static_assert(APW * NW * 16 == NS * BM && BPW * NW * 16 == NS * BN, "pieces must split evenly over waves");
+    static_assert(STAGES >= 2 && STAGES <= 4, "stages");
+    static_assert(PPW * (STAGES - 2) <= 63, "vmcnt range");
+    static_assert(EPI != EPI_ROPE || (TN % 2 == 0), "rope pairs need even TN");
+
+    __shared__ __attribute__((aligned(16))) __bf16 lds[STAGES * STG];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps rsrc/LDS bases in SGPRs
+    const int wm = wave / WN;
+    const int wn = wave % WN;
+    const int M = p.M, N = p.N, K = p.K;
+    const int MT = (M + BM - 1) / BM, NTn = (N + BN - 1) / BN;
+    const int logical = xcd_remap(blockIdx.x, gridDim.x);
+    const int nt = logical % NTn;
+    const int rest = logical / NTn;
+    const int mt = rest % MT;
+    const int b = rest / MT;
+    const int m0 = mt * BM, n0 = nt * BN;
+
+    // ---- DMA sources for this lane (16 rows x 4 chunks per piece; lane -> row lane>>2, chunk lane&3)
+    const __bf16* __restrict__ Abase = reinterpret_cast<const __bf16*>(p.Ap) + (long long)b * p.a_bstride;
+    __amdgpu_buffer_rsrc_t arsrc[NS];
+#pragma unroll
+    for (int pl = 0; pl < NS; ++pl) arsrc[pl] = make_rsrc(Abase + (long long)pl * p.a_pstride, p.a_len * 2);
+    int aoff[APW];  // byte offset of this lane's chunk at k0 = 0 (may be negative: reads 0)
+#pragma unroll
+    for (int q = 0; q < APW; ++q) {
+        const int j = wave + q * NW;
+        const int rb = j % (BM / 16);
+        const int row = rb * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ ((row >> 2) & 3);
+        const int m = m0 + row;
+        const long long e = p.a_off + (long long)m * p.a_rs + c * 8;
+        aoff[q] = (m < M) ? (int)(e * 2) : -16;  // rows past M load 0 (never stored)
+    }
+    const __bf16* __restrict__ Wp = reinterpret_cast<const __bf16*>(p.Wsplit);
+    const __bf16* bsrc[BPW];
+#pragma unroll
+    for (int q = 0; q < BPW; ++q) {
+        const int j = wave + q * NW;
+        const int pl = j / (BN / 16), rb = j % (BN / 16);
+        const int row = rb * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ ((row >> 2) & 3);
+        int n = n0 + row;
+        n = n < N ? n : N - 1;  // rows past N only feed columns that are never stored
+        bsrc[q] = Wp + ((long long)pl * N + n) * K + c * 8;
+    }
+
+    auto issue = [&](int kt, int stage) {
+        __bf16* st = lds + stage * STG;
+        const int kb = kt * BK * 2;  // bytes
+#pragma unroll
+        for (int q = 0; q < APW; ++q) {
+            const int j = wave + q * NW;
+            const int pl = j / (BM / 16), rb = j % (BM / 16);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                arsrc[pl], (__attribute__((address_space(3))) void*)(st + pl * APL + rb * 16 * BK), 16,
+                aoff[q] + kb, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < BPW; ++q) {
+            const int j = wave + q * NW;
+            const int pl = j / (BN / 16), rb = j % (BN / 16);
+            __builtin_amdgcn_global_load_lds((const void*)(bsrc[q] + kt * BK),
+                                             (__attribute__((address_space(3))) void*)(st + NS * APL + pl * BPL +
+                                                                                        rb * 16 * BK),
+                                             16, 0, 0);
+        }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    const int KT = K / BK;
+    const int arow = wm * TM * 32 + (lane & 31);
+    const int brow = wn * TN * 32 + (lane & 31);
+    const int hsel = lane >> 5;
+
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+        if (s < KT) issue(s, s);
+
+    for (int kt = 0; kt < KT; ++kt) {
+        // retire this wave's pieces of stage kt; the later stages stay in flight
+        const int later = min(STAGES - 2, KT - 1 - kt);
+        if (STAGES >= 4 && later >= 2) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+        } else if (STAGES >= 3 && later >= 1) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        // the stage consumed in step kt-1 is free: refill it with step kt + STAGES - 1
+        if (kt + STAGES - 1 < KT) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+        const __bf16* As = lds + (kt % STAGES) * STG;
+        const __bf16* Bs = As + NS * APL;
+#pragma unroll
+        for (int kk = 0; kk < BK / 16; ++kk) {
+            bf16x8 af[NS][TM], bf[NS][TN];
+#pragma unroll
+            for (int pl = 0; pl < NS; ++pl) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int row = arow + i * 32;
+                    const int phys = ((kk * 2 + hsel) ^ ((row >> 2) & 3)) * 8;
+                    af[pl][i] = *reinterpret_cast<const bf16x8*>(As + pl * APL + row * BK + phys);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int row = brow + j * 32;
+                    const int phys = ((kk * 2 + hsel) ^ ((row >> 2) & 3)) * 8;
+                    bf[pl][j] = *reinterpret_cast<const bf16x8*>(Bs + pl * BPL + row * BK + phys);
+                }
+            }
+            mma_split<NS, TM, TN>(acc, af, bf);
+        }
+    }
+
+    // ---- epilogue: lane holds col (lane&31), rows (r&3) + 8*(r>>2) + 4*(lane>>5) of each 32x32 tile
+    float* __restrict__ Cb = p.C ? p.C + (long long)b * p.c_bstride : nullptr;
+    __bf16* __restrict__ Cpb = OUTP ? reinterpret_cast<__bf16*>(p.Cp) + (long long)b * p.c_bstride : nullptr;
+    const float* __restrict__ Rb = p.R ? p.R + (long long)b * p.c_bstride : nullptr;
+    const int rbase = m0 + wm * TM * 32 + 4 * hsel;
+    const int cbase = n0 + wn * TN * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = cbase + j * 32;
+            float bias = 0.0f, scale = 0.0f;
+            if (col < N) {
+                if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU || EPI == EPI_BIAS_RES_ELU || EPI == EPI_BIAS_OUT)
+                    bias = p.bias[col];
+                if (EPI == EPI_SCALE_RES) scale = p.scale[col];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
+                if (row >= M || col >= N) continue;
+                float v = acc[i][j][r];
+                const long long off = (long long)row * p.ldc + col;
+                if (EPI == EPI_BIAS || EPI == EPI_BIAS_OUT) {
+                    v = v + bias;
+                } else if (EPI == EPI_BIAS_ELU) {
+                    v = elu1(v + bias);
+                } else if (EPI == EPI_BIAS_RES_ELU) {
+                    v = elu1(Rb[off] + (v + bias));
+                } else if (EPI == EPI_GELU) {
+                    v = gelu_erf(v);
+                } else if (EPI == EPI_SCALE_RES) {
+                    v = Rb[off] + scale * v;
+                } else if (EPI == EPI_ROPE) {
+                    if (col < p.rope_cols) {
+                        const int d = col % 64;  // head_dim = 64: pairs (d, d + 32) sit in tiles j, j + 1
+                        const float c = p.rope_cos[(long long)row * 32 + (d & 31)];
+                        const float sn = p.rope_sin[(long long)row * 32 + (d & 31)];
+                        if ((j & 1) == 0) {
+                            const float x2 = acc[i][j + 1][r];
+                            v = v * c + (-x2) * sn;
+                        } else {
+                            const float x1 = acc[i][j - 1][r];
+                            v = v * c + x1 * sn;
+                        }
+                    }
+                }
+                if (OUTP) {
+                    float rem = v;
+#pragma unroll
+                    for (int pl = 0; pl < OUTP; ++pl) {
+                        const __bf16 h = (__bf16)rem;
+                        Cpb[pl * p.c_pstride + off] = h;
+                        rem = rem - (float)h;
+                    }
+                    if (Cb) Cb[off] = v;
+                } else {
+                    Cb[off] = v;
+                }
+            }
+        }
+    }
+#endif
+}
+
+}  // namespace mimi

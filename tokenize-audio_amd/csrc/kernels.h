@@ -22,6 +22,24 @@ __device__ __forceinline__ float elu_fast(float x) {
     return x > 0.0f ? x : n;
 }
 
+// Activation store in the consumer's format: fp32 (ns == 0) or ns bf16 planes x = x0 + x1 [+ x2] with
+// x_p = bf16(x - x0 - ... - x_{p-1}) (the split of gemm_kernel.h), plane p at planes + p * pstride.  The planes
+// feed gemm_planes_kernel, which then only moves bytes (gemm_planes.h).
+__device__ __forceinline__ void store_act(float* f32, void* planes, long long pstride, int ns, long long idx,
+                                          float v) {
+    if (ns == 0) {
+        f32[idx] = v;
+        return;
+    }
+    __bf16* pp = reinterpret_cast<__bf16*>(planes) + idx;
+    const __bf16 h0 = (__bf16)v;
+    pp[0] = h0;
+    const float r1 = v - (float)h0;
+    const __bf16 h1 = (__bf16)r1;
+    pp[pstride] = h1;
+    if (ns == 3) pp[2 * pstride] = (__bf16)(r1 - (float)h1);
+}
+
 // Epilogues of the implicit-GEMM conv / linear kernel.
 enum Epi : int {
     EPI_NONE = 0,          // C = acc                                  (input_proj, downsample)
@@ -49,6 +67,8 @@ struct GemmArgs {
     long long a_len;
     const float* W;       // fp32 [N][K]
     const void* Wsplit;   // bf16 planes [3][N][K] of W (x = x0 + x1 + x2), for the split-bf16 modes
+    const void* Ap;       // bf16 planes of A (gemm_planes_kernel): plane p at Ap + p*a_pstride, same indexing as A
+    long long a_pstride;
     int M, N, K;
     int batch;
     const float* bias;
@@ -60,6 +80,8 @@ struct GemmArgs {
     float* C;
     long long c_bstride;
     int ldc;
+    void* Cp;             // optional bf16 planes of the output (planes-out epilogues), plane stride c_pstride
+    long long c_pstride;
 };
 
 // Launch the GEMM for a given conv/linear role (the role picks tile shape and template flags).
@@ -98,6 +120,9 @@ struct ResArgs {
     const float* w1;  // [C][C/2]
     const float* b1;
     float* y;
+    void* yp;             // when yns > 0: y is written as yns bf16 planes (plane stride y_pstride) instead of fp32
+    long long y_pstride;
+    int yns;
     const float* w3frag;  // optional: W3 / W1 in MFMA-fragment order [ntile][kquad][64 lanes][4] (stage 0)
     const float* w1frag;
 };
@@ -107,14 +132,20 @@ hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** 
 hipError_t launch_conv0(const float* x, long long L, int batch, const float* w /*[64][7]*/,
                         const float* b, float* y, int cout, int ksize, hipStream_t s);
 
-// LayerNorm over the last dim (C = 512) of rows.
+// LayerNorm over the last dim (C = 512) of rows; output fp32 (yns == 0) or yns bf16 planes.
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* y, long long rows,
-                            int C, float eps, hipStream_t s);
+                            int C, float eps, hipStream_t s, void* yp = nullptr, long long y_pstride = 0,
+                            int yns = 0);
 
 // Sliding-window causal attention on the fused qkv tensor [B][T][3*H*D] (q, k already rotated);
 // output [B][T][H*D].
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window,
-                            float scale, hipStream_t s);
+                            float scale, hipStream_t s, void* outp = nullptr, long long out_pstride = 0,
+                            int outns = 0);
+
+// planes -> fp32 (x0 + x1 [+ x2]); used only to materialise per-stage taps of plane-format activations.
+hipError_t launch_planes_to_f32(const void* planes, long long pstride, int ns, float* out, long long n,
+                                hipStream_t s);
 
 // Split RVQ: proj [F][2*Dq] (semantic | acoustic projections), codebooks in fragment layout, codes
 // out[level][F] int32 (or [b][level][t] when frames_per_item > 0).

@@ -72,7 +72,8 @@ __device__ __forceinline__ float wave_sum(float v) {
 template <int C>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                         const float* __restrict__ bta, float* __restrict__ y,
-                                                        long long rows, float eps) {
+                                                        long long rows, float eps, __bf16* __restrict__ yp,
+                                                        long long pstride, int yns) {
     constexpr int PER = C / 64;  // floats per lane
     static_assert(PER % 4 == 0, "C multiple of 256");
     const int lane = threadIdx.x & 63;
@@ -110,15 +111,28 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
         o.y = (v[q * 4 + 1] * sc + bi) * gg.y + bb.y;
         o.z = (v[q * 4 + 2] * sc + bi) * gg.z + bb.z;
         o.w = (v[q * 4 + 3] * sc + bi) * gg.w + bb.w;
-        *reinterpret_cast<f32x4*>(yr + c0) = o;
+        if (yns == 0) {
+            *reinterpret_cast<f32x4*>(yr + c0) = o;
+        } else {
+            // planes for the split-bf16 GEMMs that read this row (q/k/v, fc1)
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            __bf16* pr = yp + row * C + c0;
+            f32x4 rem = o;
+            for (int pl = 0; pl < yns; ++pl) {
+                bf16x4 h;
+                h.x = (__bf16)rem.x; h.y = (__bf16)rem.y; h.z = (__bf16)rem.z; h.w = (__bf16)rem.w;
+                *reinterpret_cast<bf16x4*>(pr + pl * pstride) = h;
+                rem.x -= (float)h.x; rem.y -= (float)h.y; rem.z -= (float)h.z; rem.w -= (float)h.w;
+            }
+        }
     }
 }
 
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* y, long long rows, int C,
-                            float eps, hipStream_t s) {
-    if (C != 512) return hipErrorInvalidValue;
+                            float eps, hipStream_t s, void* yp, long long y_pstride, int yns) {
+    if (C != 512 || (yns != 0 && !yp)) return hipErrorInvalidValue;
     hipLaunchKernelGGL((layernorm_kernel<512>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, g, b, y,
-                       rows, eps);
+                       rows, eps, reinterpret_cast<__bf16*>(yp), y_pstride, yns);
     return hipGetLastError();
 }
 
@@ -131,7 +145,8 @@ hipError_t launch_layernorm(const float* x, const float* g, const float* b, floa
 // by 1/sqrt(64) = 1/8 (exact).  Online softmax with running max / sum per query, fp32 throughout.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict__ qkv, float* __restrict__ out,
-                                                        int T, int H, int window, float scale) {
+                                                        int T, int H, int window, float scale,
+                                                        void* __restrict__ outp, long long pstride, int outns) {
     constexpr int D = 64;
     constexpr int KC = 32;
     constexpr int LDKS = D + 4;
@@ -241,15 +256,34 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
     __syncthreads();
     for (int qq = 0; qq < 32; ++qq) {
         const int q = qw + qq;
-        if (q < T) out[((long long)b * T + q) * (H * D) + h * D + lane] = ow[qq * LDO + lane];
+        if (q < T) store_act(out, outp, pstride, outns, ((long long)b * T + q) * (H * D) + h * D + lane, ow[qq * LDO + lane]);
     }
 }
 
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window, float scale,
-                            hipStream_t s) {
-    if (D != 64) return hipErrorInvalidValue;
+                            hipStream_t s, void* outp, long long out_pstride, int outns) {
+    if (D != 64 || (outns != 0 && !outp)) return hipErrorInvalidValue;
     dim3 grid((T + 127) / 128, H, batch);
-    hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, qkv, out, T, H, window, scale);
+    hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, qkv, out, T, H, window, scale, outp, out_pstride,
+                       outns);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void planes_to_f32_kernel(const __bf16* __restrict__ pl, long long pstride, int ns,
+                                                            float* __restrict__ out, long long n) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float v = (float)pl[i] + (float)pl[i + pstride];
+    if (ns == 3) v = v + (float)pl[i + 2 * pstride];
+    out[i] = v;
+}
+
+hipError_t launch_planes_to_f32(const void* planes, long long pstride, int ns, float* out, long long n,
+                                hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (ns != 2 && ns != 3) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(planes_to_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const __bf16*>(planes), pstride, ns, out, n);
     return hipGetLastError();
 }
 

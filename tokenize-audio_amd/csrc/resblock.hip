@@ -46,6 +46,48 @@ __device__ __forceinline__ void mma_k32(f32x16 (&acc)[TM][TN], const float* A, i
     }
 }
 
+// Stores one wave's 32 x 64 block of y (v[j][r] in the MFMA C layout: row (r&3) + 8(r>>2) + 4h, column
+// 32j + (lane&31)) through an 8 x 68-float wave-private LDS buffer, 8 rows at a time, so that each lane writes
+// 8 consecutive values of one row: 2 x 16 B of fp32, or one 16-B bf16x8 per plane -- instead of one scattered
+// 4-byte (or per plane 2-byte) store per value.  Same wave writes and reads: LDS order needs no barrier.
+constexpr int YSTG_LD = 68;
+constexpr int YSTG_FLOATS = 8 * YSTG_LD;
+__device__ __forceinline__ void store_y_block(const ResArgs& p, float* stg, const f32x16 (&v)[2], long long ybase,
+                                              long long row0, int col0, int C, long long T, int lane) {
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    const int h = lane >> 5, c = lane & 31;
+    const int lr = lane >> 3, lc = (lane & 7) * 8;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) stg[(rr + 4 * h) * YSTG_LD + 32 * j + c] = v[j][4 * g + rr];
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(stg + lr * YSTG_LD + lc);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(stg + lr * YSTG_LD + lc + 4);
+        const long long row = row0 + 8 * g + lr;
+        if (row < T) {
+            const long long idx = ybase + row * C + col0 + lc;
+            if (p.yns == 0) {
+                *reinterpret_cast<f32x4*>(p.y + idx) = a0;
+                *reinterpret_cast<f32x4*>(p.y + idx + 4) = a1;
+            } else {
+                float rem[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                __bf16* dst = reinterpret_cast<__bf16*>(p.yp) + idx;
+                for (int pl = 0; pl < p.yns; ++pl) {
+                    bf16x8 hv;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        hv[e] = (__bf16)rem[e];
+                        rem[e] = rem[e] - (float)hv[e];
+                    }
+                    *reinterpret_cast<bf16x8*>(dst + pl * p.y_pstride) = hv;
+                }
+            }
+        }
+    }
+}
+
 template <int C, int BM, bool WINDOW, bool FIRST, int W1M, int W1N, int W2M, int W2N, int NP>
 __global__ __launch_bounds__(256) void resblock_kernel(ResArgs p) {
     constexpr int H = C / 2;
@@ -58,7 +100,9 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs p) {
     static_assert(W1M * W1N == 4 && W2M * W2N == 4, "4 waves");
     static_assert(TM1 >= 1 && TN1 >= 1 && TM2 >= 1 && TN2 >= 1, "tiles");
     static_assert(C % NP == 0 && H % 32 == 0, "shapes");
-    constexpr int XS = WINDOW ? (BM + 2) * LDX : BM * LDK;
+    // Xs (the ELU(x) slab / streamed A slices) is dead after GEMM1 and doubles as the y staging of store_y_block
+    constexpr int XS0 = WINDOW ? (BM + 2) * LDX : BM * LDK;
+    constexpr int XS = XS0 > 4 * YSTG_FLOATS ? XS0 : 4 * YSTG_FLOATS;
     constexpr int BST = (H > NP ? H : NP) * LDK;
     constexpr int A_F4 = WINDOW ? 1 : BM * 8 / 256;  // streamed A slice: float4 per thread
     constexpr int B1_F4 = H * 8 / 256 > 0 ? H * 8 / 256 : 1;
@@ -244,7 +288,7 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs p) {
     }
 
     // ---------------- GEMM2: y = ELU(x + b1 + h . W1^T), NP columns per pass ----------------
-    float* __restrict__ yb = p.y + (long long)b * T * C;
+    const long long ybase = (long long)b * T * C;
     for (int n0 = 0; n0 < C; n0 += NP) {
         auto load2 = [&](int k0) {
 #pragma unroll
@@ -286,6 +330,16 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs p) {
         }
         const int rb0 = w2m * TM2 * 32 + 4 * (lane >> 5);
         const int cb0 = n0 + w2n * TN2 * 32 + (lane & 31);
+        if constexpr (!FIRST && TM2 == 1 && TN2 == 2) {
+            f32x16 v[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const float bias = p.b1[cb0 + j * 32];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[j][r] = elu_f(xres[0][j][r] + (acc2[0][j][r] + bias));
+            }
+            store_y_block(p, Xs + wave * YSTG_FLOATS, v, ybase, m0 + w2m * 32, n0 + w2n * 64, C, T, lane);
+        } else {
 #pragma unroll
         for (int j = 0; j < TN2; ++j) {
             const int col = cb0 + j * 32;
@@ -297,9 +351,11 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs p) {
                     const long long row = m0 + rb0 + i * 32 + (r & 3) + 8 * (r >> 2);
                     if (row < T) {
                         const float xr = FIRST ? Xs[(row - m0) * LDX + col] : xres[i][j][r];
-                        yb[row * C + col] = elu_f(xr + (acc2[i][j][r] + bias));
+                        store_act(p.y, p.yp, p.y_pstride, p.yns, ybase + row * C + col,
+                                  elu_f(xr + (acc2[i][j][r] + bias)));
                     }
                 }
+        }
         }
         if (n0 + NP < C) prefetch_res(n0 + NP);
     }
@@ -408,8 +464,10 @@ __global__ __launch_bounds__(256) void resblock0_wave_kernel(ResArgs p) {
             for (int j = 0; j < 2; ++j)
                 acc2[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], b1q[j * 4 + kq][s], acc2[j], 0, 0, 0);
     }
-    // epilogue 2: y = ELU(x0 + (acc + b1)); x0 (the identity skip) recomputed from the audio window
-    float* __restrict__ yb = p.y + (long long)b * T * C;
+    // epilogue 2: y = ELU(x0 + (acc + b1)); x0 (the identity skip) recomputed from the audio window; y leaves
+    // through the wave's own (now free) slab region
+    const long long ybase = (long long)b * T * C;
+    f32x16 v[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int col = j * 32 + (lane & 31);
@@ -425,9 +483,11 @@ __global__ __launch_bounds__(256) void resblock0_wave_kernel(ResArgs p) {
 #pragma unroll
             for (int k = 0; k < 7; ++k) x0 = fmaf(wc[k], Aw[row + 2 + k], x0);
             x0 = x0 + bc;
-            if (r0 + row < T) yb[(r0 + row) * C + col] = elu_fast(x0 + (acc2[j][r] + bias));
+            v[j][r] = elu_fast(x0 + (acc2[j][r] + bias));
         }
     }
+    static_assert(34 * LDX >= YSTG_FLOATS, "staging fits the slab");
+    store_y_block(p, Xw, v, ybase, r0, 0, C, T, lane);
 }
 
 template <int C, int BM, bool WINDOW, bool FIRST, int W1M, int W1N, int W2M, int W2N, int NP>

@@ -8,7 +8,7 @@
 #include <cstring>
 #include <vector>
 
-#include "gemm_kernel.h"
+#include "gemm_planes.h"
 
 using namespace mimi;
 
@@ -42,6 +42,24 @@ void launch_bf(const GemmArgs& a, hipStream_t s) {
     dim3 grid((a.M + BM - 1) / BM, (a.N + BN - 1) / BN, a.batch);
     hipLaunchKernelGGL((gemm_bf16x_kernel<BM, BN, WM, WN, NS, false, PAD_ZERO, EPI_BIAS, 0>), grid,
                        dim3(WM * WN * 64), 0, s, a);
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int ST>
+void launch_pl(const GemmArgs& a, hipStream_t s) {
+    const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.batch;
+    hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI_BIAS, 0, 0>), dim3(nwg),
+                       dim3(WM * WN * 64), 0, s, a);
+}
+
+__global__ void split_planes(const float* x, __bf16* out, long long n) {
+    const long long i = blockIdx.x * 256LL + threadIdx.x;
+    if (i >= n) return;
+    float r = x[i];
+    for (int p = 0; p < 3; ++p) {
+        const __bf16 h = (__bf16)r;
+        out[p * n + i] = h;
+        r -= (float)h;
+    }
 }
 
 struct Variant {
@@ -84,6 +102,13 @@ int main(int argc, char** argv) {
         {"bf16x2p 128x128", launch_bf<128, 128, 2, 2, 2>, 32, 2},
         {"bf16x2p 256x128 8w", launch_bf<256, 128, 4, 2, 2>, 32, 2},
         {"bf16x2p 256x256 8w", launch_bf<256, 256, 4, 2, 2>, 32, 2},
+        {"planes3 128x128 s3", launch_pl<128, 128, 2, 2, 3, 3>, 32, 3},
+        {"planes3 128x128 s2", launch_pl<128, 128, 2, 2, 3, 2>, 32, 3},
+        {"planes3 256x128 8w s2", launch_pl<256, 128, 4, 2, 3, 2>, 32, 3},
+        {"planes3 128x64 s3", launch_pl<128, 64, 2, 2, 3, 3>, 32, 3},
+        {"planes3 64x128 s3", launch_pl<64, 128, 1, 2, 3, 3>, 32, 3},
+        {"planes2 128x128 s3", launch_pl<128, 128, 2, 2, 2, 3>, 32, 2},
+        {"planes2 256x128 8w s3", launch_pl<256, 128, 4, 2, 2, 3>, 32, 2},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
@@ -126,6 +151,10 @@ int main(int argc, char** argv) {
         CK(hipMalloc(&C, nC * 4));
         CK(hipMalloc(&Cref, nC * 4));
         CK(hipMemcpy(A, hA.data(), nA * 4, hipMemcpyHostToDevice));
+        __bf16* Apl;
+        CK(hipMalloc(&Apl, 3 * nA * 2));
+        hipLaunchKernelGGL(split_planes, dim3((unsigned)((nA + 255) / 256)), dim3(256), 0, 0, A, Apl, (long long)nA);
+        CK(hipDeviceSynchronize());
         CK(hipMemcpy(W, hW.data(), nW * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy(bias, hb.data(), sh.N * 4, hipMemcpyHostToDevice));
         GemmArgs a{};
@@ -135,6 +164,8 @@ int main(int argc, char** argv) {
         a.a_rs = sh.s * sh.cin;
         a.a_cin = sh.cin;
         a.a_len = sh.tin * sh.cin;
+        a.Ap = Apl;
+        a.a_pstride = (long long)nA;
         a.W = W;
         a.M = (int)sh.tout;
         a.N = sh.N;
@@ -182,7 +213,7 @@ int main(int argc, char** argv) {
                    vars[v].name, best, tot / reps, flops / (best * 1e-3) / 1e12, maxrel);
             fflush(stdout);
         }
-        CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(Wp)); CK(hipFree(bias)); CK(hipFree(C)); CK(hipFree(Cref));
+        CK(hipFree(A)); CK(hipFree(Apl)); CK(hipFree(W)); CK(hipFree(Wp)); CK(hipFree(bias)); CK(hipFree(C)); CK(hipFree(Cref));
     }
     return 0;
 }
