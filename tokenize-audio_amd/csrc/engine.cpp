@@ -744,6 +744,7 @@ struct Workspace {
     float *x, *y;                  // SEANet ping-pong (the residual blocks keep their hidden tile on chip)
     float *t0, *t1, *qkv, *att, *ff;  // transformer
     float *dsout, *proj;
+    float* rvq;  // rvq_work_bytes(frames)
 };
 
 // Planes of the split-bf16 path: activations consumed only by GEMMs (resblock outputs, the last down conv's
@@ -785,9 +786,10 @@ static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspa
                             act(T * Hd * B),
                             act(T * (size_t)c.intermediate_size * B),
                             (size_t)p.frames12 * Hd * B,
-                            (size_t)p.frames12 * 2 * c.vq_hidden_dim * B};
+                            (size_t)p.frames12 * 2 * c.vq_hidden_dim * B,
+                            rvq_work_bytes((long long)p.frames12 * B) / sizeof(float)};
     size_t off = 0;
-    float** ptrs[] = {&w->x, &w->y, &w->t0, &w->t1, &w->qkv, &w->att, &w->ff, &w->dsout, &w->proj};
+    float** ptrs[] = {&w->x, &w->y, &w->t0, &w->t1, &w->qkv, &w->att, &w->ff, &w->dsout, &w->proj, &w->rvq};
     char* base = reinterpret_cast<char*>(e->ws);
     for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); ++i) {
         if (w) *ptrs[i] = reinterpret_cast<float*>(base + off);
@@ -964,8 +966,9 @@ static GemmArgs linear_args(const float* in, int64_t rows, int K, const float* W
     } while (0)
 
 static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int32_t* codes, int frames_per_item,
-                   hipStream_t s, Recorder& rec) {
+                   void* work, hipStream_t s, Recorder& rec) {
     RvqArgs r{};
+    r.work = work;
     r.proj = proj;
     r.frames = frames;
     r.D = e->cfg.codebook_dim;
@@ -979,7 +982,7 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     r.frames_per_item = frames_per_item;
     LAUNCH_TRY(launch_rvq(r, s), "rvq");
     rec.mark("rvq", 2.0 * frames * r.D * r.ncodes * K, (double)frames * (2 * r.D) * 4 + (double)frames * K * 4,
-             "mimi::rvq_kernel<256, 8>");
+             "mimi::rvq_level_kernel<256>");
     return MIMI_OK;
 }
 
@@ -1135,7 +1138,7 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
     LAUNCH_TRY(launch_gemm(ROLE_INPROJ, ap, s, &kname), "input_proj");
     rec.mark("input_proj", gemm_flops(ap), gemm_bytes(ap, false), kname);
     if ((rc = save_tap(e, "proj", w.proj, B, T2, 2 * Dq, s))) return rc;
-    if ((rc = run_rvq(e, w.proj, (int64_t)B * T2, K, codes, (int)T2, s, rec))) return rc;
+    if ((rc = run_rvq(e, w.proj, (int64_t)B * T2, K, codes, (int)T2, w.rvq, s, rec))) return rc;
     HIP_TRY(hipEventRecord(e->ws_free, s));
     return MIMI_OK;
 }
@@ -1176,7 +1179,8 @@ extern "C" int mimi_rvq_encode(mimi_engine* e, const float* emb, int64_t frames,
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the HIP null stream, as in every HIP API
     const int Hd = e->cfg.hidden_size, Dq = e->cfg.vq_hidden_dim;
-    const size_t need = (size_t)frames * 2 * Dq * sizeof(float);
+    const size_t projb = ((size_t)frames * 2 * Dq * sizeof(float) + 255) / 256 * 256;
+    const size_t need = projb + rvq_work_bytes(frames);
     int rc = ensure_ws(e, std::max(need, e->ws_bytes), s);
     if (rc) return rc;
     float* proj = reinterpret_cast<float*>(e->ws);
@@ -1187,7 +1191,7 @@ extern "C" int mimi_rvq_encode(mimi_engine* e, const float* emb, int64_t frames,
     const char* kname = "?";
     LAUNCH_TRY(launch_gemm(ROLE_INPROJ, ap, s, &kname), "input_proj");
     rec.mark("input_proj", 2.0 * frames * Hd * 2 * Dq, 0, kname);
-    if ((rc = run_rvq(e, proj, frames, K, codes, 0, s, rec))) return rc;
+    if ((rc = run_rvq(e, proj, frames, K, codes, 0, reinterpret_cast<char*>(e->ws) + projb, s, rec))) return rc;
     HIP_TRY(hipEventRecord(e->ws_free, s));
     return MIMI_OK;
 }

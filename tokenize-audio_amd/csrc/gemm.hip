@@ -75,9 +75,10 @@ static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Tiles of the planes kernel (tools/gemm_bench.hip, profiles/r1_gemm_bench_planes.log): 256x128 (8 waves,
-// 2 stages at NS = 3 / 3 stages at NS = 2, 144 KiB LDS) where M x N is large, 128x128 (4 waves, 3 stages)
-// where a 256-row tile would leave CUs idle (final conv, o_proj, fc2: M = B*250 rows, N = 512).
+// Tiles of the planes kernel (tools/gemm_bench.hip, profiles/r1_gemm_bench_planes*.log): 256x128 with 8 waves
+// (2 stages at NS = 3 / 3 stages at NS = 2, 144 KiB LDS) where M x N is large (down convs, fc1); 128x128 with
+// 8 waves of 32x64 (3 stages, 2 waves per SIMD) where a 256-row tile would leave CUs idle (final conv, q/k/v,
+// o_proj, fc2: M = B*250 rows).
 template <int EPI, int OUTP3, int OUTP2, int TAG>
 static hipError_t run_planes_big(const GemmArgs& a, hipStream_t s, int prec) {
     if (prec == PREC_BF16X6) return run_planes<256, 128, 4, 2, 3, 2, EPI, OUTP3, TAG>(a, s);
@@ -85,8 +86,8 @@ static hipError_t run_planes_big(const GemmArgs& a, hipStream_t s, int prec) {
 }
 template <int EPI, int TAG>
 static hipError_t run_planes_small(const GemmArgs& a, hipStream_t s, int prec) {
-    if (prec == PREC_BF16X6) return run_planes<128, 128, 2, 2, 3, 3, EPI, 0, TAG>(a, s);
-    return run_planes<128, 128, 2, 2, 2, 3, EPI, 0, TAG>(a, s);
+    if (prec == PREC_BF16X6) return run_planes<128, 128, 4, 2, 3, 3, EPI, 0, TAG>(a, s);
+    return run_planes<128, 128, 4, 2, 2, 3, EPI, 0, TAG>(a, s);
 }
 
 template <bool ELU_IN, int PAD, int EPI, int TAG>
@@ -131,7 +132,7 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         case ROLE_DOWN: return run_planes_big<EPI_BIAS, 0, 0, 2>(a, s, prec);
         case ROLE_DOWN_ELU: return run_planes_big<EPI_BIAS_ELU, 3, 2, 3>(a, s, prec);  // planes out: final conv
         case ROLE_FINAL: return run_planes_small<EPI_BIAS_OUT, 4>(a, s, prec);
-        case ROLE_QKV: return run_planes_big<EPI_ROPE, 0, 0, 5>(a, s, prec);
+        case ROLE_QKV: return run_planes_small<EPI_ROPE, 5>(a, s, prec);
         case ROLE_OPROJ: return run_planes_small<EPI_SCALE_RES, 6>(a, s, prec);
         case ROLE_FC1: return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);  // planes out: fc2
         case ROLE_FC2: return run_planes_small<EPI_SCALE_RES, 8>(a, s, prec);

@@ -161,7 +161,9 @@ struct RvqArgs {
     const float* cb_norm;   // [level][ncodes]
     int32_t* codes;
     int frames_per_item;    // T (for [b][level][t] output); 0 -> [level][frame]
+    void* work;             // rvq_work_bytes(frames): residual ping-pong + per-slice partial argmins
 };
+size_t rvq_work_bytes(long long frames);
 hipError_t launch_rvq(const RvqArgs& a, hipStream_t s);
 
 }  // namespace mimi

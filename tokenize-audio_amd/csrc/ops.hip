@@ -180,9 +180,13 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
 
     const int kstart = max(0, q0 - window + 1);
     const int kend = min(T - 1, q0 + 127);
-    for (int c0 = kstart; c0 <= kend; c0 += KC) {
-        __syncthreads();
-        for (int idx = tid; idx < KC * (D / 4); idx += 256) {
+    // K/V chunks: registers hold chunk c+1 while chunk c is computed (2 float4 of K and of V per thread)
+    constexpr int PER = KC * (D / 4) / 256;
+    f32x4 kreg[PER], vreg[PER];
+    auto fetch = [&](int c0) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int idx = tid + q * 256;
             const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
             const int j = c0 + r;
             f32x4 kv = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
@@ -190,10 +194,22 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
                 kv = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + H * D + h * D + c);
                 vv = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + 2 * H * D + h * D + c);
             }
-            *reinterpret_cast<f32x4*>(Ks + r * LDKS + c) = kv;
-            *reinterpret_cast<f32x4*>(Vs + r * D + c) = vv;
+            kreg[q] = kv;
+            vreg[q] = vv;
+        }
+    };
+    fetch(kstart);
+    for (int c0 = kstart; c0 <= kend; c0 += KC) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int idx = tid + q * 256;
+            const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
+            *reinterpret_cast<f32x4*>(Ks + r * LDKS + c) = kreg[q];
+            *reinterpret_cast<f32x4*>(Vs + r * D + c) = vreg[q];
         }
         __syncthreads();
+        if (c0 + KC <= kend) fetch(c0 + KC);
         // skip chunks entirely outside this wave's band [qw - W + 1, qw + 31]
         if (c0 > qw + 31 || c0 + KC - 1 < qw - window + 1) continue;
         // S^T[key][query]
@@ -317,84 +333,172 @@ __device__ __forceinline__ float torch_sqsum(const float* r) {
     return tot;
 }
 
-template <int D, int NW>
-__global__ __launch_bounds__(NW * 64) void rvq_kernel(RvqArgs p) {
-    constexpr int FR = 32;
-    constexpr int LDH = D / 2 + 4;  // half-image row (even or odd k), +4 pad
-    __shared__ __attribute__((aligned(16))) float res[FR][D];
-    __shared__ __attribute__((aligned(16))) float img[2][FR][LDH];  // -2*r split by k parity
-    __shared__ float xn[FR];
-    __shared__ float redd[NW][FR];
-    __shared__ int redi[NW][FR];
-    __shared__ int best[FR];
+// Level-parallel form.  One launch per level L over (frame tiles of RVQ_FT) x (code slices of RVQ_CS): every
+// workgroup computes the distances of its 128 frames to its 256 codes (8 waves x 32 codes, 4 MFMA tiles per
+// wave) and writes the slice's (min distance, first index) per frame.  The NEXT launch's prologue
+// merges the slices of level L-1 (lexicographic (d, idx): the global first-index argmin), writes those codes
+// (slice-0 workgroups), and forms r_L = r_{L-1} - embed_{L-1}[idx] (bitwise the same in every slice's
+// workgroup); a last launch merges level K-1.  8 + 1 launches of 256 workgroups instead of one launch of
+// F/32 = 125 workgroups that left half the CUs idle.  Distances: identical arithmetic and k order to the
+// reference chain above (|r|^2 from the (-2r)^2 image: scaling by 4 is exact).
+constexpr int RVQ_FT = 128;
+constexpr int RVQ_CS = 256;
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int h = lane >> 5;
-    const long long f0 = (long long)blockIdx.x * FR;
-    const int ntile = p.ncodes / 32;
-    const int tiles_per_wave = ntile / NW;
-    const int nu = D / 8;
+size_t rvq_work_bytes(long long frames) {
+    const long long fp = (frames + RVQ_FT - 1) / RVQ_FT * RVQ_FT;
+    const int nsl = 2048 / RVQ_CS;
+    return (size_t)(2 * fp * 256 * 4 + 2 * 2 * fp * nsl * 4);
+}
 
-    for (int level = 0; level < p.levels; ++level) {
-        if (level == 0 || level == p.nsem) {
-            // (re)load the projection this quantizer works on: semantic half, then acoustic half
-            const int coff = (level == 0) ? 0 : D;
-            for (int idx = tid; idx < FR * D; idx += NW * 64) {
-                const int i = idx / D, k = idx % D;
-                const long long f = f0 + i;
-                res[i][k] = (f < p.frames) ? p.proj[f * (2 * D) + coff + k] : 0.0f;
-            }
-            __syncthreads();
+// work layout: res[2][Fp][D] | pd[2][Fp][nsl] | pi[2][Fp][nsl]; parity = level & 1 (selected without
+// indexing a pointer array, which would live in scratch)
+struct RvqWork {
+    float* base;
+    long long fp;
+    int D, nsl;
+    __device__ float* res(int par) const { return base + (par ? fp * D : 0); }
+    __device__ float* pd(int par) const { return base + 2 * fp * D + (par ? fp * nsl : 0); }
+    __device__ int* pi(int par) const {
+        return reinterpret_cast<int*>(base + 2 * fp * D + 2 * fp * nsl) + (par ? fp * nsl : 0);
+    }
+};
+
+__device__ __forceinline__ RvqWork rvq_work(const RvqArgs& p, int nsl) {
+    RvqWork r;
+    r.base = reinterpret_cast<float*>(p.work);
+    r.fp = (p.frames + RVQ_FT - 1) / RVQ_FT * RVQ_FT;
+    r.D = p.D;
+    r.nsl = nsl;
+    return r;
+}
+
+__device__ __forceinline__ void rvq_store_code(const RvqArgs& p, int level, long long f, int ix) {
+    if (p.frames_per_item > 0) {
+        const long long bb = f / p.frames_per_item, t = f % p.frames_per_item;
+        p.codes[(bb * p.levels + level) * p.frames_per_item + t] = ix;
+    } else {
+        p.codes[(long long)level * p.frames + f] = ix;
+    }
+}
+
+// merged argmin of level L over its slices (ties -> lower index; an all-NaN row keeps index 0)
+__device__ __forceinline__ int rvq_merge(const RvqWork& w, int L, long long f, int nsl, int ncodes) {
+    const float* pd = w.pd(L & 1) + f * nsl;
+    const int* pi = w.pi(L & 1) + f * nsl;
+    float d = pd[0];
+    int ix = pi[0];
+    for (int q = 1; q < nsl; ++q) {
+        const float od = pd[q];
+        const int oi = pi[q];
+        if (od < d || (od == d && oi < ix)) { d = od; ix = oi; }
+    }
+    return (ix < 0 || ix >= ncodes) ? 0 : ix;
+}
+
+template <int D>
+__global__ __launch_bounds__(512) void rvq_level_kernel(RvqArgs p, int L) {
+    constexpr int FT = RVQ_FT, LDH = D / 2 + 4;
+    constexpr int NSL = 2048 / RVQ_CS;
+    __shared__ __attribute__((aligned(16))) float img[2][FT][LDH];  // -2 r, split by k parity
+    __shared__ float xn[FT];
+    __shared__ int prev[FT];
+    __shared__ float redd[8][FT];
+    __shared__ int redi[8][FT];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+    const long long f0 = (long long)blockIdx.x * FT;
+    const int slice = blockIdx.y;
+    const RvqWork w = rvq_work(p, NSL);
+
+    // ---- prologue: finish level L-1, form r_L
+    if (L >= 1 && tid < FT) {
+        const long long f = f0 + tid;
+        int ix = 0;
+        if (f < p.frames) {
+            ix = rvq_merge(w, L - 1, f, NSL, p.ncodes);
+            if (slice == 0) rvq_store_code(p, L - 1, f, ix);
         }
-        // A image and |r|^2
-        for (int idx = tid; idx < FR * D; idx += NW * 64) {
-            const int i = idx / D, k = idx % D;
-            img[k & 1][i][k >> 1] = -2.0f * res[i][k];
-        }
-        if (tid < FR) xn[tid] = torch_sqsum<D>(res[tid]);
-        __syncthreads();
-
-        const float* cbf = p.cb_frag + (long long)level * ntile * nu * 256;
-        const float* cbn = p.cb_norm + (long long)level * p.ncodes;
-        float bd[16];
-        int bi[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { bd[r] = INFINITY; bi[r] = 0x7fffffff; }
-        float xr[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) xr[r] = xn[(r & 3) + 8 * (r >> 2) + 4 * h];
-
-        for (int tt = 0; tt < tiles_per_wave; ++tt) {
-            const int jt = wave * tiles_per_wave + tt;
-            const f32x4* bsrc = reinterpret_cast<const f32x4*>(cbf + (long long)jt * nu * 256) + lane;
-            f32x16 acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-            const float* arow = &img[h][lane & 31][0];
+        prev[tid] = ix;
+    }
+    __syncthreads();
+    const bool fresh = (L == 0 || L == p.nsem);  // semantic start / acoustic start: r = projection
+    const int coff = (L < p.nsem) ? 0 : D;
+    const float* rows_prev = p.cb_rows + (long long)(L - 1) * p.ncodes * D;
+    const float* rin = w.res((L + 1) & 1);  // residual entering level L-1
+    float* rout = w.res(L & 1);
+    // float4 chunks, 16 per thread, loads batched 8 at a time (a serial load->use loop here is latency-bound)
 #pragma unroll 8
-            for (int u = 0; u < D / 8; ++u) {
-                const f32x4 bv = bsrc[u * 64];
-                const f32x4 av = *reinterpret_cast<const f32x4*>(arow + u * 4);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0], bv[0], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1], bv[1], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[2], bv[2], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[3], bv[3], acc, 0, 0, 0);
+    for (int idx = tid; idx < FT * D / 4; idx += 512) {
+        const int i = idx / (D / 4), k = (idx % (D / 4)) * 4;
+        const long long f = f0 + i;
+        f32x4 r = {0.f, 0.f, 0.f, 0.f};
+        if (f < p.frames) {
+            if (fresh) {
+                r = *reinterpret_cast<const f32x4*>(p.proj + f * (2 * D) + coff + k);
+            } else {
+                const f32x4 a = *reinterpret_cast<const f32x4*>(rin + f * D + k);
+                const f32x4 e = *reinterpret_cast<const f32x4*>(rows_prev + (long long)prev[i] * D + k);
+                r = a - e;
             }
-            const int j = jt * 32 + (lane & 31);
-            const float yn = cbn[j];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float d2 = acc[r] + xr[r];
-                d2 = d2 + yn;
-                const float d = __builtin_sqrtf(fmaxf(d2, 0.0f));
-                if (d < bd[r]) { bd[r] = d; bi[r] = j; }
-            }
+            if (slice == 0) *reinterpret_cast<f32x4*>(rout + f * D + k) = r;
         }
-        // reduce over the 32 lanes of each half (same rows), ties -> lower index
+        img[0][i][k >> 1] = -2.0f * r.x;
+        img[1][i][k >> 1] = -2.0f * r.y;
+        img[0][i][(k >> 1) + 1] = -2.0f * r.z;
+        img[1][i][(k >> 1) + 1] = -2.0f * r.w;
+    }
+    __syncthreads();
+    // torch x.pow(2).sum(-1) order (8 lanes x 4 accumulators, accumulators combined, lanes summed in order) on
+    // (-2r)^2 = 4 r^2, then * 0.25 (power-of-two scaling: exact); 8 threads per frame, one per lane
+    for (int fi = tid >> 3; fi < FT; fi += 64) {
+        const int l = tid & 7;
+        float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+        for (int blk = 0; blk < D / 8; ++blk) {
+            const int k = blk * 8 + l;
+            const float v = img[k & 1][fi][k >> 1];
+            a[blk & 3] = a[blk & 3] + v * v;
+        }
+        const float part = ((a[0] + a[1]) + a[2]) + a[3];
+        float tot = __shfl(part, (lane & ~7));
+#pragma unroll
+        for (int q = 1; q < 8; ++q) tot = tot + __shfl(part, (lane & ~7) + q);
+        if (l == 0) xn[fi] = tot * 0.25f;
+    }
+    __syncthreads();
+
+    // ---- distances of FT frames x this wave's 32 codes (8 waves: 2 per SIMD)
+    const int code0 = slice * RVQ_CS + wave * 32;
+    const int nu = D / 8;
+    const float* cbf = p.cb_frag + (long long)L * (p.ncodes / 32) * nu * 256;
+    f32x16 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+    const f32x4* bp = reinterpret_cast<const f32x4*>(cbf + (long long)(code0 / 32) * nu * 256) + lane;
+    f32x4 bnext = bp[0];
+#pragma unroll 2
+    for (int u = 0; u < nu; ++u) {
+        const f32x4 bv = bnext;
+        if (u + 1 < nu) bnext = bp[(u + 1) * 64];  // in flight under this step's 16 MFMAs
+        f32x4 av[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = *reinterpret_cast<const f32x4*>(&img[h][i * 32 + (lane & 31)][u * 4]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][s], bv[s], acc[i], 0, 0, 0);
+    }
+    const float yn = p.cb_norm[(long long)L * p.ncodes + code0 + (lane & 31)];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            float d = bd[r];
-            int ix = bi[r];
+            const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float d2 = acc[i][r] + xn[row];
+            d2 = d2 + yn;
+            float d = __builtin_sqrtf(fmaxf(d2, 0.0f));
+            int ix = code0 + (lane & 31);
 #pragma unroll
             for (int o = 16; o >= 1; o >>= 1) {
                 const float od = __shfl_xor(d, o);
@@ -402,48 +506,44 @@ __global__ __launch_bounds__(NW * 64) void rvq_kernel(RvqArgs p) {
                 if (od < d || (od == d && oi < ix)) { d = od; ix = oi; }
             }
             if ((lane & 31) == 0) {
-                const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
-                redd[wave][i] = d;
-                redi[wave][i] = ix;
+                redd[wave][row] = d;
+                redi[wave][row] = ix;
             }
         }
-        __syncthreads();
-        if (tid < FR) {
-            float d = redd[0][tid];
-            int ix = redi[0][tid];
-            for (int w = 1; w < NW; ++w) {
-                const float od = redd[w][tid];
-                const int oi = redi[w][tid];
-                if (od < d || (od == d && oi < ix)) { d = od; ix = oi; }
-            }
-            if (ix < 0 || ix >= p.ncodes) ix = 0;  // all-NaN row: torch would return a NaN index; keep in range
-            best[tid] = ix;
-            const long long f = f0 + tid;
-            if (f < p.frames) {
-                if (p.frames_per_item > 0) {
-                    const long long bb = f / p.frames_per_item, t = f % p.frames_per_item;
-                    p.codes[(bb * p.levels + level) * p.frames_per_item + t] = ix;
-                } else {
-                    p.codes[(long long)level * p.frames + f] = ix;
-                }
-            }
+    }
+    __syncthreads();
+    if (tid < FT && f0 + tid < p.frames) {
+        float d = redd[0][tid];
+        int ix = redi[0][tid];
+        for (int q = 1; q < 8; ++q) {
+            const float od = redd[q][tid];
+            const int oi = redi[q][tid];
+            if (od < d || (od == d && oi < ix)) { d = od; ix = oi; }
         }
-        __syncthreads();
-        // residual -= embed[idx]
-        const float* rows = p.cb_rows + (long long)level * p.ncodes * D;
-        for (int idx = tid; idx < FR * D; idx += NW * 64) {
-            const int i = idx / D, k = idx % D;
-            res[i][k] = res[i][k] - rows[(long long)best[i] * D + k];
-        }
-        __syncthreads();
+        const long long f = f0 + tid;
+        w.pd(L & 1)[f * NSL + slice] = d;
+        w.pi(L & 1)[f * NSL + slice] = ix;
     }
 }
 
+__global__ __launch_bounds__(256) void rvq_final_kernel(RvqArgs p, int L) {
+    const long long f = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (f >= p.frames) return;
+    constexpr int NSL = 2048 / RVQ_CS;
+    const RvqWork w = rvq_work(p, NSL);
+    rvq_store_code(p, L, f, rvq_merge(w, L, f, NSL, p.ncodes));
+}
+
 hipError_t launch_rvq(const RvqArgs& a, hipStream_t s) {
-    if (a.D != 256 || a.ncodes % (32 * 8) != 0) return hipErrorInvalidValue;
+    if (a.D != 256 || a.ncodes != 2048 || !a.work) return hipErrorInvalidValue;
     if (a.frames <= 0) return hipSuccess;
-    dim3 grid((unsigned)((a.frames + 31) / 32));
-    hipLaunchKernelGGL((rvq_kernel<256, 8>), grid, dim3(512), 0, s, a);
+    const dim3 grid((unsigned)((a.frames + RVQ_FT - 1) / RVQ_FT), 2048 / RVQ_CS);
+    for (int L = 0; L < a.levels; ++L) {
+        hipLaunchKernelGGL((rvq_level_kernel<256>), grid, dim3(512), 0, s, a, L);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(rvq_final_kernel, dim3((unsigned)((a.frames + 255) / 256)), dim3(256), 0, s, a, a.levels - 1);
     return hipGetLastError();
 }
 

@@ -107,6 +107,10 @@ int main(int argc, char** argv) {
         {"planes3 256x128 8w s2", launch_pl<256, 128, 4, 2, 3, 2>, 32, 3},
         {"planes3 128x64 s3", launch_pl<128, 64, 2, 2, 3, 3>, 32, 3},
         {"planes3 64x128 s3", launch_pl<64, 128, 1, 2, 3, 3>, 32, 3},
+        {"planes3 128x128 8w s3", launch_pl<128, 128, 4, 2, 3, 3>, 32, 3},
+        {"planes3 128x128 8w24 s3", launch_pl<128, 128, 2, 4, 3, 3>, 32, 3},
+        {"planes3 256x128 4w s2", launch_pl<256, 128, 2, 2, 3, 2>, 32, 3},
+        {"planes3 128x256 8w s2", launch_pl<128, 256, 2, 4, 3, 2>, 32, 3},
         {"planes2 128x128 s3", launch_pl<128, 128, 2, 2, 2, 3>, 32, 2},
         {"planes2 256x128 8w s3", launch_pl<256, 128, 4, 2, 2, 3>, 32, 2},
     };
