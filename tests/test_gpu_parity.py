@@ -197,3 +197,34 @@ def test_thread_safety(engine):
     [t.join() for t in ts]
     assert not errors
     assert all(torch.equal(r, ref) for r in results)
+
+
+@pytest.mark.parametrize("mode,tol", [("f32", ACT_TOL), ("bf16x3", ACT_TOL)])
+def test_precision_modes(engine, golden, mode, tol):
+    """The non-default GEMM modes stay within the activation tolerance and explain every code flip."""
+    arrays, meta = golden
+    x = synthetic.speech_like(240000, meta["audio_seed"], 6)
+    engine.set_precision(mode)
+    engine.set_taps(True)
+    try:
+        codes = engine.encode(torch.from_numpy(x)[None, None].cuda()).audio_codes[0].cpu().numpy()
+        emb = engine.get_tap("downsample")[0].T
+    finally:
+        engine.set_taps(False)
+        engine.set_precision("bf16x6")
+    assert rel_err(emb, arrays["emb_speech10s"]) < tol
+    frac, bad = margin_audit(codes, arrays["embcodes_speech10s"].astype(np.int64), arrays["margins_speech10s"])
+    assert not bad, (mode, frac, bad[:5])
+
+
+def test_long_clip_without_planes_matches_prefix(engine):
+    """Clips too long for the 32-bit plane addressing (> 8.39 M samples per item at stage 0) take the
+    register-split GEMMs; the arithmetic is the same split, so a causal prefix's codes match bit for bit."""
+    L = 8_400_000
+    x = synthetic.speech_like(L, 11, 0)
+    long_codes = engine.encode_int32(torch.from_numpy(x)[None].cuda(), 8)[0].cpu().numpy()
+    P = 1_440_000
+    pre = engine.encode_int32(torch.from_numpy(x[:P].copy())[None].cuda(), 8)[0].cpu().numpy()
+    n = encoded_length(P) - 2  # the prefix's last frames see its right-edge padding
+    assert long_codes.shape == (8, encoded_length(L))
+    assert np.array_equal(long_codes[:, :n], pre[:, :n]), (long_codes[:, :n] != pre[:, :n]).sum()

@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
@@ -172,6 +173,9 @@ struct mimi_engine {
     bool finalized = false;
     int levels_available = 0;
     int precision = PREC_BF16X6;
+    // planes path: residual blocks of stages >= unfuse_from run as two plane GEMMs (k3 -> h planes, k1 + skip)
+    // instead of the fused fp32-MFMA kernel (MIMI_HIP_UNFUSE_FROM overrides; >= num_ratios disables)
+    int unfuse_from = 2;
 
     std::unordered_map<std::string, std::vector<float>> host_w;
     std::unordered_map<std::string, std::vector<int64_t>> expected;  // name -> shape
@@ -355,6 +359,7 @@ extern "C" int mimi_create(const mimi_config* cfg, int device, mimi_engine** out
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return set_err(MIMI_ERR_INVALID_ARGUMENT, "device %d of %d", device, ndev);
     e->device = device;
+    if (const char* uf = std::getenv("MIMI_HIP_UNFUSE_FROM")) e->unfuse_from = std::atoi(uf);
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipEventCreateWithFlags(&e->ws_free, hipEventDisableTiming));
     build_expected(e.get());
@@ -745,6 +750,7 @@ struct Workspace {
     float *t0, *t1, *qkv, *att, *ff;  // transformer
     float *dsout, *proj;
     float* rvq;  // rvq_work_bytes(frames)
+    float *xe, *h;  // planes path, unfused residual blocks: ELU(x) planes, hidden planes
 };
 
 // Planes of the split-bf16 path: activations consumed only by GEMMs (resblock outputs, the last down conv's
@@ -769,11 +775,12 @@ static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspa
     const int ns = act_planes(e, p);
     // a plane-format buffer of n values takes ns * n bf16 = ns * n / 2 floats
     auto act = [&](size_t n) { return ns ? (n * ns + 1) / 2 : n; };
-    size_t xmax = 0, ymax = 0;
+    size_t xmax = 0, ymax = 0, xemax = 0;
     int C = c.num_filters;
     for (int s = 0; s < c.num_ratios; ++s) {
         xmax = std::max(xmax, (size_t)p.T[s] * C);
         ymax = std::max(ymax, (size_t)p.T[s] * C);
+        if (ns && s >= e->unfuse_from && s > 0) xemax = std::max(xemax, (size_t)p.T[s] * C);
         C *= 2;
     }
     xmax = std::max(xmax, act((size_t)p.T[c.num_ratios] * C));  // last down conv's (planes) output
@@ -787,9 +794,12 @@ static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspa
                             act(T * (size_t)c.intermediate_size * B),
                             (size_t)p.frames12 * Hd * B,
                             (size_t)p.frames12 * 2 * c.vq_hidden_dim * B,
-                            rvq_work_bytes((long long)p.frames12 * B) / sizeof(float)};
+                            rvq_work_bytes((long long)p.frames12 * B) / sizeof(float),
+                            act(xemax * B),
+                            act(xemax / 2 * B)};
     size_t off = 0;
-    float** ptrs[] = {&w->x, &w->y, &w->t0, &w->t1, &w->qkv, &w->att, &w->ff, &w->dsout, &w->proj, &w->rvq};
+    float** ptrs[] = {&w->x, &w->y, &w->t0, &w->t1, &w->qkv, &w->att, &w->ff, &w->dsout, &w->proj, &w->rvq,
+                      &w->xe, &w->h};
     char* base = reinterpret_cast<char*>(e->ws);
     for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); ++i) {
         if (w) *ptrs[i] = reinterpret_cast<float*>(base + off);
@@ -1017,46 +1027,72 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
     char nm[64];
     for (int si = 0; si < c.num_ratios; ++si) {
         const int64_t T = p.T[si];
-        ResArgs ra{};
-        ra.x = w.x;
-        if (si == 0) {
-            ra.audio = audio;
-            ra.w0 = e->conv0.w;
-            ra.b0 = e->conv0.b;
-            ra.w3frag = e->res3[0].wfrag;
-            ra.w1frag = e->res1[0].wfrag;
-        }
-        ra.T = T;
-        ra.batch = B;
-        ra.w3 = e->res3[si].w;
-        ra.b3 = e->res3[si].b;
-        ra.w1 = e->res1[si].w;
-        ra.b1 = e->res1[si].b;
-        ra.y = w.y;
-        ra.yp = w.y;
-        ra.y_pstride = (long long)B * T * C;
-        ra.yns = ns;
-        LAUNCH_TRY(launch_resblock(C, ra, s, &kname), "resblock");
-        snprintf(nm, sizeof nm, "res_s%d", si);
-        {
+        const bool unf = ns && si > 0 && si >= e->unfuse_from;
+        if (!unf) {
+            ResArgs ra{};
+            ra.x = w.x;
+            if (si == 0) {
+                ra.audio = audio;
+                ra.w0 = e->conv0.w;
+                ra.b0 = e->conv0.b;
+                ra.w3frag = e->res3[0].wfrag;
+                ra.w1frag = e->res1[0].wfrag;
+            }
+            ra.T = T;
+            ra.batch = B;
+            ra.w3 = e->res3[si].w;
+            ra.b3 = e->res3[si].b;
+            ra.w1 = e->res1[si].w;
+            ra.b1 = e->res1[si].b;
+            ra.y = w.y;
+            ra.yp = w.y;
+            ra.y_pstride = (long long)B * T * C;
+            ra.yns = ns;
+            LAUNCH_TRY(launch_resblock(C, ra, s, &kname), "resblock");
+            snprintf(nm, sizeof nm, "res_s%d", si);
             const double H = C / c.compress;
             const double fl = 2.0 * B * T * (3.0 * C * H + H * C) + (si == 0 ? 2.0 * B * T * C * c.kernel_size : 0.0);
             const double by = (double)B * T * 4 * (si == 0 ? 1 + C : 2 * C) + (3.0 * C * H + H * C) * 4;
             rec.mark(nm, fl, by, kname);
+        } else {
+            // two plane GEMMs: h = ELU(b3 + W3 (*) ELU(x)) from the ELU(x) planes the down conv wrote, then
+            // y = ELU(x + b1 + W1 . h) with the fp32 x as the skip
+            const int Hh = C / c.compress;
+            GemmArgs a3 = conv_args(e->res3[si], nullptr, T, nullptr, T, B);
+            planes_in(a3, w.xe, (long long)B * T * C);
+            a3.Cp = w.h;
+            a3.c_pstride = (long long)B * T * Hh;
+            LAUNCH_TRY(launch_gemm(ROLE_RES3P, a3, s, &kname, e->precision), "res3");
+            snprintf(nm, sizeof nm, "res3_s%d", si);
+            rec.mark(nm, gemm_flops(a3), gemm_bytes(a3, false), kname);
+            GemmArgs a1 = conv_args(e->res1[si], nullptr, T, nullptr, T, B);
+            planes_in(a1, w.h, (long long)B * T * Hh);
+            a1.R = w.x;
+            a1.Cp = w.y;
+            a1.c_pstride = (long long)B * T * C;
+            LAUNCH_TRY(launch_gemm(ROLE_RES1P, a1, s, &kname, e->precision), "res1");
+            snprintf(nm, sizeof nm, "res1_s%d", si);
+            rec.mark(nm, gemm_flops(a1), gemm_bytes(a1, true), kname);
         }
         snprintf(nm, sizeof nm, "res%d_elu", si);
         if ((rc = save_tap_planes(e, nm, w.y, ns, B, T, C, s))) return rc;
         const bool last = si == c.num_ratios - 1;
+        const bool next_unf = ns && !last && si + 1 >= e->unfuse_from;
         GemmArgs ad = conv_args(e->down[si], w.y, T, w.x, p.T[si + 1], B);
+        int role = last ? ROLE_DOWN_ELU : ROLE_DOWN;
         if (ns) {
             planes_in(ad, w.y, (long long)B * T * C);
             if (last) {  // only the final conv reads it: planes out
                 ad.Cp = w.x;
                 ad.c_pstride = (long long)B * p.T[si + 1] * 2 * C;
                 ad.C = nullptr;
+            } else if (next_unf) {  // fp32 x (the skip) + ELU(x) planes (the next k3 conv's input)
+                ad.Cp = w.xe;
+                ad.c_pstride = (long long)B * p.T[si + 1] * 2 * C;
+                role = ROLE_DOWN_XE;
             }
         }
-        LAUNCH_TRY(launch_gemm(last ? ROLE_DOWN_ELU : ROLE_DOWN, ad, s, &kname, e->precision), "down");
+        LAUNCH_TRY(launch_gemm(role, ad, s, &kname, e->precision), "down");
         snprintf(nm, sizeof nm, "down_s%d", si);
         rec.mark(nm, gemm_flops(ad), gemm_bytes(ad, false), kname);
         snprintf(nm, sizeof nm, last ? "down%d_elu" : "down%d", si);

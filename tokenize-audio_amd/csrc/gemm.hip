@@ -66,8 +66,12 @@ static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
         snprintf(name, sizeof(name), "mimi::gemm_planes_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d>", BM, BN, WM, WN, NS,
                  ST, EPI, OUTP, TAG);
     g_last_kernel = name;
-    if (a.K % 32 != 0 || !a.Wsplit || !a.Ap || (OUTP && !a.Cp) || (!OUTP && !a.C)) return hipErrorInvalidValue;
+    if (a.K % 32 != 0 || !a.Wsplit || !a.Ap || ((OUTP & 7) && !a.Cp) || (!(OUTP & 7) && !a.C) ||
+        ((OUTP & 8) && !a.C) || (EPI == EPI_BIAS_RES_ELU && !a.R))
+        return hipErrorInvalidValue;
     if (a.a_len * 2 > 0x7fffffffLL) return hipErrorInvalidValue;  // buffer-resource byte offsets are 32-bit
+    // the staged epilogue writes 8 consecutive outputs per lane (16-B vectors)
+    if (a.N % 8 || a.ldc % 8 || a.c_bstride % 8 || a.c_pstride % 8) return hipErrorInvalidValue;
     const long long nwg = (long long)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.batch;
     if (nwg > 0x7fffffffLL) return hipErrorInvalidValue;
     hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG>), dim3((unsigned)nwg),
@@ -136,6 +140,9 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         case ROLE_OPROJ: return run_planes_small<EPI_SCALE_RES, 6>(a, s, prec);
         case ROLE_FC1: return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);  // planes out: fc2
         case ROLE_FC2: return run_planes_small<EPI_SCALE_RES, 8>(a, s, prec);
+        case ROLE_DOWN_XE: return run_planes_big<EPI_BIAS, 3 | 8, 2 | 8, 11>(a, s, prec);
+        case ROLE_RES3P: return run_planes_big<EPI_BIAS_ELU, 3, 2, 12>(a, s, prec);
+        case ROLE_RES1P: return run_planes_big<EPI_BIAS_RES_ELU, 3, 2, 13>(a, s, prec);
         default: return hipErrorInvalidValue;
     }
 }

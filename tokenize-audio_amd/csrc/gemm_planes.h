@@ -50,6 +50,10 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
     static_assert(STAGES >= 2 && STAGES <= 4, "stages");
     static_assert(PPW * (STAGES - 2) <= 63, "vmcnt range");
     static_assert(EPI != EPI_ROPE || (TN % 2 == 0), "rope pairs need even TN");
+    // OUTP: 0 = fp32 C only; 2/3 = that many bf16 planes of the output (+ fp32 C when p.C is set);
+    // | 8 = the planes hold ELU(output) (fp32 C keeps the raw value)
+    constexpr int ONS = OUTP & 7;
+    constexpr bool OELU = (OUTP & 8) != 0;
 
     __shared__ __attribute__((aligned(16))) __bf16 lds[STAGES * STG];
 
@@ -172,12 +176,17 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
         }
     }
 
-    // ---- epilogue: lane holds col (lane&31), rows (r&3) + 8*(r>>2) + 4*(lane>>5) of each 32x32 tile
-    float* __restrict__ Cb = p.C ? p.C + (long long)b * p.c_bstride : nullptr;
-    __bf16* __restrict__ Cpb = OUTP ? reinterpret_cast<__bf16*>(p.Cp) + (long long)b * p.c_bstride : nullptr;
+    // ---- epilogue.  Phase 1 (MFMA layout: lane holds col lane&31, rows (r&3) + 8(r>>2) + 4h of each 32x32
+    // tile): the epilogue math, into a wave-private fp32 tile in the (now idle) LDS ring.  Phase 2: each lane
+    // reads 8 consecutive columns of one row back and stores them as 2 x 16 B fp32 and / or one 16-B bf16x8
+    // per plane -- instead of one scattered 4-B (2-B per plane) store per value.
+    constexpr int CW = TN * 32, LDE = CW + 4, RW = TM * 32;
+    static_assert(NW * RW * LDE * 4 <= STAGES * STG * 2, "epilogue staging fits the ring");
+    __syncthreads();  // every wave is done with the ring
+    float* stg = reinterpret_cast<float*>(lds) + wave * (RW * LDE);
     const float* __restrict__ Rb = p.R ? p.R + (long long)b * p.c_bstride : nullptr;
-    const int rbase = m0 + wm * TM * 32 + 4 * hsel;
-    const int cbase = n0 + wn * TN * 32 + (lane & 31);
+    const int rbase = m0 + wm * RW + 4 * hsel;
+    const int cbase = n0 + wn * CW + (lane & 31);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -191,8 +200,9 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
+                const int lrow = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
                 const int row = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
-                if (row >= M || col >= N) continue;
+                const bool ok = row < M && col < N;
                 float v = acc[i][j][r];
                 const long long off = (long long)row * p.ldc + col;
                 if (EPI == EPI_BIAS || EPI == EPI_BIAS_OUT) {
@@ -200,13 +210,13 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
                 } else if (EPI == EPI_BIAS_ELU) {
                     v = elu1(v + bias);
                 } else if (EPI == EPI_BIAS_RES_ELU) {
-                    v = elu1(Rb[off] + (v + bias));
+                    v = elu1((ok ? Rb[off] : 0.0f) + (v + bias));
                 } else if (EPI == EPI_GELU) {
                     v = gelu_erf(v);
                 } else if (EPI == EPI_SCALE_RES) {
-                    v = Rb[off] + scale * v;
+                    v = (ok ? Rb[off] : 0.0f) + scale * v;
                 } else if (EPI == EPI_ROPE) {
-                    if (col < p.rope_cols) {
+                    if (ok && col < p.rope_cols) {
                         const int d = col % 64;  // head_dim = 64: pairs (d, d + 32) sit in tiles j, j + 1
                         const float c = p.rope_cos[(long long)row * 32 + (d & 31)];
                         const float sn = p.rope_sin[(long long)row * 32 + (d & 31)];
@@ -219,19 +229,43 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
                         }
                     }
                 }
-                if (OUTP) {
-                    float rem = v;
-#pragma unroll
-                    for (int pl = 0; pl < OUTP; ++pl) {
-                        const __bf16 h = (__bf16)rem;
-                        Cpb[pl * p.c_pstride + off] = h;
-                        rem = rem - (float)h;
-                    }
-                    if (Cb) Cb[off] = v;
-                } else {
-                    Cb[off] = v;
-                }
+                stg[lrow * LDE + j * 32 + (lane & 31)] = v;
             }
+        }
+    }
+    float* __restrict__ Cb = p.C ? p.C + (long long)b * p.c_bstride : nullptr;
+    __bf16* __restrict__ Cpb = ONS ? reinterpret_cast<__bf16*>(p.Cp) + (long long)b * p.c_bstride : nullptr;
+    constexpr int LPR = CW / 8;  // lanes per row
+    constexpr int RPP = 64 / LPR;  // rows per pass
+#pragma unroll
+    for (int ps = 0; ps < RW / RPP; ++ps) {
+        const int lr = ps * RPP + lane / LPR, lc = (lane % LPR) * 8;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc + 4);
+        const int row = m0 + wm * RW + lr, col = n0 + wn * CW + lc;
+        if (row >= M || col >= N) continue;  // N % 8 == 0: a lane's 8 columns are all in or all out
+        const long long off = (long long)row * p.ldc + col;
+        if (ONS) {
+            // planes out (of ELU(v) when OELU: the next residual block's conv input), fp32 v beside
+            float rem[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+            if (OELU) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) rem[e] = elu1(rem[e]);
+            }
+#pragma unroll
+            for (int pl = 0; pl < ONS; ++pl) {
+                bf16x8 hv;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    hv[e] = (__bf16)rem[e];
+                    rem[e] = rem[e] - (float)hv[e];
+                }
+                *reinterpret_cast<bf16x8*>(Cpb + pl * p.c_pstride + off) = hv;
+            }
+        }
+        if (Cb) {
+            *reinterpret_cast<f32x4*>(Cb + off) = v0;
+            *reinterpret_cast<f32x4*>(Cb + off + 4) = v1;
         }
     }
 #endif

@@ -97,6 +97,9 @@ enum GemmRole : int {
     ROLE_FC2,        // scale + residual
     ROLE_DOWNSAMPLE, // replicate pad, no bias
     ROLE_INPROJ,     // plain
+    ROLE_DOWN_XE,    // planes path: bias, fp32 out (the residual skip) + ELU(out) planes (the next conv3 input)
+    ROLE_RES3P,      // planes path, unfused residual block: k3 conv, bias + ELU -> h planes
+    ROLE_RES1P,      // planes path, unfused residual block: k1 conv, bias + skip + ELU -> y planes
     ROLE_COUNT
 };
 // Arithmetic of the GEMMs: fp32 MFMA, or fp32 emulated on the bf16 matrix cores with 3 (6 products) or
