@@ -1048,6 +1048,10 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
             ra.yp = w.y;
             ra.y_pstride = (long long)B * T * C;
             ra.yns = ns;
+            if (ns && C == 128) {  // split-bf16 fused block (resblock.hip)
+                ra.w3s = e->res3[si].wsplit;
+                ra.w1s = e->res1[si].wsplit;
+            }
             LAUNCH_TRY(launch_resblock(C, ra, s, &kname), "resblock");
             snprintf(nm, sizeof nm, "res_s%d", si);
             const double H = C / c.compress;

@@ -6,20 +6,14 @@
 
 namespace mimi {
 
-// ELU(x) = x (x > 0), expm1(x) (x <= 0), branchless: degree-8 Taylor on [-0.5, 0] (truncation < 2e-8
-// relative), exp(x) - 1 below it (v_exp_f32; |error| ~1e-7 on a value in [-1, -0.39]).  ~14 VALU instead of
-// ocml expm1f's ~24 plus exec-mask branches; the SEANet applies it to every conv input.
+// ELU(x) = x (x > 0), expm1(x) (x <= 0), branchless, as exp(x) - 1 on the exp unit (v_exp_f32 of x*log2(e)):
+// 4 VALU.  exp(x) - 1 cancels for small |x|, but the error stays ABSOLUTE ~1e-7 (an ulp of 1.0), the size of
+// the fp32 rounding of any O(1) activation, so the block outputs are unchanged at the 1e-6 level (the
+// per-stage parity tests bound it).  The SEANet applies ELU to every conv input and output: it is the
+// dominant VALU cost of the fused residual blocks.
 __device__ __forceinline__ float elu_fast(float x) {
-    float p = x * (1.0f / 40320.0f) + (1.0f / 5040.0f);
-    p = p * x + (1.0f / 720.0f);
-    p = p * x + (1.0f / 120.0f);
-    p = p * x + (1.0f / 24.0f);
-    p = p * x + (1.0f / 6.0f);
-    p = p * x + 0.5f;
-    p = (p * x) * x + x;
     const float e = __expf(x) - 1.0f;
-    const float n = x > -0.5f ? p : e;
-    return x > 0.0f ? x : n;
+    return x > 0.0f ? x : e;
 }
 
 // Activation store in the consumer's format: fp32 (ns == 0) or ns bf16 planes x = x0 + x1 [+ x2] with
@@ -128,6 +122,8 @@ struct ResArgs {
     int yns;
     const float* w3frag;  // optional: W3 / W1 in MFMA-fragment order [ntile][kquad][64 lanes][4] (stage 0)
     const float* w1frag;
+    const void* w3s;      // optional: W3 / W1 as 3 bf16 planes [3][N][K] (split-bf16 fused block, C = 128)
+    const void* w1s;
 };
 hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** kname);
 
