@@ -228,3 +228,36 @@ def test_long_clip_without_planes_matches_prefix(engine):
     n = encoded_length(P) - 2  # the prefix's last frames see its right-edge padding
     assert long_codes.shape == (8, encoded_length(L))
     assert np.array_equal(long_codes[:, :n], pre[:, :n]), (long_codes[:, :n] != pre[:, :n]).sum()
+
+
+def test_split_bf16_fused_block_c128(golden, state_dict, monkeypatch):
+    """The opt-in split-bf16 fused residual block for C = 128 (MIMI_HIP_RES128_SPLIT=1) meets the same bars."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from mimi_hip.model import MimiHipModel
+    arrays, meta = golden
+    monkeypatch.setenv("MIMI_HIP_RES128_SPLIT", "1")
+    eng = MimiHipModel(state_dict, device="cuda:0")
+    x = synthetic.speech_like(240000, meta["audio_seed"], 6)
+    eng.set_taps(True)
+    try:
+        codes = eng.encode(torch.from_numpy(x)[None, None].cuda()).audio_codes[0].cpu().numpy()
+        emb = eng.get_tap("downsample")[0].T
+    finally:
+        eng.set_taps(False)
+    assert rel_err(emb, arrays["emb_speech10s"]) < ACT_TOL
+    frac, bad = margin_audit(codes, arrays["embcodes_speech10s"].astype(np.int64), arrays["margins_speech10s"])
+    assert not bad, (frac, bad[:5])
+    # stage tensors of the 0.5 s clip, through the C = 128 block
+    xs = torch.from_numpy(synthetic.speech_like(12000, meta["audio_seed"], 100))[None, None].cuda()
+    eng.set_taps(True)
+    try:
+        eng.encode(xs, num_quantizers=32)
+        t = eng.get_tap("res1_elu")[0].T[:, ::int([k for k in arrays if k.startswith("stage_res1_sub")][0].rsplit("_sub", 1)[1])]
+    finally:
+        eng.set_taps(False)
+    key = [k for k in arrays if k.startswith("stage_res1_sub")][0]
+    r = arrays[key]
+    r = np.where(r > 0, r, np.expm1(r.astype(np.float64))).astype(np.float32)
+    assert rel_err(t, r) < ACT_TOL
+    eng.close()

@@ -176,6 +176,10 @@ struct mimi_engine {
     // planes path: residual blocks of stages >= unfuse_from run as two plane GEMMs (k3 -> h planes, k1 + skip)
     // instead of the fused fp32-MFMA kernel (MIMI_HIP_UNFUSE_FROM overrides; >= num_ratios disables)
     int unfuse_from = 2;
+    // planes path: split-bf16 persistent fused block for C = 128 (MIMI_HIP_RES128_SPLIT=1).  Off by default: it
+    // is VALU/phase-bound at one workgroup per CU and measured 1.81 ms vs 1.69 ms for the fp32-MFMA fused
+    // kernel at B = 32 x 10 s (profiles/r1_ab_res128.txt)
+    bool res128_split = false;
 
     std::unordered_map<std::string, std::vector<float>> host_w;
     std::unordered_map<std::string, std::vector<int64_t>> expected;  // name -> shape
@@ -360,6 +364,7 @@ extern "C" int mimi_create(const mimi_config* cfg, int device, mimi_engine** out
     if (device < 0 || device >= ndev) return set_err(MIMI_ERR_INVALID_ARGUMENT, "device %d of %d", device, ndev);
     e->device = device;
     if (const char* uf = std::getenv("MIMI_HIP_UNFUSE_FROM")) e->unfuse_from = std::atoi(uf);
+    if (const char* rs = std::getenv("MIMI_HIP_RES128_SPLIT")) e->res128_split = std::atoi(rs) != 0;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipEventCreateWithFlags(&e->ws_free, hipEventDisableTiming));
     build_expected(e.get());
@@ -1048,7 +1053,7 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
             ra.yp = w.y;
             ra.y_pstride = (long long)B * T * C;
             ra.yns = ns;
-            if (ns && C == 128) {  // split-bf16 fused block (resblock.hip)
+            if (ns && C == 128 && e->res128_split) {  // split-bf16 fused block (resblock.hip)
                 ra.w3s = e->res3[si].wsplit;
                 ra.w1s = e->res1[si].wsplit;
             }
