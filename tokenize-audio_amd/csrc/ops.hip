@@ -334,14 +334,14 @@ __device__ __forceinline__ float torch_sqsum(const float* r) {
 }
 
 // Level-parallel form.  One launch per level L over (frame tiles of RVQ_FT) x (code slices of RVQ_CS): every
-// workgroup computes the distances of its 128 frames to its 256 codes (8 waves x 32 codes, 4 MFMA tiles per
-// wave) and writes the slice's (min distance, first index) per frame.  The NEXT launch's prologue
+// workgroup computes the distances of its RVQ_FT frames to its 256 codes (8 waves x 32 codes, RVQ_FT / 32
+// MFMA tiles per wave) and writes the slice's (min distance, first index) per frame.  The NEXT launch's prologue
 // merges the slices of level L-1 (lexicographic (d, idx): the global first-index argmin), writes those codes
 // (slice-0 workgroups), and forms r_L = r_{L-1} - embed_{L-1}[idx] (bitwise the same in every slice's
-// workgroup); a last launch merges level K-1.  8 + 1 launches of 256 workgroups instead of one launch of
-// F/32 = 125 workgroups that left half the CUs idle.  Distances: identical arithmetic and k order to the
+// workgroup); a last launch merges level K-1.  8 + 1 launches of F/64 x 8 = 504 workgroups (B = 32 x 10 s)
+// instead of one launch of F/32 = 125 workgroups that left half the CUs idle.  Distances: identical arithmetic and k order to the
 // reference chain above (|r|^2 from the (-2r)^2 image: scaling by 4 is exact).
-constexpr int RVQ_FT = 128;
+constexpr int RVQ_FT = 64;  // 64 frames: 68 KiB of LDS, two workgroups per CU overlap prologue / MFMA / argmin
 constexpr int RVQ_CS = 256;
 
 size_t rvq_work_bytes(long long frames) {
@@ -470,9 +470,10 @@ __global__ __launch_bounds__(512) void rvq_level_kernel(RvqArgs p, int L) {
     const int code0 = slice * RVQ_CS + wave * 32;
     const int nu = D / 8;
     const float* cbf = p.cb_frag + (long long)L * (p.ncodes / 32) * nu * 256;
-    f32x16 acc[4];
+    constexpr int RT = FT / 32;  // row tiles per wave
+    f32x16 acc[RT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
     const f32x4* bp = reinterpret_cast<const f32x4*>(cbf + (long long)(code0 / 32) * nu * 256) + lane;
@@ -481,17 +482,17 @@ __global__ __launch_bounds__(512) void rvq_level_kernel(RvqArgs p, int L) {
     for (int u = 0; u < nu; ++u) {
         const f32x4 bv = bnext;
         if (u + 1 < nu) bnext = bp[(u + 1) * 64];  // in flight under this step's 16 MFMAs
-        f32x4 av[4];
+        f32x4 av[RT];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) av[i] = *reinterpret_cast<const f32x4*>(&img[h][i * 32 + (lane & 31)][u * 4]);
+        for (int i = 0; i < RT; ++i) av[i] = *reinterpret_cast<const f32x4*>(&img[h][i * 32 + (lane & 31)][u * 4]);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][s], bv[s], acc[i], 0, 0, 0);
+            for (int i = 0; i < RT; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][s], bv[s], acc[i], 0, 0, 0);
     }
     const float yn = p.cb_norm[(long long)L * p.ncodes + code0 + (lane & 31)];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < RT; ++i) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
