@@ -224,20 +224,27 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
         }
         // mask + online softmax for this lane's query
         float cmax = -INFINITY;
+        // wave-uniform: a chunk wholly inside every query's window needs no mask
+        const bool full = c0 + KC - 1 <= qw && c0 > qw + 31 - window && c0 + KC - 1 <= kend;
+        if (full) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int key = c0 + (r & 3) + 8 * (r >> 2) + 4 * hf;
-            const bool ok = key <= qi && key > qi - window && key <= kend;
-            st[r] = ok ? st[r] : -INFINITY;
-            cmax = fmaxf(cmax, st[r]);
+            for (int r = 0; r < 16; ++r) cmax = fmaxf(cmax, st[r]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = c0 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+                const bool ok = key <= qi && key > qi - window && key <= kend;
+                st[r] = ok ? st[r] : -INFINITY;
+                cmax = fmaxf(cmax, st[r]);
+            }
         }
         cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
         const float mnew = fmaxf(m, cmax);
-        const float corr = (m == -INFINITY) ? 0.f : expf(m - mnew);
+        const float corr = (m == -INFINITY) ? 0.f : __expf(m - mnew);  // v_exp_f32: ~1 ulp
         float psum = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const float pv = (st[r] == -INFINITY) ? 0.f : expf(st[r] - mnew);
+            const float pv = (st[r] == -INFINITY) ? 0.f : __expf(st[r] - mnew);
             st[r] = pv;
             psum += pv;
         }
