@@ -231,6 +231,44 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_f32_kernel(GemmArgs p) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
+// K-step order of the implicit-GEMM convs.  A K step reads a 64-B half line (32 channels) of one tap of
+// every tile row.  Tap kk + s of output row m reads the input row that tap kk of row m + 1 reads, so each
+// 128-B input line is touched 4 times per tile: 2 channel halves x 2 taps (k = 2s; 3 x 2 for k = 3, s = 1).
+// Order (outer -> inner): chain start j < s, 128-B channel block hi, position c in the tap chain
+// j, j+s, j+2s, ..., channel half lo -- so the 4 (6) touches of a line are consecutive K steps (L2 hits)
+// instead of up to k*Cin/64 steps apart (with 30+ CUs streaming through an XCD's 4 MB L2 in between: HBM
+// re-reads).  Linear layers (k = 1) get the plain order; layouts it does not cover too.  Wave-uniform state
+// (SGPRs); advance with next() once per K step.
+struct KOrder {
+    int cin, s, cl, nhi, nlo, j, hi, c, lo;
+    __device__ __forceinline__ void init(const GemmArgs& p) {
+        j = hi = c = lo = 0;
+        const int k = p.a_cin > 0 ? p.K / p.a_cin : 0;
+        const int st = p.a_cin > 0 ? p.a_rs / p.a_cin : 0;
+        if (p.a_cin % 64 == 0 && k * p.a_cin == p.K && st > 0 && st * p.a_cin == p.a_rs && k % st == 0) {
+            cin = p.a_cin;
+            s = st;
+            cl = k / st;
+        } else {  // plain order: one "tap" spanning all of K
+            cin = 0;
+            s = 1;
+            cl = 1;
+        }
+        nlo = (cin || p.K % 64 == 0) ? 2 : 1;
+        nhi = (cin ? cin : p.K) / (32 * nlo);
+    }
+    __device__ __forceinline__ int offset() const { return (j + c * s) * cin + (hi * nlo + lo) * 32; }
+    __device__ __forceinline__ void next() {
+        if (++lo < nlo) return;
+        lo = 0;
+        if (++c < cl) return;
+        c = 0;
+        if (++hi < nhi) return;
+        hi = 0;
+        ++j;
+    }
+};
+
 template <int NS>
 __device__ __forceinline__ void split_bf16x4(f32x4 v, bf16x4 (&out)[NS]) {
 #pragma unroll
@@ -377,16 +415,20 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_bf16x_kernel(GemmArgs p) {
             *reinterpret_cast<bf16x4*>(dst + pl * BM * LDB) = h[pl];                           \
     }
 
-    MIMI_SPLIT_LOAD_A(0)
-    MIMI_SPLIT_DMA_B(0, 0)
+    KOrder ko;
+    ko.init(p);
+    MIMI_SPLIT_LOAD_A(ko.offset())
+    MIMI_SPLIT_DMA_B(ko.offset(), 0)
     MIMI_SPLIT_STORE_A()
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int kt = 0; kt < KT; ++kt) {
         const int cur = kt & 1;
         if (kt + 1 < KT) {
-            MIMI_SPLIT_LOAD_A((kt + 1) * BK)
-            MIMI_SPLIT_DMA_B((kt + 1) * BK, cur ^ 1)
+            ko.next();
+            const int k1 = ko.offset();
+            MIMI_SPLIT_LOAD_A(k1)
+            MIMI_SPLIT_DMA_B(k1, cur ^ 1)
         }
         const __bf16* Bs = Bs0 + cur * NS * BPL;
 #pragma unroll

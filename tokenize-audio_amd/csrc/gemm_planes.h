@@ -100,9 +100,13 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
         bsrc[q] = Wp + ((long long)pl * N + n) * K + c * 8;
     }
 
-    auto issue = [&](int kt, int stage) {
+    KOrder ko;  // K steps are issued in order: the cursor follows the issues
+    ko.init(p);
+    auto issue = [&](int stage) {
         __bf16* st = lds + stage * STG;
-        const int kb = kt * BK * 2;  // bytes
+        const int k0 = ko.offset();
+        ko.next();
+        const int kb = k0 * 2;  // bytes
 #pragma unroll
         for (int q = 0; q < APW; ++q) {
             const int j = wave + q * NW;
@@ -115,7 +119,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
         for (int q = 0; q < BPW; ++q) {
             const int j = wave + q * NW;
             const int pl = j / (BN / 16), rb = j % (BN / 16);
-            __builtin_amdgcn_global_load_lds((const void*)(bsrc[q] + kt * BK),
+            __builtin_amdgcn_global_load_lds((const void*)(bsrc[q] + k0),
                                              (__attribute__((address_space(3))) void*)(st + NS * APL + pl * BPL +
                                                                                         rb * 16 * BK),
                                              16, 0, 0);
@@ -137,7 +141,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
 
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
-        if (s < KT) issue(s, s);
+        if (s < KT) issue(s);
 
     for (int kt = 0; kt < KT; ++kt) {
         // retire this wave's pieces of stage kt; the later stages stay in flight
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
         }
         __builtin_amdgcn_s_barrier();
         // the stage consumed in step kt-1 is free: refill it with step kt + STAGES - 1
-        if (kt + STAGES - 1 < KT) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+        if (kt + STAGES - 1 < KT) issue((kt + STAGES - 1) % STAGES);
         const __bf16* As = lds + (kt % STAGES) * STG;
         const __bf16* Bs = As + NS * APL;
 #pragma unroll
