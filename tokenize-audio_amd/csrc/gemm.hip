@@ -142,7 +142,9 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         case ROLE_FC2: return run_planes_small<EPI_SCALE_RES, 8>(a, s, prec);
         case ROLE_DOWN_XE: return run_planes_big<EPI_BIAS, 3 | 8, 2 | 8, 11>(a, s, prec);
         case ROLE_RES3P: return run_planes_big<EPI_BIAS_ELU, 3, 2, 12>(a, s, prec);
-        case ROLE_RES1P: return run_planes_big<EPI_BIAS_RES_ELU, 3, 2, 13>(a, s, prec);
+        case ROLE_RES1P:  // K = C/2 = 128 / 256: short K, output-heavy -> 74 KiB tiles, two workgroups per CU
+            if (prec == PREC_BF16X6) return run_planes<128, 64, 2, 2, 3, 2, EPI_BIAS_RES_ELU, 3, 13>(a, s);
+            return run_planes<128, 64, 2, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13>(a, s);
         default: return hipErrorInvalidValue;
     }
 }

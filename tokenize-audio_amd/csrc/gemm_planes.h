@@ -208,17 +208,16 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
                 const int row = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
                 const bool ok = row < M && col < N;
                 float v = acc[i][j][r];
-                const long long off = (long long)row * p.ldc + col;
                 if (EPI == EPI_BIAS || EPI == EPI_BIAS_OUT) {
                     v = v + bias;
                 } else if (EPI == EPI_BIAS_ELU) {
                     v = elu1(v + bias);
                 } else if (EPI == EPI_BIAS_RES_ELU) {
-                    v = elu1((ok ? Rb[off] : 0.0f) + (v + bias));
+                    v = v + bias;  // + R and ELU in phase 2 (vector R loads)
                 } else if (EPI == EPI_GELU) {
                     v = gelu_erf(v);
                 } else if (EPI == EPI_SCALE_RES) {
-                    v = (ok ? Rb[off] : 0.0f) + scale * v;
+                    v = scale * v;  // + R in phase 2
                 } else if (EPI == EPI_ROPE) {
                     if (ok && col < p.rope_cols) {
                         const int d = col % 64;  // head_dim = 64: pairs (d, d + 32) sit in tiles j, j + 1
@@ -244,11 +243,21 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
 #pragma unroll
     for (int ps = 0; ps < RW / RPP; ++ps) {
         const int lr = ps * RPP + lane / LPR, lc = (lane % LPR) * 8;
-        const f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc);
-        const f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc + 4);
+        f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc);
+        f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc + 4);
         const int row = m0 + wm * RW + lr, col = n0 + wn * CW + lc;
         if (row >= M || col >= N) continue;  // N % 8 == 0: a lane's 8 columns are all in or all out
         const long long off = (long long)row * p.ldc + col;
+        if (EPI == EPI_BIAS_RES_ELU || EPI == EPI_SCALE_RES) {
+            const f32x4 r0 = *reinterpret_cast<const f32x4*>(Rb + off);
+            const f32x4 r1 = *reinterpret_cast<const f32x4*>(Rb + off + 4);
+            v0 = r0 + v0;  // R + (acc + bias) / R + scale * acc: the reference's operation order
+            v1 = r1 + v1;
+            if (EPI == EPI_BIAS_RES_ELU) {
+                v0.x = elu1(v0.x); v0.y = elu1(v0.y); v0.z = elu1(v0.z); v0.w = elu1(v0.w);
+                v1.x = elu1(v1.x); v1.y = elu1(v1.y); v1.z = elu1(v1.z); v1.w = elu1(v1.w);
+            }
+        }
         if (ONS) {
             // planes out (of ELU(v) when OELU: the next residual block's conv input), fp32 v beside
             float rem[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
