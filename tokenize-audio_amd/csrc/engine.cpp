@@ -783,7 +783,8 @@ static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspa
     size_t xmax = 0, ymax = 0, xemax = 0;
     int C = c.num_filters;
     for (int s = 0; s < c.num_ratios; ++s) {
-        xmax = std::max(xmax, (size_t)p.T[s] * C);
+        // x at stage 0 only holds the conv0 tap (the stage-0 block recomputes conv0 from the audio)
+        if (s > 0 || e->taps) xmax = std::max(xmax, (size_t)p.T[s] * C);
         ymax = std::max(ymax, (size_t)p.T[s] * C);
         if (ns && s >= e->unfuse_from && s > 0) xemax = std::max(xemax, (size_t)p.T[s] * C);
         C *= 2;
