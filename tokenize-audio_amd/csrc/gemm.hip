@@ -59,12 +59,12 @@ static hipError_t run_split(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int ST, int EPI, int OUTP, int TAG>
+template <int BM, int BN, int WM, int WN, int NS, int ST, int EPI, int OUTP, int TAG, int LW = 0>
 static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
     static char name[160];
     if (!name[0])
-        snprintf(name, sizeof(name), "mimi::gemm_planes_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d>", BM, BN, WM, WN, NS,
-                 ST, EPI, OUTP, TAG);
+        snprintf(name, sizeof(name), "mimi::gemm_planes_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d>", BM, BN, WM, WN,
+                 NS, ST, EPI, OUTP, TAG, LW);
     g_last_kernel = name;
     if (a.K % 32 != 0 || !a.Wsplit || !a.Ap || ((OUTP & 7) && !a.Cp) || (!(OUTP & 7) && !a.C) ||
         ((OUTP & 8) && !a.C) || (EPI == EPI_BIAS_RES_ELU && !a.R))
@@ -74,24 +74,35 @@ static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
     if (a.N % 8 || a.ldc % 8 || a.c_bstride % 8 || a.c_pstride % 8) return hipErrorInvalidValue;
     const long long nwg = (long long)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.batch;
     if (nwg > 0x7fffffffLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG>), dim3((unsigned)nwg),
-                       dim3(WM * WN * 64), 0, s, a);
+    hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW>), dim3((unsigned)nwg),
+                       dim3((WM * WN + LW) * 64), 0, s, a);
     return hipGetLastError();
 }
 
-// Tiles of the planes kernel (tools/gemm_bench.hip, profiles/r1_gemm_bench_planes*.log): 256x128 with 8 waves
-// (2 stages at NS = 3 / 3 stages at NS = 2, 144 KiB LDS) where M x N is large (down convs, fc1); 128x128 with
-// 8 waves of 32x64 (3 stages, 2 waves per SIMD) where a 256-row tile would leave CUs idle (final conv, q/k/v,
-// o_proj, fc2: M = B*250 rows).
+// Tiles of the planes kernel (tools/gemm_bench.hip; profiles/r1_gemm_bench_planes*.log, r1_gemm_bench_ws.log):
+//   big:    256x128, 8 compute waves, 2 stages (NS = 3; 3 at NS = 2), 144 KiB LDS: down convs, k3 convs, fc1
+//   big_ld: 256x128, 4 compute waves of 128x64 + 4 loader waves (warp-specialised DMA): down_s3
+//   small:  128x128, 8 compute waves of 32x64, 3 stages: final conv, q/k/v (M = B*250 rows)
+//   small_ld: 128x128, 4 compute waves of 64x64 + 4 loader waves, 3 stages: o_proj, fc2
 template <int EPI, int OUTP3, int OUTP2, int TAG>
 static hipError_t run_planes_big(const GemmArgs& a, hipStream_t s, int prec) {
     if (prec == PREC_BF16X6) return run_planes<256, 128, 4, 2, 3, 2, EPI, OUTP3, TAG>(a, s);
     return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP2, TAG>(a, s);
 }
+template <int EPI, int OUTP3, int OUTP2, int TAG>
+static hipError_t run_planes_big_ld(const GemmArgs& a, hipStream_t s, int prec) {
+    if (prec == PREC_BF16X6) return run_planes<256, 128, 2, 2, 3, 2, EPI, OUTP3, TAG, 4>(a, s);
+    return run_planes<256, 128, 2, 2, 2, 3, EPI, OUTP2, TAG, 4>(a, s);
+}
 template <int EPI, int TAG>
 static hipError_t run_planes_small(const GemmArgs& a, hipStream_t s, int prec) {
     if (prec == PREC_BF16X6) return run_planes<128, 128, 4, 2, 3, 3, EPI, 0, TAG>(a, s);
     return run_planes<128, 128, 4, 2, 2, 3, EPI, 0, TAG>(a, s);
+}
+template <int EPI, int TAG>
+static hipError_t run_planes_small_ld(const GemmArgs& a, hipStream_t s, int prec) {
+    if (prec == PREC_BF16X6) return run_planes<128, 128, 2, 2, 3, 3, EPI, 0, TAG, 4>(a, s);
+    return run_planes<128, 128, 2, 2, 2, 3, EPI, 0, TAG, 4>(a, s);
 }
 
 template <bool ELU_IN, int PAD, int EPI, int TAG>
@@ -134,12 +145,12 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
     if (prec != PREC_BF16X6 && prec != PREC_BF16X3) return hipErrorInvalidValue;
     switch (role) {
         case ROLE_DOWN: return run_planes_big<EPI_BIAS, 0, 0, 2>(a, s, prec);
-        case ROLE_DOWN_ELU: return run_planes_big<EPI_BIAS_ELU, 3, 2, 3>(a, s, prec);  // planes out: final conv
+        case ROLE_DOWN_ELU: return run_planes_big_ld<EPI_BIAS_ELU, 3, 2, 3>(a, s, prec);  // planes out: final conv
         case ROLE_FINAL: return run_planes_small<EPI_BIAS_OUT, 4>(a, s, prec);
         case ROLE_QKV: return run_planes_small<EPI_ROPE, 5>(a, s, prec);
-        case ROLE_OPROJ: return run_planes_small<EPI_SCALE_RES, 6>(a, s, prec);
+        case ROLE_OPROJ: return run_planes_small_ld<EPI_SCALE_RES, 6>(a, s, prec);
         case ROLE_FC1: return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);  // planes out: fc2
-        case ROLE_FC2: return run_planes_small<EPI_SCALE_RES, 8>(a, s, prec);
+        case ROLE_FC2: return run_planes_small_ld<EPI_SCALE_RES, 8>(a, s, prec);
         case ROLE_DOWN_XE: return run_planes_big<EPI_BIAS, 3 | 8, 2 | 8, 11>(a, s, prec);
         case ROLE_RES3P: return run_planes_big<EPI_BIAS_ELU, 3, 2, 12>(a, s, prec);
         case ROLE_RES1P:  // K = C/2 = 128 / 256: short K, output-heavy -> 74 KiB tiles, two workgroups per CU

@@ -34,19 +34,24 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int STAGES, int EPI, int OUTP, int TAG>
-__global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
+// LW > 0: warp-specialised -- LW extra loader waves issue every LDS-DMA piece and do the counted waits, the
+// WM x WN compute waves only ds_read and MFMA (an LDS-DMA piece costs its issuing wave ~60-185 cycles,
+// MI355X_MICROARCH.md; with LW = 0 the compute waves pay it between their MFMAs).  Both kinds meet at the one
+// barrier per K step.
+template <int BM, int BN, int WM, int WN, int NS, int STAGES, int EPI, int OUTP, int TAG, int LW = 0>
+__global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmArgs p) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
     constexpr int NW = WM * WN;
+    constexpr int NLD = LW > 0 ? LW : NW;        // waves issuing DMA
     constexpr int BK = 32;
     constexpr int TM = BM / WM / 32;
     constexpr int TN = BN / WN / 32;
     constexpr int APL = BM * BK, BPL = BN * BK;  // bf16 per plane image
     constexpr int STG = NS * (APL + BPL);        // bf16 per stage
-    constexpr int APW = NS * BM / 16 / NW;       // A pieces per wave per stage
-    constexpr int BPW = NS * BN / 16 / NW;       // B pieces per wave per stage
+    constexpr int APW = NS * BM / 16 / NLD;      // A pieces per loading wave per stage
+    constexpr int BPW = NS * BN / 16 / NLD;      // B pieces per loading wave per stage
     constexpr int PPW = APW + BPW;
-    static_assert(APW * NW * 16 == NS * BM && BPW * NW * 16 == NS * BN, "pieces must split evenly over waves");
+    static_assert(APW * NLD * 16 == NS * BM && BPW * NLD * 16 == NS * BN, "pieces must split evenly over waves");
     static_assert(STAGES >= 2 && STAGES <= 4, "stages");
     static_assert(PPW * (STAGES - 2) <= 63, "vmcnt range");
     static_assert(EPI != EPI_ROPE || (TN % 2 == 0), "rope pairs need even TN");
@@ -60,8 +65,11 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps rsrc/LDS bases in SGPRs
-    const int wm = wave / WN;
-    const int wn = wave % WN;
+    const bool loader = LW == 0 || wave >= NW;
+    const bool compute = LW == 0 || wave < NW;
+    const int ldw = LW > 0 ? (loader ? wave - NW : 0) : wave;  // index among the loading waves
+    const int wm = compute ? wave / WN : 0;
+    const int wn = compute ? wave % WN : 0;
     const int M = p.M, N = p.N, K = p.K;
     const int MT = (M + BM - 1) / BM, NTn = (N + BN - 1) / BN;
     const int logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -79,7 +87,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
     int aoff[APW];  // byte offset of this lane's chunk at k0 = 0 (may be negative: reads 0)
 #pragma unroll
     for (int q = 0; q < APW; ++q) {
-        const int j = wave + q * NW;
+        const int j = ldw + q * NLD;
         const int rb = j % (BM / 16);
         const int row = rb * 16 + (lane >> 2);
         const int c = (lane & 3) ^ ((row >> 2) & 3);
@@ -91,7 +99,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
     const __bf16* bsrc[BPW];
 #pragma unroll
     for (int q = 0; q < BPW; ++q) {
-        const int j = wave + q * NW;
+        const int j = ldw + q * NLD;
         const int pl = j / (BN / 16), rb = j % (BN / 16);
         const int row = rb * 16 + (lane >> 2);
         const int c = (lane & 3) ^ ((row >> 2) & 3);
@@ -109,7 +117,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
         const int kb = k0 * 2;  // bytes
 #pragma unroll
         for (int q = 0; q < APW; ++q) {
-            const int j = wave + q * NW;
+            const int j = ldw + q * NLD;
             const int pl = j / (BM / 16), rb = j % (BM / 16);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 arsrc[pl], (__attribute__((address_space(3))) void*)(st + pl * APL + rb * 16 * BK), 16,
@@ -117,7 +125,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
         }
 #pragma unroll
         for (int q = 0; q < BPW; ++q) {
-            const int j = wave + q * NW;
+            const int j = ldw + q * NLD;
             const int pl = j / (BN / 16), rb = j % (BN / 16);
             __builtin_amdgcn_global_load_lds((const void*)(bsrc[q] + k0),
                                              (__attribute__((address_space(3))) void*)(st + NS * APL + pl * BPL +
@@ -139,23 +147,28 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
     const int brow = wn * TN * 32 + (lane & 31);
     const int hsel = lane >> 5;
 
+    if (loader) {
 #pragma unroll
-    for (int s = 0; s < STAGES - 1; ++s)
-        if (s < KT) issue(s);
+        for (int s = 0; s < STAGES - 1; ++s)
+            if (s < KT) issue(s);
+    }
 
     for (int kt = 0; kt < KT; ++kt) {
-        // retire this wave's pieces of stage kt; the later stages stay in flight
-        const int later = min(STAGES - 2, KT - 1 - kt);
-        if (STAGES >= 4 && later >= 2) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
-        } else if (STAGES >= 3 && later >= 1) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (loader) {
+            // retire this wave's pieces of stage kt; the later stages stay in flight
+            const int later = min(STAGES - 2, KT - 1 - kt);
+            if (STAGES >= 4 && later >= 2) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+            } else if (STAGES >= 3 && later >= 1) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
         }
         __builtin_amdgcn_s_barrier();
         // the stage consumed in step kt-1 is free: refill it with step kt + STAGES - 1
-        if (kt + STAGES - 1 < KT) issue((kt + STAGES - 1) % STAGES);
+        if (loader && kt + STAGES - 1 < KT) issue((kt + STAGES - 1) % STAGES);
+        if (!compute) continue;
         const __bf16* As = lds + (kt % STAGES) * STG;
         const __bf16* Bs = As + NS * APL;
 #pragma unroll
@@ -187,6 +200,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_planes_kernel(GemmArgs p) {
     constexpr int CW = TN * 32, LDE = CW + 4, RW = TM * 32;
     static_assert(NW * RW * LDE * 4 <= STAGES * STG * 2, "epilogue staging fits the ring");
     __syncthreads();  // every wave is done with the ring
+    if (!compute) return;
     float* stg = reinterpret_cast<float*>(lds) + wave * (RW * LDE);
     const float* __restrict__ Rb = p.R ? p.R + (long long)b * p.c_bstride : nullptr;
     const int rbase = m0 + wm * RW + 4 * hsel;

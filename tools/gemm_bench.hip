@@ -44,11 +44,11 @@ void launch_bf(const GemmArgs& a, hipStream_t s) {
                        dim3(WM * WN * 64), 0, s, a);
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int ST>
+template <int BM, int BN, int WM, int WN, int NS, int ST, int LW = 0>
 void launch_pl(const GemmArgs& a, hipStream_t s) {
     const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.batch;
-    hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI_BIAS, 0, 0>), dim3(nwg),
-                       dim3(WM * WN * 64), 0, s, a);
+    hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI_BIAS, 0, 0, LW>), dim3(nwg),
+                       dim3((WM * WN + LW) * 64), 0, s, a);
 }
 
 __global__ void split_planes(const float* x, __bf16* out, long long n) {
@@ -93,26 +93,13 @@ int main(int argc, char** argv) {
     };
     Variant vars[] = {
         {"f32 128x128 bk32 nb1", launch<128, 128, 2, 2, 32, 1, false>, 32, 0},
-        {"f32 256x128 8w", launch<256, 128, 4, 2, 32, 1, false>, 32, 0},
-        {"bf16x3p 128x128", launch_bf<128, 128, 2, 2, 3>, 32, 3},
-        {"bf16x3p 256x128 8w", launch_bf<256, 128, 4, 2, 3>, 32, 3},
-        {"bf16x3p 128x256 8w", launch_bf<128, 256, 2, 4, 3>, 32, 3},
-        {"bf16x3p 64x128", launch_bf<64, 128, 1, 2, 3>, 32, 3},
-        {"bf16x3p 256x256 8w", launch_bf<256, 256, 4, 2, 3>, 32, 3},
-        {"bf16x2p 128x128", launch_bf<128, 128, 2, 2, 2>, 32, 2},
-        {"bf16x2p 256x128 8w", launch_bf<256, 128, 4, 2, 2>, 32, 2},
-        {"bf16x2p 256x256 8w", launch_bf<256, 256, 4, 2, 2>, 32, 2},
-        {"planes3 128x128 s3", launch_pl<128, 128, 2, 2, 3, 3>, 32, 3},
-        {"planes3 128x128 s2", launch_pl<128, 128, 2, 2, 3, 2>, 32, 3},
         {"planes3 256x128 8w s2", launch_pl<256, 128, 4, 2, 3, 2>, 32, 3},
-        {"planes3 128x64 s3", launch_pl<128, 64, 2, 2, 3, 3>, 32, 3},
-        {"planes3 64x128 s3", launch_pl<64, 128, 1, 2, 3, 3>, 32, 3},
+        {"planes3 256x128 8w s2 +4ld", launch_pl<256, 128, 4, 2, 3, 2, 4>, 32, 3},
+        {"planes3 256x128 8w s2 +2ld", launch_pl<256, 128, 4, 2, 3, 2, 2>, 32, 3},
         {"planes3 128x128 8w s3", launch_pl<128, 128, 4, 2, 3, 3>, 32, 3},
-        {"planes3 128x128 8w24 s3", launch_pl<128, 128, 2, 4, 3, 3>, 32, 3},
-        {"planes3 256x128 4w s2", launch_pl<256, 128, 2, 2, 3, 2>, 32, 3},
-        {"planes3 128x256 8w s2", launch_pl<128, 256, 2, 4, 3, 2>, 32, 3},
-        {"planes2 128x128 s3", launch_pl<128, 128, 2, 2, 2, 3>, 32, 2},
-        {"planes2 256x128 8w s3", launch_pl<256, 128, 4, 2, 2, 3>, 32, 2},
+        {"planes3 128x128 8w s3 +4ld", launch_pl<128, 128, 4, 2, 3, 3, 4>, 32, 3},
+        {"planes3 128x128 4w s3 +4ld", launch_pl<128, 128, 2, 2, 3, 3, 4>, 32, 3},
+        {"planes3 256x128 4w s2 +4ld", launch_pl<256, 128, 2, 2, 3, 2, 4>, 32, 3},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
