@@ -144,6 +144,68 @@ hipError_t launch_layernorm(const float* x, const float* g, const float* b, floa
 // from the S^T accumulator registers as the B operand (no shuffles, no LDS round trip).  Q is pre-scaled
 // by 1/sqrt(64) = 1/8 (exact).  Online softmax with running max / sum per query, fp32 throughout.
 // ------------------------------------------------------------------------------------------------
+// One 32-key chunk of the online-softmax attention for the wave's 32 queries (S^T = K . Q^T with keys on
+// rows, queries on lanes; O^T += V^T . P^T).  Ks / Vs: the chunk's K rows (stride D + 4) and V rows (stride D)
+// in LDS; keys c0 .. c0 + 31, masked to key <= query, key > query - window, key <= kend.
+__device__ __forceinline__ void attn_chunk(f32x16 (&o)[2], float& m, float& l, const f32x4 (&qf)[8],
+                                           const float* Ks, const float* Vs, int c0, int qw, int qi, int kend,
+                                           int window, int hf, int col) {
+    constexpr int D = 64, KC = 32, LDKS = D + 4;
+    // S^T[key][query]
+    f32x16 st;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st[r] = 0.f;
+#pragma unroll
+    for (int kq = 0; kq < 8; ++kq) {
+        const f32x4 kf = *reinterpret_cast<const f32x4*>(Ks + col * LDKS + kq * 8 + hf * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) st = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[s], qf[kq][s], st, 0, 0, 0);
+    }
+    // mask + online softmax for this lane's query
+    float cmax = -INFINITY;
+    // wave-uniform: a chunk wholly inside every query's window needs no mask
+    const bool full = c0 + KC - 1 <= qw && c0 > qw + 31 - window && c0 + KC - 1 <= kend;
+    if (full) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cmax = fmaxf(cmax, st[r]);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = c0 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            const bool ok = key <= qi && key > qi - window && key <= kend;
+            st[r] = ok ? st[r] : -INFINITY;
+            cmax = fmaxf(cmax, st[r]);
+        }
+    }
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
+    const float mnew = fmaxf(m, cmax);
+    const float corr = (m == -INFINITY) ? 0.f : __expf(m - mnew);  // v_exp_f32: ~1 ulp
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float pv = (st[r] == -INFINITY) ? 0.f : __expf(st[r] - mnew);
+        st[r] = pv;
+        psum += pv;
+    }
+    psum += __shfl_xor(psum, 32);
+    l = l * corr + psum;
+    m = mnew;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] *= corr;
+    // O^T[d][query] += V^T . P^T : step r pairs key (r&3)+8(r>>2) (half 0) with +4 (half 1)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int key = (r & 3) + 8 * (r >> 2) + 4 * hf;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const float va = Vs[key * D + t * 32 + col];
+            o[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(va, st[r], o[t], 0, 0, 0);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict__ qkv, float* __restrict__ out,
                                                         int T, int H, int window, float scale,
                                                         void* __restrict__ outp, long long pstride, int outns) {
@@ -212,59 +274,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
         if (c0 + KC <= kend) fetch(c0 + KC);
         // skip chunks entirely outside this wave's band [qw - W + 1, qw + 31]
         if (c0 > qw + 31 || c0 + KC - 1 < qw - window + 1) continue;
-        // S^T[key][query]
-        f32x16 st;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) st[r] = 0.f;
-#pragma unroll
-        for (int kq = 0; kq < 8; ++kq) {
-            const f32x4 kf = *reinterpret_cast<const f32x4*>(Ks + col * LDKS + kq * 8 + hf * 4);
-#pragma unroll
-            for (int s = 0; s < 4; ++s) st = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[s], qf[kq][s], st, 0, 0, 0);
-        }
-        // mask + online softmax for this lane's query
-        float cmax = -INFINITY;
-        // wave-uniform: a chunk wholly inside every query's window needs no mask
-        const bool full = c0 + KC - 1 <= qw && c0 > qw + 31 - window && c0 + KC - 1 <= kend;
-        if (full) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) cmax = fmaxf(cmax, st[r]);
-        } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int key = c0 + (r & 3) + 8 * (r >> 2) + 4 * hf;
-                const bool ok = key <= qi && key > qi - window && key <= kend;
-                st[r] = ok ? st[r] : -INFINITY;
-                cmax = fmaxf(cmax, st[r]);
-            }
-        }
-        cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
-        const float mnew = fmaxf(m, cmax);
-        const float corr = (m == -INFINITY) ? 0.f : __expf(m - mnew);  // v_exp_f32: ~1 ulp
-        float psum = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float pv = (st[r] == -INFINITY) ? 0.f : __expf(st[r] - mnew);
-            st[r] = pv;
-            psum += pv;
-        }
-        psum += __shfl_xor(psum, 32);
-        l = l * corr + psum;
-        m = mnew;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[t][r] *= corr;
-        // O^T[d][query] += V^T . P^T : step r pairs key (r&3)+8(r>>2) (half 0) with +4 (half 1)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int key = (r & 3) + 8 * (r >> 2) + 4 * hf;
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const float va = Vs[key * D + t * 32 + col];
-                o[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(va, st[r], o[t], 0, 0, 0);
-            }
-        }
+        attn_chunk(o, m, l, qf, Ks, Vs, c0, qw, qi, kend, window, hf, col);
     }
     // O^T -> LDS (per wave) -> coalesced rows of out[b][q][h*64 + d]
     const float inv = (l > 0.f) ? 1.0f / l : 0.f;
@@ -283,9 +293,94 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
     }
 }
 
+// T <= 256 (every 10 s clip: T = 250): one workgroup per (head, batch item) with the item's whole K and V
+// resident in LDS (loaded once, 128 KiB), 8 waves x 32 queries and no per-chunk barriers.  Wave w takes query
+// tile w (w < 4) or 11 - w, so the two waves sharing a SIMD (w, w + 4) own 9 causal chunks between them.
+__global__ __launch_bounds__(512) void attention_t256_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                             int T, int H, int window, float scale,
+                                                             void* __restrict__ outp, long long pstride, int outns) {
+    constexpr int D = 64, LDKS = D + 4, LDO = D + 1, TM = 256;
+    __shared__ __attribute__((aligned(16))) float lds[TM * LDKS + TM * D];
+    float* Ks = lds;
+    float* Vs = lds + TM * LDKS;
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hf = lane >> 5, col = lane & 31;
+    const long long ld = 3LL * H * D;
+    const float* base = qkv + (long long)b * T * ld;
+    // K / V rows 0 .. 255 (zeros past T): 2 x 16 float4 per thread, all in flight before the first store
+    {
+        constexpr int PER = TM * (D / 4) / 512;  // 8
+        f32x4 kv[PER], vv[PER];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int idx = tid + q * 512;
+            const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
+            const int rr = r < T ? r : T - 1;
+            const f32x4 k4 = *reinterpret_cast<const f32x4*>(base + (long long)rr * ld + H * D + h * D + c);
+            const f32x4 v4 = *reinterpret_cast<const f32x4*>(base + (long long)rr * ld + 2 * H * D + h * D + c);
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            kv[q] = r < T ? k4 : z;
+            vv[q] = r < T ? v4 : z;
+        }
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int idx = tid + q * 512;
+            const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
+            *reinterpret_cast<f32x4*>(Ks + r * LDKS + c) = kv[q];
+            *reinterpret_cast<f32x4*>(Vs + r * D + c) = vv[q];
+        }
+    }
+    const int qt = wave < 4 ? wave : 11 - wave;
+    const int qw = qt * 32;
+    const int qi = qw + col;
+    f32x4 qf[8];
+#pragma unroll
+    for (int kq = 0; kq < 8; ++kq) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (qi < T) v = *reinterpret_cast<const f32x4*>(base + (long long)qi * ld + h * D + kq * 8 + hf * 4);
+        qf[kq] = v * scale;
+    }
+    f32x16 o[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    __syncthreads();
+    const int kend = min(T - 1, qw + 31);
+    if (qw < T) {
+        const int kstart = max(0, qw - window + 1) & ~31;
+        for (int c0 = kstart; c0 <= kend; c0 += 32)
+            attn_chunk(o, m, l, qf, Ks + c0 * LDKS, Vs + c0 * D, c0, qw, qi, kend, window, hf, col);
+    }
+    __syncthreads();  // K / V dead: the output staging reuses the LDS
+    float* ow = lds + wave * 32 * LDO;
+    const float inv = (l > 0.f) ? 1.0f / l : 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            ow[col * LDO + d] = o[t][r] * inv;
+        }
+    // same wave wrote and reads its staging rows: LDS order, no barrier
+    for (int qq = 0; qq < 32; ++qq) {
+        const int q = qw + qq;
+        if (q < T)
+            store_act(out, outp, pstride, outns, ((long long)b * T + q) * (H * D) + h * D + lane, ow[qq * LDO + lane]);
+    }
+}
+
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window, float scale,
                             hipStream_t s, void* outp, long long out_pstride, int outns) {
     if (D != 64 || (outns != 0 && !outp)) return hipErrorInvalidValue;
+    if (T <= 256) {
+        hipLaunchKernelGGL(attention_t256_kernel, dim3(H, batch), dim3(512), 0, s, qkv, out, T, H, window, scale,
+                           outp, out_pstride, outns);
+        return hipGetLastError();
+    }
     dim3 grid((T + 127) / 128, H, batch);
     hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, qkv, out, T, H, window, scale, outp, out_pstride,
                        outns);
