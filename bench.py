@@ -37,9 +37,12 @@ def mfma_peak_for(kernel: str):
     as P bf16 products per fp32 multiply-add (NS = 3 planes -> 6 products, NS = 2 -> 3) on the dense bf16
     MFMA, so their ceiling is 2.5 PF / P (416.7 TF for bf16x6, 833.3 TF for bf16x3)."""
     if "gemm_bf16x_kernel<" in kernel or "gemm_planes_kernel<" in kernel:
-        ns = int(kernel.split("<", 1)[1].split(",")[4])
+        targs = [t.strip() for t in kernel.split("<", 1)[1].rstrip(">").split(",")]
+        ns = int(targs[4])
         products = {3: 6, 2: 3}[ns]
-        return BF16_PEAK_TFLOPS / products, f"bf16 MFMA dense peak / {products} products (split-bf16, {ns} planes)"
+        kind = "fp16" if targs[-1] == "true" else "bf16"
+        return BF16_PEAK_TFLOPS / products, (f"{kind} MFMA dense peak (= bf16 rate) / {products} products "
+                                             f"(split-{kind}, {ns} planes)")
     return FP32_PEAK_TFLOPS, "fp32 MFMA peak"
 
 
@@ -55,6 +58,7 @@ def parse():
                     help="wall budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage events")
+    ap.add_argument("--precision", default=None, help="GEMM precision mode (default: the engine's)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -114,6 +118,8 @@ def main():
     B = args.batch
     L = int(round(args.seconds * 24000))
     model = MimiHipModel(synthetic.make_state_dict(seed=0, num_quantizers=K), device=dev)
+    if args.precision:
+        model.set_precision(args.precision)
     # this rank's utterances: a distinct seeded slice of the shard (round-robin i -> rank i % N)
     audio = torch.from_numpy(synthetic.clip_batch(B, L, seed=1000 + rank)).to(dev)
     codes = torch.empty((B, K, encoded_length(L)), dtype=torch.int32, device=dev)
@@ -178,7 +184,8 @@ def main():
         "config": {"workload": f"LibriTTS-R-style batch encode: batch={B} x {args.seconds:g} s @ 24 kHz, "
                                f"K={K} codebooks, 1 encode per step per GPU",
                    "global_batch": world * B, "clip_seconds": args.seconds, "num_quantizers": K,
-                   "parallelism": f"utterance round-robin x{world} (no collective)"},
+                   "parallelism": f"utterance round-robin x{world} (no collective)",
+                   "gemm_precision": model.precision},
         "pcie_inclusive_value": round(pcie_rate * world, 2),
     }
     if prof:

@@ -199,11 +199,12 @@ def test_thread_safety(engine):
     assert all(torch.equal(r, ref) for r in results)
 
 
-@pytest.mark.parametrize("mode,tol", [("f32", ACT_TOL), ("bf16x3", ACT_TOL)])
+@pytest.mark.parametrize("mode,tol", [("f32", ACT_TOL), ("bf16x6", ACT_TOL), ("bf16x3", ACT_TOL)])
 def test_precision_modes(engine, golden, mode, tol):
     """The non-default GEMM modes stay within the activation tolerance and explain every code flip."""
     arrays, meta = golden
     x = synthetic.speech_like(240000, meta["audio_seed"], 6)
+    default = engine.precision
     engine.set_precision(mode)
     engine.set_taps(True)
     try:
@@ -211,7 +212,7 @@ def test_precision_modes(engine, golden, mode, tol):
         emb = engine.get_tap("downsample")[0].T
     finally:
         engine.set_taps(False)
-        engine.set_precision("bf16x6")
+        engine.set_precision(default)
     assert rel_err(emb, arrays["emb_speech10s"]) < tol
     frac, bad = margin_audit(codes, arrays["embcodes_speech10s"].astype(np.int64), arrays["margins_speech10s"])
     assert not bad, (mode, frac, bad[:5])
@@ -261,3 +262,35 @@ def test_split_bf16_fused_block_c128(golden, state_dict, monkeypatch):
     r = np.where(r > 0, r, np.expm1(r.astype(np.float64))).astype(np.float32)
     assert rel_err(t, r) < ACT_TOL
     eng.close()
+
+
+@pytest.mark.parametrize("gain", [3e4, 1e-6])
+def test_f16_scales_follow_the_signal(state_dict, gain):
+    """f16x3 (default): a fresh engine fed audio far louder / quieter than speech still matches the bf16x6
+    arithmetic within the activation tolerance -- the range check re-centres every activation scale that left
+    fp16's window and re-runs the encode (a loud input must trigger it)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from mimi_hip.model import MimiHipModel
+    eng = MimiHipModel(state_dict, device="cuda:0")
+    assert eng.precision == "f16x3"
+    x = torch.from_numpy(synthetic.speech_like(72000, 5, 1) * np.float32(gain))[None, None].cuda()
+    eng.set_taps(True)
+    try:
+        c16 = eng.encode(x, num_quantizers=32).audio_codes.cpu().numpy()
+        e16 = eng.get_tap("downsample")
+        reruns = eng.f16_reruns
+        eng.set_precision("bf16x6")
+        c6 = eng.encode(x, num_quantizers=32).audio_codes.cpu().numpy()
+        e6 = eng.get_tap("downsample")
+    finally:
+        eng.set_taps(False)
+        eng.close()
+    assert np.isfinite(e16).all()
+    assert rel_err(e16, e6) < ACT_TOL, rel_err(e16, e6)
+    if gain > 1:
+        # an embedding 3e4 x louder than any codebook entry: distances are |r|^2-dominated near-ties, so only
+        # the embedding (above) is a meaningful comparison
+        assert reruns >= 1
+    else:
+        assert (c16 == c6).mean() > 0.99

@@ -144,6 +144,8 @@ struct DevConv {
     int cin = 0, cout = 0, k = 0, stride = 1;
     float* w = nullptr;      // [cout][k*cin]
     void* wsplit = nullptr;  // bf16 planes [3][cout][k*cin] of w (split-bf16 precision modes)
+    void* wh = nullptr;      // fp16 planes [2][cout][k*cin] of w * wscale (PREC_F16X3)
+    float wscale = 1.0f;
     float* wfrag = nullptr;  // w in 32x32x2-MFMA fragment order [cout/32][k*cin/8][64][4] (stage-0 block)
     float* b = nullptr;      // [cout] or null
 };
@@ -151,6 +153,8 @@ struct DevConv {
 struct DevXfmr {
     float *ln1_w, *ln1_b, *wqkv, *wo, *ls1, *ln2_w, *ln2_b, *w1, *w2, *ls2;
     void *wqkv_s, *wo_s, *w1_s, *w2_s;  // bf16 planes
+    void *wqkv_h, *wo_h, *w1_h, *w2_h;  // fp16 planes (x scale)
+    float wqkv_hs, wo_hs, w1_hs, w2_hs;
 };
 
 struct ProfEvent {
@@ -166,13 +170,15 @@ struct ProfStat {
     int64_t launches = 0;
 };
 
+constexpr int kMaxActSlots = 256;  // plane-format tensors per encode (~41 for kyutai/mimi)
+
 struct mimi_engine {
     mimi_config cfg;
     int device = 0;
     std::mutex mu;
     bool finalized = false;
     int levels_available = 0;
-    int precision = PREC_BF16X6;
+    int precision = PREC_F16X3;
     // planes path: residual blocks of stages >= unfuse_from run as two plane GEMMs (k3 -> h planes, k1 + skip)
     // instead of the fused fp32-MFMA kernel (MIMI_HIP_UNFUSE_FROM overrides; >= num_ratios disables)
     int unfuse_from = 2;
@@ -203,6 +209,14 @@ struct mimi_engine {
     size_t ws_bytes = 0;
 
     hipEvent_t ws_free = nullptr;  // recorded at the end of every encode: the next one (any stream) waits on it
+
+    // PREC_F16X3 activation scales: plane-format tensor i of an encode (in launch order) is stored as fp16
+    // planes of x * act_scale[i]; its producer max-reduces |x| into amax_dev[i] (see f16_rescale)
+    std::vector<float> act_scale;
+    unsigned* amax_dev = nullptr;   // [kMaxActSlots][AMAX_SLOT_WORDS] sub-slots, then [kMaxActSlots] reduced
+    unsigned* amax_red = nullptr;
+    unsigned* amax_host = nullptr;  // pinned
+    int f16_reruns = 0;             // encodes re-run with corrected scales (diagnostic)
     bool profiling = false;
     std::vector<ProfEvent> pending;  // recorded since last read; first event of each encode named ""
     std::vector<hipEvent_t> event_pool;
@@ -262,6 +276,28 @@ static int upload_split(mimi_engine* e, void** dst, const std::vector<float>& ho
     int rc = dev_alloc(e, dst, planes.size() * sizeof(uint16_t));
     if (rc) return rc;
     HIP_TRY(hipMemcpy(*dst, planes.data(), planes.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    return MIMI_OK;
+}
+
+// fp16 planes of w * scale: h0 = fp16(w s), h1 = fp16(w s - h0) (22-bit significand), scale a power of two
+// putting max|w| s in [2^13, 2^14): every weight >= 2^-17 max|w| keeps its full 22 bits, and no product of a
+// plane with an activation plane (|x s_x| < 2^15) can overflow the fp32 accumulator
+static int upload_f16(mimi_engine* e, void** dst, const std::vector<float>& host, float* scale) {
+    const size_t n = host.size();
+    float wmax = 0.0f;
+    for (float v : host) wmax = std::max(wmax, std::fabs(v));
+    const float sc = wmax > 0.0f && std::isfinite(wmax) ? std::ldexp(1.0f, 13 - std::ilogb(wmax)) : 1.0f;
+    std::vector<_Float16> planes(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+        const float t = host[i] * sc;
+        const _Float16 h0 = (_Float16)t;
+        planes[i] = h0;
+        planes[n + i] = (_Float16)(t - (float)h0);
+    }
+    int rc = dev_alloc(e, dst, planes.size() * sizeof(_Float16));
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(*dst, planes.data(), planes.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    *scale = sc;
     return MIMI_OK;
 }
 
@@ -367,6 +403,9 @@ extern "C" int mimi_create(const mimi_config* cfg, int device, mimi_engine** out
     if (const char* rs = std::getenv("MIMI_HIP_RES128_SPLIT")) e->res128_split = std::atoi(rs) != 0;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipEventCreateWithFlags(&e->ws_free, hipEventDisableTiming));
+    HIP_TRY(hipMalloc(&e->amax_dev, ((size_t)kMaxActSlots * AMAX_SLOT_WORDS + kMaxActSlots) * sizeof(unsigned)));
+    e->amax_red = e->amax_dev + (size_t)kMaxActSlots * AMAX_SLOT_WORDS;
+    HIP_TRY(hipHostMalloc(&e->amax_host, kMaxActSlots * sizeof(unsigned), hipHostMallocDefault));
     build_expected(e.get());
     *out = e.release();
     return MIMI_OK;
@@ -606,7 +645,9 @@ static int make_conv(mimi_engine* e, DevConv& dc, const std::string& prefix, int
     const std::vector<float> wl = cin == 1 ? *w : relayout_conv(*w, cout, cin, k);
     rc = upload(e, &dc.w, wl);
     if (rc) return rc;
-    if (cin % 4 == 0 && (k * cin) % 32 == 0 && (rc = upload_split(e, &dc.wsplit, wl))) return rc;
+    if (cin % 4 == 0 && (k * cin) % 32 == 0 &&
+        ((rc = upload_split(e, &dc.wsplit, wl)) || (rc = upload_f16(e, &dc.wh, wl, &dc.wscale))))
+        return rc;
     if (cout % 32 == 0 && (k * cin) % 8 == 0 && (rc = upload(e, &dc.wfrag, frag_layout(wl, cout, k * cin)))) return rc;
     if (bias) {
         std::vector<float>* b;
@@ -679,7 +720,9 @@ extern "C" int mimi_finalize(mimi_engine* e) {
         qkv.insert(qkv.end(), q->begin(), q->end());
         qkv.insert(qkv.end(), k->begin(), k->end());
         qkv.insert(qkv.end(), v->begin(), v->end());
-        if ((rc = upload(e, &x.wqkv, qkv)) || (rc = upload_split(e, &x.wqkv_s, qkv))) return rc;
+        if ((rc = upload(e, &x.wqkv, qkv)) || (rc = upload_split(e, &x.wqkv_s, qkv)) ||
+            (rc = upload_f16(e, &x.wqkv_h, qkv, &x.wqkv_hs)))
+            return rc;
         struct {
             const char* n;
             float** d;
@@ -696,7 +739,9 @@ extern "C" int mimi_finalize(mimi_engine* e) {
             if ((rc = get_w(e, p + sp.n, &t))) return rc;
             if ((rc = upload(e, sp.d, *t))) return rc;
             void** sd = sp.d == &x.wo ? &x.wo_s : sp.d == &x.w1 ? &x.w1_s : sp.d == &x.w2 ? &x.w2_s : nullptr;
-            if (sd && (rc = upload_split(e, sd, *t))) return rc;
+            void** hd = sp.d == &x.wo ? &x.wo_h : sp.d == &x.w1 ? &x.w1_h : sp.d == &x.w2 ? &x.w2_h : nullptr;
+            float* hs = sp.d == &x.wo ? &x.wo_hs : sp.d == &x.w1 ? &x.w1_hs : sp.d == &x.w2 ? &x.w2_hs : nullptr;
+            if (sd && ((rc = upload_split(e, sd, *t)) || (rc = upload_f16(e, hd, *t, hs)))) return rc;
         }
     }
     if ((rc = make_conv(e, e->ds, "downsample.conv.", h, h, c.downsample_kernel, c.downsample_stride, false))) return rc;
@@ -762,8 +807,8 @@ struct Workspace {
 // output, LayerNorm / attention / GELU outputs) are stored as NS bf16 planes instead of fp32 so the GEMMs
 // only move bytes (gemm_planes.h).  0 = fp32 activations (f32 mode, or a clip so long that a batch item's
 // plane exceeds the 2 GiB buffer-resource range).
-static int act_planes(const mimi_engine* e, const StagePlan& p) {
-    const int ns = e->precision == PREC_BF16X6 ? 3 : e->precision == PREC_BF16X3 ? 2 : 0;
+static int act_planes(const mimi_engine* e, const StagePlan& p, int prec) {
+    const int ns = prec == PREC_BF16X6 ? 3 : (prec == PREC_BF16X3 || prec == PREC_F16X3) ? 2 : 0;
     if (ns == 0) return 0;
     const mimi_config& c = e->cfg;
     int C = c.num_filters;
@@ -775,9 +820,9 @@ static int act_planes(const mimi_engine* e, const StagePlan& p) {
     return ns;
 }
 
-static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspace* w) {
+static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspace* w, int prec) {
     const mimi_config& c = e->cfg;
-    const int ns = act_planes(e, p);
+    const int ns = act_planes(e, p, prec);
     // a plane-format buffer of n values takes ns * n bf16 = ns * n / 2 floats
     auto act = [&](size_t n) { return ns ? (n * ns + 1) / 2 : n; };
     size_t xmax = 0, ymax = 0, xemax = 0;
@@ -816,7 +861,7 @@ static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspa
 
 extern "C" int64_t mimi_workspace_bytes(const mimi_engine* e, int32_t batch, int64_t length) {
     if (!e || batch <= 0 || length <= 0) return -1;
-    return (int64_t)ws_layout(e, batch, plan_lengths(e->cfg, length), nullptr);
+    return (int64_t)ws_layout(e, batch, plan_lengths(e->cfg, length), nullptr, e->precision);
 }
 
 static int ensure_ws(mimi_engine* e, size_t bytes, hipStream_t s) {
@@ -912,7 +957,7 @@ static int save_tap(mimi_engine* e, const char* name, const float* src, int64_t 
 
 // tap of a plane-format activation (materialised as fp32 only when taps are on)
 static int save_tap_planes(mimi_engine* e, const char* name, const void* planes, int ns, int64_t b, int64_t t,
-                           int64_t ch, hipStream_t s) {
+                           int64_t ch, hipStream_t s, float hscale = 0.0f) {
     if (!e->taps) return MIMI_OK;
     if (ns == 0) return save_tap(e, name, reinterpret_cast<const float*>(planes), b, t, ch, s);
     auto& tp = e->tapmap[name];
@@ -922,7 +967,7 @@ static int save_tap_planes(mimi_engine* e, const char* name, const void* planes,
         HIP_TRY(hipMalloc(&tp.d, n * 4));
         tp.cap = n;
     }
-    HIP_TRY(launch_planes_to_f32(planes, (long long)n, ns, tp.d, (long long)n, s));
+    HIP_TRY(launch_planes_to_f32(planes, (long long)n, ns, tp.d, (long long)n, s, hscale));
     tp.dims[0] = b;
     tp.dims[1] = t;
     tp.dims[2] = ch;
@@ -1002,15 +1047,44 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     return MIMI_OK;
 }
 
-static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s) {
+// One pass of the whole encode at precision prec (f16 mode: *nslots = the plane-format tensors written).
+static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s,
+                       int prec, int* nslots) {
     const mimi_config& c = e->cfg;
     const StagePlan p = plan_lengths(c, L);
     Workspace w{};
-    int rc = ensure_ws(e, ws_layout(e, B, p, nullptr), s);
+    int rc = ensure_ws(e, ws_layout(e, B, p, nullptr, prec), s);
     if (rc) return rc;
-    ws_layout(e, B, p, &w);
+    ws_layout(e, B, p, &w, prec);
     if ((rc = ensure_rope(e, p.frames25))) return rc;
-    const int ns = act_planes(e, p);  // 0: fp32 activations; 2/3: plane-format GEMM inputs
+    const int ns = act_planes(e, p, prec);  // 0: fp32 activations; 2/3: plane-format GEMM inputs
+    // fp16 planes: each plane-format tensor takes the next activation-scale slot (launch order)
+    const bool h16 = prec == PREC_F16X3 && ns == 2;
+    struct Act {
+        float scale = 0.0f;  // > 0: fp16 planes of x * scale
+        unsigned* amax = nullptr;
+    };
+    int nslot = 0;
+    auto new_act = [&]() {
+        Act a;
+        if (!h16 || nslot >= kMaxActSlots) return a;
+        if ((int)e->act_scale.size() <= nslot) e->act_scale.resize(nslot + 1, 1.0f);
+        a.scale = e->act_scale[nslot];
+        a.amax = e->amax_dev + (size_t)nslot * AMAX_SLOT_WORDS;
+        ++nslot;
+        return a;
+    };
+    if (h16 && nslots) *nslots = 0;
+    // fp16 weight planes + 1 / (activation scale x weight scale) for a GEMM reading plane tensor `in`
+    auto use_h = [&](GemmArgs& a, const void* wh, float wscale, const Act& in) {
+        if (!h16) return;
+        a.Wsplit = wh;
+        a.unscale = 1.0f / (in.scale * wscale);
+    };
+    auto out_act = [&](GemmArgs& a, const Act& o) {
+        a.out_scale = o.scale;
+        a.out_amax = o.amax;
+    };
     Recorder rec{e, s};
     const char* kname = "?";
     HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));
@@ -1031,6 +1105,7 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
     }
     int C = c.num_filters;
     char nm[64];
+    Act yact, xact, xeact, hact;  // the tensors currently held by y, x (last down conv), xe, h
     for (int si = 0; si < c.num_ratios; ++si) {
         const int64_t T = p.T[si];
         const bool unf = ns && si > 0 && si >= e->unfuse_from;
@@ -1054,7 +1129,10 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
             ra.yp = w.y;
             ra.y_pstride = (long long)B * T * C;
             ra.yns = ns;
-            if (ns && C == 128 && e->res128_split) {  // split-bf16 fused block (resblock.hip)
+            yact = new_act();
+            ra.yscale = yact.scale;
+            ra.yamax = yact.amax;
+            if (ns && !h16 && C == 128 && e->res128_split) {  // split-bf16 fused block (resblock.hip)
                 ra.w3s = e->res3[si].wsplit;
                 ra.w1s = e->res1[si].wsplit;
             }
@@ -1070,50 +1148,63 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
             const int Hh = C / c.compress;
             GemmArgs a3 = conv_args(e->res3[si], nullptr, T, nullptr, T, B);
             planes_in(a3, w.xe, (long long)B * T * C);
+            use_h(a3, e->res3[si].wh, e->res3[si].wscale, xeact);
             a3.Cp = w.h;
             a3.c_pstride = (long long)B * T * Hh;
-            LAUNCH_TRY(launch_gemm(ROLE_RES3P, a3, s, &kname, e->precision), "res3");
+            hact = new_act();
+            out_act(a3, hact);
+            LAUNCH_TRY(launch_gemm(ROLE_RES3P, a3, s, &kname, prec), "res3");
             snprintf(nm, sizeof nm, "res3_s%d", si);
             rec.mark(nm, gemm_flops(a3), gemm_bytes(a3, false), kname);
             GemmArgs a1 = conv_args(e->res1[si], nullptr, T, nullptr, T, B);
             planes_in(a1, w.h, (long long)B * T * Hh);
+            use_h(a1, e->res1[si].wh, e->res1[si].wscale, hact);
             a1.R = w.x;
             a1.Cp = w.y;
             a1.c_pstride = (long long)B * T * C;
-            LAUNCH_TRY(launch_gemm(ROLE_RES1P, a1, s, &kname, e->precision), "res1");
+            yact = new_act();
+            out_act(a1, yact);
+            LAUNCH_TRY(launch_gemm(ROLE_RES1P, a1, s, &kname, prec), "res1");
             snprintf(nm, sizeof nm, "res1_s%d", si);
             rec.mark(nm, gemm_flops(a1), gemm_bytes(a1, true), kname);
         }
         snprintf(nm, sizeof nm, "res%d_elu", si);
-        if ((rc = save_tap_planes(e, nm, w.y, ns, B, T, C, s))) return rc;
+        if ((rc = save_tap_planes(e, nm, w.y, ns, B, T, C, s, yact.scale))) return rc;
         const bool last = si == c.num_ratios - 1;
         const bool next_unf = ns && !last && si + 1 >= e->unfuse_from;
         GemmArgs ad = conv_args(e->down[si], w.y, T, w.x, p.T[si + 1], B);
         int role = last ? ROLE_DOWN_ELU : ROLE_DOWN;
         if (ns) {
             planes_in(ad, w.y, (long long)B * T * C);
+            use_h(ad, e->down[si].wh, e->down[si].wscale, yact);
             if (last) {  // only the final conv reads it: planes out
                 ad.Cp = w.x;
                 ad.c_pstride = (long long)B * p.T[si + 1] * 2 * C;
                 ad.C = nullptr;
+                xact = new_act();
+                out_act(ad, xact);
             } else if (next_unf) {  // fp32 x (the skip) + ELU(x) planes (the next k3 conv's input)
                 ad.Cp = w.xe;
                 ad.c_pstride = (long long)B * p.T[si + 1] * 2 * C;
                 role = ROLE_DOWN_XE;
+                xeact = new_act();
+                out_act(ad, xeact);
             }
         }
-        LAUNCH_TRY(launch_gemm(role, ad, s, &kname, e->precision), "down");
+        LAUNCH_TRY(launch_gemm(role, ad, s, &kname, prec), "down");
         snprintf(nm, sizeof nm, "down_s%d", si);
         rec.mark(nm, gemm_flops(ad), gemm_bytes(ad, false), kname);
         snprintf(nm, sizeof nm, last ? "down%d_elu" : "down%d", si);
-        if ((rc = save_tap_planes(e, nm, w.x, last ? ns : 0, B, p.T[si + 1], 2 * C, s))) return rc;
+        if ((rc = save_tap_planes(e, nm, w.x, last ? ns : 0, B, p.T[si + 1], 2 * C, s, last ? xact.scale : 0.0f)))
+            return rc;
         C *= 2;
     }
     const int64_t T = p.frames25;
     const int Hd = c.hidden_size;
     GemmArgs af = conv_args(e->final_conv, w.x, p.T[c.num_ratios], w.t0, T, B);
     if (ns) planes_in(af, w.x, (long long)B * p.T[c.num_ratios] * C);
-    LAUNCH_TRY(launch_gemm(ROLE_FINAL, af, s, &kname, e->precision), "final");
+    use_h(af, e->final_conv.wh, e->final_conv.wscale, xact);
+    LAUNCH_TRY(launch_gemm(ROLE_FINAL, af, s, &kname, prec), "final");
     rec.mark("final", gemm_flops(af), gemm_bytes(af, false), kname);
     if ((rc = save_tap(e, "encoder", w.t0, B, T, Hd, s))) return rc;
 
@@ -1126,7 +1217,10 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
     for (int l = 0; l < c.num_hidden_layers; ++l) {
         const DevXfmr& x = e->xf[l];
         const long long nact = rows * Hd;
-        LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns), "ln1");
+        const Act t1a = new_act();
+        LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1a.scale,
+                                    t1a.amax),
+                   "ln1");
         rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512>");
         GemmArgs aq = linear_args(w.t1, T, Hd, x.wqkv, 3 * H * Dh, w.qkv);
         aq.Wsplit = x.wqkv_s;
@@ -1137,10 +1231,12 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
         aq.rope_sin = e->rope_sin;
         aq.rope_cols = 2 * H * Dh;
         if (ns) planes_in(aq, w.t1, nact);
-        LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, e->precision), "qkv");
+        use_h(aq, x.wqkv_h, x.wqkv_hs, t1a);
+        LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, prec), "qkv");
         rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
+        const Act atta = new_act();
         LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh), s,
-                                    w.att, nact, ns),
+                                    w.att, nact, ns, atta.scale, atta.amax),
                    "attention");
         rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4, "mimi::attention_kernel");
         GemmArgs ao = linear_args(w.att, rows, H * Dh, x.wo, Hd, w.t0);
@@ -1148,26 +1244,35 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
         ao.R = w.t0;
         ao.scale = x.ls1;
         if (ns) planes_in(ao, w.att, nact);
-        LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, e->precision), "o_proj");
+        use_h(ao, x.wo_h, x.wo_hs, atta);
+        LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
         rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
-        LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns), "ln2");
+        const Act t1b = new_act();
+        LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1b.scale,
+                                    t1b.amax),
+                   "ln2");
         rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512>");
         GemmArgs a1 = linear_args(w.t1, rows, Hd, x.w1, c.intermediate_size, w.ff);
         a1.Wsplit = x.w1_s;
+        Act ffa;
         if (ns) {
             planes_in(a1, w.t1, nact);
+            use_h(a1, x.w1_h, x.w1_hs, t1b);
             a1.Cp = w.ff;  // only fc2 reads it: planes out
             a1.c_pstride = rows * c.intermediate_size;
             a1.C = nullptr;
+            ffa = new_act();
+            out_act(a1, ffa);
         }
-        LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, e->precision), "fc1");
+        LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, prec), "fc1");
         rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
         GemmArgs a2 = linear_args(w.ff, rows, c.intermediate_size, x.w2, Hd, w.t0);
         a2.Wsplit = x.w2_s;
         a2.R = w.t0;
         a2.scale = x.ls2;
         if (ns) planes_in(a2, w.ff, rows * (long long)c.intermediate_size);
-        LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname, e->precision), "fc2");
+        use_h(a2, x.w2_h, x.w2_hs, ffa);
+        LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname, prec), "fc2");
         rec.mark("fc2", gemm_flops(a2), gemm_bytes(a2, true), kname);
         snprintf(nm, sizeof nm, "xfmr%d", l);
         if ((rc = save_tap(e, nm, w.t0, B, T, Hd, s))) return rc;
@@ -1176,7 +1281,7 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
     // ---- downsample (replicate pad) + input projections + RVQ ----
     const int64_t T2 = p.frames12;
     GemmArgs ad = conv_args(e->ds, w.t0, T, w.dsout, T2, B);
-    LAUNCH_TRY(launch_gemm(ROLE_DOWNSAMPLE, ad, s, &kname, e->precision), "downsample");
+    LAUNCH_TRY(launch_gemm(ROLE_DOWNSAMPLE, ad, s, &kname, prec), "downsample");
     rec.mark("downsample", gemm_flops(ad), gemm_bytes(ad, false), kname);
     if ((rc = save_tap(e, "downsample", w.dsout, B, T2, Hd, s))) return rc;
     const int Dq = c.vq_hidden_dim;
@@ -1186,7 +1291,46 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
     if ((rc = save_tap(e, "proj", w.proj, B, T2, 2 * Dq, s))) return rc;
     if ((rc = run_rvq(e, w.proj, (int64_t)B * T2, K, codes, (int)T2, w.rvq, s, rec))) return rc;
     HIP_TRY(hipEventRecord(e->ws_free, s));
+    if (h16 && nslots) *nslots = nslot;
     return MIMI_OK;
+}
+
+// Activation scales (PREC_F16X3).  A plane tensor with max|x| = a stored at scale s keeps every element's full
+// 22-bit significand down to 2^-3 / s (h1 = fp16(x s - h0) normal) and an absolute error <= 2^-25 / s below,
+// i.e. <= 2^-22 a for all of it, as long as a s >= 2^-3; a s < 2^15 keeps x s (and h0) finite.  A tensor that
+// left [2^-3, 2^15) is re-centred at a s in [2^6, 2^7) and the encode re-run (the scales persist, so a shard of
+// similar audio re-runs only its first batch, if at all).  Non-finite or zero maxima are left alone (an
+// upstream overflow in this pass, or a NaN input the reference would propagate too).
+static bool f16_rescale(mimi_engine* e, int nslots) {
+    bool again = false;
+    for (int i = 0; i < nslots; ++i) {
+        float a;
+        std::memcpy(&a, &e->amax_host[i], 4);
+        if (!(a > 0.0f) || !std::isfinite(a)) continue;
+        const float as = a * e->act_scale[i];
+        if (as >= 32768.0f || as < 0.125f) {
+            e->act_scale[i] = std::ldexp(1.0f, 6 - std::ilogb(a));
+            again = true;
+        }
+    }
+    return again;
+}
+
+static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s) {
+    int prec = e->precision;
+    for (int attempt = 0;; ++attempt) {
+        const bool h16 = prec == PREC_F16X3;
+        if (h16) HIP_TRY(hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), s));
+        int nslots = 0;
+        int rc = encode_pass(e, audio, B, L, K, codes, s, prec, &nslots);
+        if (rc || !h16 || nslots == 0) return rc;
+        LAUNCH_TRY(launch_amax_reduce(e->amax_dev, nslots, e->amax_red, s), "amax_reduce");
+        HIP_TRY(hipMemcpyAsync(e->amax_host, e->amax_red, nslots * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (!f16_rescale(e, nslots)) return MIMI_OK;
+        ++e->f16_reruns;
+        if (attempt >= 2) prec = PREC_BF16X6;  // scales still moving: finish this call in bf16x6
+    }
 }
 
 extern "C" int mimi_encode(mimi_engine* e, const float* audio, int32_t batch, int64_t length, int32_t K,
@@ -1255,6 +1399,8 @@ extern "C" void mimi_destroy(mimi_engine* e) {
     for (auto& pe : e->pending) (void)hipEventDestroy(pe.ev);
     for (auto ev : e->event_pool) (void)hipEventDestroy(ev);
     if (e->ws_free) (void)hipEventDestroy(e->ws_free);
+    if (e->amax_dev) (void)hipFree(e->amax_dev);
+    if (e->amax_host) (void)hipHostFree(e->amax_host);
     delete e;
 }
 
@@ -1263,7 +1409,7 @@ extern "C" void mimi_destroy(mimi_engine* e) {
 // ------------------------------------------------------------------------------------------------
 extern "C" int mimi_set_precision(mimi_engine* e, int32_t mode) {
     if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
-    if (mode < MIMI_PRECISION_F32 || mode > MIMI_PRECISION_BF16X3)
+    if (mode < MIMI_PRECISION_F32 || mode > MIMI_PRECISION_F16X3)
         return set_err(MIMI_ERR_INVALID_ARGUMENT, "precision mode %d", mode);
     std::lock_guard<std::mutex> lk(e->mu);
     e->precision = mode;
@@ -1271,6 +1417,8 @@ extern "C" int mimi_set_precision(mimi_engine* e, int32_t mode) {
 }
 
 extern "C" int mimi_get_precision(const mimi_engine* e) { return e ? e->precision : -1; }
+
+extern "C" int64_t mimi_f16_reruns(const mimi_engine* e) { return e ? e->f16_reruns : -1; }
 
 extern "C" int mimi_set_profiling(mimi_engine* e, int enable) {
     if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");

@@ -59,14 +59,15 @@ static hipError_t run_split(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int ST, int EPI, int OUTP, int TAG, int LW = 0>
+template <int BM, int BN, int WM, int WN, int NS, int ST, int EPI, int OUTP, int TAG, int LW = 0, int BK = 32, int MF = 32,
+          int FL = 0, bool F16 = false>
 static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
     static char name[160];
     if (!name[0])
-        snprintf(name, sizeof(name), "mimi::gemm_planes_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d>", BM, BN, WM, WN,
-                 NS, ST, EPI, OUTP, TAG, LW);
+        snprintf(name, sizeof(name), "mimi::gemm_planes_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %s>", BM,
+                 BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL, F16 ? "true" : "false");
     g_last_kernel = name;
-    if (a.K % 32 != 0 || !a.Wsplit || !a.Ap || ((OUTP & 7) && !a.Cp) || (!(OUTP & 7) && !a.C) ||
+    if (a.K % BK != 0 || !a.Wsplit || !a.Ap || ((OUTP & 7) && !a.Cp) || (!(OUTP & 7) && !a.C) ||
         ((OUTP & 8) && !a.C) || (EPI == EPI_BIAS_RES_ELU && !a.R))
         return hipErrorInvalidValue;
     if (a.a_len * 2 > 0x7fffffffLL) return hipErrorInvalidValue;  // buffer-resource byte offsets are 32-bit
@@ -74,33 +75,41 @@ static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
     if (a.N % 8 || a.ldc % 8 || a.c_bstride % 8 || a.c_pstride % 8) return hipErrorInvalidValue;
     const long long nwg = (long long)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.batch;
     if (nwg > 0x7fffffffLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW>), dim3((unsigned)nwg),
+    if (F16 && ((OUTP & 7) ? a.out_scale <= 0.0f : false)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL, F16>), dim3((unsigned)nwg),
                        dim3((WM * WN + LW) * 64), 0, s, a);
     return hipGetLastError();
 }
 
-// Tiles of the planes kernel (tools/gemm_bench.hip; profiles/r1_gemm_bench_planes*.log, r1_gemm_bench_ws.log):
+// Tiles of the planes kernel (tools/gemm_bench.hip; profiles/r1_gemm_bench_planes*.log, r1_gemm_bench_ws.log,
+// r1_gemm_bench_f16.log):
 //   big:    256x128, 8 compute waves, 2 stages (NS = 3; 3 at NS = 2), 144 KiB LDS: down convs, k3 convs, fc1
 //   big_ld: 256x128, 4 compute waves of 128x64 + 4 loader waves (warp-specialised DMA): down_s3
 //   small:  128x128, 8 compute waves of 32x64, 3 stages: final conv, q/k/v (M = B*250 rows)
 //   small_ld: 128x128, 4 compute waves of 64x64 + 4 loader waves, 3 stages: o_proj, fc2
+// fp16 planes (PREC_F16X3, 2 planes): 16x16x32 MFMAs; big = 256x128 x 3 stages (every big / big_ld role),
+// small = 128x128 x 4 stages (every small / small_ld role).
 template <int EPI, int OUTP3, int OUTP2, int TAG>
 static hipError_t run_planes_big(const GemmArgs& a, hipStream_t s, int prec) {
+    if (prec == PREC_F16X3) return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP2, TAG, 0, 32, 16, 0, true>(a, s);
     if (prec == PREC_BF16X6) return run_planes<256, 128, 4, 2, 3, 2, EPI, OUTP3, TAG>(a, s);
     return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP2, TAG>(a, s);
 }
 template <int EPI, int OUTP3, int OUTP2, int TAG>
 static hipError_t run_planes_big_ld(const GemmArgs& a, hipStream_t s, int prec) {
+    if (prec == PREC_F16X3) return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP2, TAG, 0, 32, 16, 0, true>(a, s);
     if (prec == PREC_BF16X6) return run_planes<256, 128, 2, 2, 3, 2, EPI, OUTP3, TAG, 4>(a, s);
     return run_planes<256, 128, 2, 2, 2, 3, EPI, OUTP2, TAG, 4>(a, s);
 }
 template <int EPI, int TAG>
 static hipError_t run_planes_small(const GemmArgs& a, hipStream_t s, int prec) {
+    if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 4, EPI, 0, TAG, 0, 32, 16, 0, true>(a, s);
     if (prec == PREC_BF16X6) return run_planes<128, 128, 4, 2, 3, 3, EPI, 0, TAG>(a, s);
     return run_planes<128, 128, 4, 2, 2, 3, EPI, 0, TAG>(a, s);
 }
 template <int EPI, int TAG>
 static hipError_t run_planes_small_ld(const GemmArgs& a, hipStream_t s, int prec) {
+    if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 4, EPI, 0, TAG, 0, 32, 16, 0, true>(a, s);
     if (prec == PREC_BF16X6) return run_planes<128, 128, 2, 2, 3, 3, EPI, 0, TAG, 4>(a, s);
     return run_planes<128, 128, 2, 2, 2, 3, EPI, 0, TAG, 4>(a, s);
 }
@@ -124,7 +133,8 @@ static thread_local int g_prec = PREC_F32;
 
 template <bool ELU_IN, int PAD, int EPI, int TAG>
 static hipError_t run_prec(const GemmArgs& a, hipStream_t s, int prec) {
-    if (prec == PREC_BF16X6) return run_split<128, 128, 2, 2, 3, ELU_IN, PAD, EPI, TAG>(a, s);
+    // fp32 activations in a split mode (downsample, or clips too long for the plane buffers): register split
+    if (prec == PREC_BF16X6 || prec == PREC_F16X3) return run_split<128, 128, 2, 2, 3, ELU_IN, PAD, EPI, TAG>(a, s);
     if (prec == PREC_BF16X3) return run_split<128, 128, 2, 2, 2, ELU_IN, PAD, EPI, TAG>(a, s);
     return run_auto<ELU_IN, PAD, EPI, TAG>(a, s);
 }
@@ -142,7 +152,7 @@ hipError_t launch_gemm(int role, const GemmArgs& a, hipStream_t s, const char** 
 
 static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
     const int prec = g_prec;
-    if (prec != PREC_BF16X6 && prec != PREC_BF16X3) return hipErrorInvalidValue;
+    if (prec != PREC_BF16X6 && prec != PREC_BF16X3 && prec != PREC_F16X3) return hipErrorInvalidValue;
     switch (role) {
         case ROLE_DOWN: return run_planes_big<EPI_BIAS, 0, 0, 2>(a, s, prec);
         case ROLE_DOWN_ELU: return run_planes_big_ld<EPI_BIAS_ELU, 3, 2, 3>(a, s, prec);  // planes out: final conv
@@ -154,6 +164,8 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         case ROLE_DOWN_XE: return run_planes_big<EPI_BIAS, 3 | 8, 2 | 8, 11>(a, s, prec);
         case ROLE_RES3P: return run_planes_big<EPI_BIAS_ELU, 3, 2, 12>(a, s, prec);
         case ROLE_RES1P:  // K = C/2 = 128 / 256: short K, output-heavy -> 74 KiB tiles, two workgroups per CU
+            if (prec == PREC_F16X3)
+                return run_planes<128, 64, 2, 2, 2, 3, EPI_BIAS_RES_ELU, 2, 13, 0, 32, 16, 0, true>(a, s);
             if (prec == PREC_BF16X6) return run_planes<128, 64, 2, 2, 3, 2, EPI_BIAS_RES_ELU, 3, 13>(a, s);
             return run_planes<128, 64, 2, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13>(a, s);
         default: return hipErrorInvalidValue;
@@ -167,7 +179,7 @@ static hipError_t dispatch(int role, const GemmArgs& a, hipStream_t s) {
         case ROLE_DOWN_ELU: return run_prec<false, PAD_ZERO, EPI_BIAS_ELU, 3>(a, s, g_prec);
         case ROLE_FINAL: return run_prec<false, PAD_ZERO, EPI_BIAS_OUT, 4>(a, s, g_prec);
         case ROLE_QKV:
-            if (g_prec == PREC_BF16X6) return run_split<128, 128, 2, 2, 3, false, PAD_ZERO, EPI_ROPE, 5>(a, s);
+            if (g_prec == PREC_BF16X6 || g_prec == PREC_F16X3) return run_split<128, 128, 2, 2, 3, false, PAD_ZERO, EPI_ROPE, 5>(a, s);
             if (g_prec == PREC_BF16X3) return run_split<128, 128, 2, 2, 2, false, PAD_ZERO, EPI_ROPE, 5>(a, s);
             return run<64, 128, 1, 2, 32, 1, false, false, PAD_ZERO, EPI_ROPE, 5>(a, s);
         case ROLE_OPROJ: return run_prec<false, PAD_ZERO, EPI_SCALE_RES, 6>(a, s, g_prec);

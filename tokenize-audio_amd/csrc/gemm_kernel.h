@@ -239,7 +239,8 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 // instead of up to k*Cin/64 steps apart (with 30+ CUs streaming through an XCD's 4 MB L2 in between: HBM
 // re-reads).  Linear layers (k = 1) get the plain order; layouts it does not cover too.  Wave-uniform state
 // (SGPRs); advance with next() once per K step.
-struct KOrder {
+template <int BK>
+struct KOrderT {
     int cin, s, cl, nhi, nlo, j, hi, c, lo;
     __device__ __forceinline__ void init(const GemmArgs& p) {
         j = hi = c = lo = 0;
@@ -254,10 +255,11 @@ struct KOrder {
             s = 1;
             cl = 1;
         }
-        nlo = (cin || p.K % 64 == 0) ? 2 : 1;
-        nhi = (cin ? cin : p.K) / (32 * nlo);
+        const int blk = (cin || p.K % 64 == 0) ? 64 : BK;  // 128-B channel block (or one K step)
+        nlo = blk / BK;
+        nhi = (cin ? cin : p.K) / blk;
     }
-    __device__ __forceinline__ int offset() const { return (j + c * s) * cin + (hi * nlo + lo) * 32; }
+    __device__ __forceinline__ int offset() const { return (j + c * s) * cin + (hi * nlo + lo) * BK; }
     __device__ __forceinline__ void next() {
         if (++lo < nlo) return;
         lo = 0;
@@ -268,6 +270,7 @@ struct KOrder {
         ++j;
     }
 };
+using KOrder = KOrderT<32>;
 
 template <int NS>
 __device__ __forceinline__ void split_bf16x4(f32x4 v, bf16x4 (&out)[NS]) {
@@ -282,22 +285,48 @@ __device__ __forceinline__ void split_bf16x4(f32x4 v, bf16x4 (&out)[NS]) {
     }
 }
 
-template <int NS, int TM, int TN>
-__device__ __forceinline__ void mma_split(f32x16 (&acc)[TM][TN], const bf16x8 (&a)[NS][TM],
-                                          const bf16x8 (&b)[NS][TN]) {
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// one 32x32x16 (MF = 32) or 16x16x32 (MF = 16) MFMA on bf16 or fp16 planes (the planes are carried as bf16x8
+// bit patterns either way)
+template <bool F16>
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+    if constexpr (F16)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                      0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+    if constexpr (F16)
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                      0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// the plane products of one (i, j) tile pair: small terms first, the leading product last
+template <int NS, int TM, int TN, bool F16 = false, typename AccT>
+__device__ __forceinline__ void mma_split(AccT (&acc)[TM][TN], const bf16x8 (&a)[NS][TM], const bf16x8 (&b)[NS][TN]) {
+    auto mf = [](bf16x8 x, bf16x8 y, AccT c) {
+        if constexpr (sizeof(AccT) == 64)
+            return mfma32<F16>(x, y, c);
+        else
+            return mfma16<F16>(x, y, c);
+    };
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            // small terms first, the leading product last
             if (NS == 3) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2 % NS][i], b[0][j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2 % NS][j], acc[i][j], 0, 0, 0);
+                acc[i][j] = mf(a[2 % NS][i], b[0][j], acc[i][j]);
+                acc[i][j] = mf(a[1][i], b[1][j], acc[i][j]);
+                acc[i][j] = mf(a[0][i], b[2 % NS][j], acc[i][j]);
             }
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mf(a[1][i], b[0][j], acc[i][j]);
+            acc[i][j] = mf(a[0][i], b[1][j], acc[i][j]);
+            acc[i][j] = mf(a[0][i], b[0][j], acc[i][j]);
         }
 }
 

@@ -17,6 +17,8 @@
 //   * workgroup -> tile map is XCD-aware: the 8 XCDs each take a contiguous run of the (m, n) tile order
 //     with n fastest, so the N tiles sharing an A tile hit the same L2.
 #pragma once
+#include <type_traits>
+
 #include "gemm_kernel.h"
 
 namespace mimi {
@@ -34,33 +36,71 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-// LW > 0: warp-specialised -- LW extra loader waves issue every LDS-DMA piece and do the counted waits, the
-// WM x WN compute waves only ds_read and MFMA (an LDS-DMA piece costs its issuing wave ~60-185 cycles,
-// MI355X_MICROARCH.md; with LW = 0 the compute waves pay it between their MFMAs).  Both kinds meet at the one
-// barrier per K step.
-template <int BM, int BN, int WM, int WN, int NS, int STAGES, int EPI, int OUTP, int TAG, int LW = 0>
+// 16-B chunk position of an LDS image row (applied on the DMA source and on the fragment read: an involution),
+// chosen so that every ds_read_b128 lane group of the fragment reads (MI355X_MICROARCH.md §LDS) hits 16
+// distinct 16-B bank slots:
+//   BK = 32 (64-B rows), 32x32x16 reads (row lane&31, chunk 2ks + lane>>5): chunk ^ ((row >> 2) & 3)
+//   BK = 32 (64-B rows), 16x16x32 reads (row lane&15, chunk lane>>4):        chunk ^ 3 * ((row >> 3) & 1)
+//   BK = 16 (32-B rows), 32x32x16 reads (row lane&31, chunk lane>>5):        chunk ^ ((row >> 3) & 1)
+template <int BK, int MF>
+__device__ __forceinline__ int chunk_swz(int row) {
+    if (BK == 16) return (row >> 3) & 1;
+    if (MF == 16) return ((row >> 3) & 1) * 3;
+    return (row >> 2) & 3;
+}
+
+
+// Template knobs beyond the tile (BM x BN, WM x WN compute waves, NS planes, STAGES-deep ring):
+//   LW > 0: warp-specialised -- LW extra loader waves issue every LDS-DMA piece and do the counted waits, the
+//           compute waves only ds_read and MFMA (an LDS-DMA piece costs its issuing wave ~60-185 cycles,
+//           MI355X_MICROARCH.md; with LW = 0 the compute waves pay it between their MFMAs).  Both kinds meet at
+//           the one barrier per K step.
+//   BK:     K per step, 32 (64-B image rows, 16 rows x 4 chunks per DMA piece) or 16 (32-B rows, 32 x 2):
+//           BK = 16 halves the stage so a 256-row tile fits a 4-deep ring.
+//   MF:     MFMA shape, 32 (v_mfma_f32_32x32x16_bf16) or 16 (v_mfma_f32_16x16x32_bf16, BK = 32).
+//   F16:    the planes are fp16 (2 planes, 3 products, PREC_F16X3) scaled by powers of two; the accumulator is
+//           multiplied by p.unscale before the epilogue; fp16 output planes hold out * p.out_scale.
+//   FL:     FL_READFIRST -- a K step's first fragment reads are issued before its DMA refill;
+//           FL_PRIO -- s_setprio(1) over the MFMA section.
+enum : int { FL_READFIRST = 1, FL_PRIO = 2 };
+
+template <int BM, int BN, int WM, int WN, int NS, int STAGES, int EPI, int OUTP, int TAG, int LW = 0, int BK = 32,
+          int MF = 32, int FL = 0, bool F16 = false>
 __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmArgs p) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
     constexpr int NW = WM * WN;
     constexpr int NLD = LW > 0 ? LW : NW;        // waves issuing DMA
-    constexpr int BK = 32;
-    constexpr int TM = BM / WM / 32;
-    constexpr int TN = BN / WN / 32;
+    constexpr int CPR = BK / 8;                  // 16-B chunks per image row
+    constexpr int RPP = 64 / CPR;                // image rows per 1-KiB DMA piece
+    constexpr int TM = BM / WM / MF;
+    constexpr int TN = BN / WN / MF;
+    constexpr int KSUB = MF == 32 ? BK / 16 : BK / 32;  // MFMA k-steps per K step
     constexpr int APL = BM * BK, BPL = BN * BK;  // bf16 per plane image
     constexpr int STG = NS * (APL + BPL);        // bf16 per stage
-    constexpr int APW = NS * BM / 16 / NLD;      // A pieces per loading wave per stage
-    constexpr int BPW = NS * BN / 16 / NLD;      // B pieces per loading wave per stage
-    constexpr int PPW = APW + BPW;
-    static_assert(APW * NLD * 16 == NS * BM && BPW * NLD * 16 == NS * BN, "pieces must split evenly over waves");
+    // DMA pieces of a stage: A planes [0, TPA), then B planes; piece j is issued by loading wave j % NLD
+    constexpr int TPA = NS * BM / RPP, TP = TPA + NS * BN / RPP;
+    constexpr int PMAX = (TP + NLD - 1) / NLD;   // pieces per loading wave per stage (the first TP % NLD waves)
+    constexpr int PMIN = TP / NLD;               // (the others)
+    static_assert(BK == 32 || (BK == 16 && MF == 32), "BK");
+    static_assert(MF == 32 || MF == 16, "MFMA shape");
+    static_assert(TM >= 1 && TN >= 1 && KSUB >= 1, "tile");
+    static_assert(NS * BM % RPP == 0 && NS * BN % RPP == 0, "whole pieces");
     static_assert(STAGES >= 2 && STAGES <= 4, "stages");
-    static_assert(PPW * (STAGES - 2) <= 63, "vmcnt range");
-    static_assert(EPI != EPI_ROPE || (TN % 2 == 0), "rope pairs need even TN");
+    static_assert(PMAX * (STAGES - 2) <= 63, "vmcnt range");
+    static_assert(EPI != EPI_ROPE || (MF == 32 ? TN % 2 == 0 : TN % 4 == 0), "rope pairs (d, d+32) in one lane");
+    static_assert(!F16 || NS == 2, "fp16 planes: 2 planes, 3 products");
     // OUTP: 0 = fp32 C only; 2/3 = that many bf16 planes of the output (+ fp32 C when p.C is set);
     // | 8 = the planes hold ELU(output) (fp32 C keeps the raw value)
     constexpr int ONS = OUTP & 7;
     constexpr bool OELU = (OUTP & 8) != 0;
+    typedef typename std::conditional<MF == 32, f32x16, f32x4>::type accT;
+    constexpr int NACC = MF == 32 ? 16 : 4;
 
-    __shared__ __attribute__((aligned(16))) __bf16 lds[STAGES * STG];
+    // epilogue staging (wave-private fp32 tiles) reuses the ring
+    constexpr int CW = TN * MF, LDE = CW + 4, RW = TM * MF;
+    constexpr int LDS_EL = STAGES * STG > NW * RW * LDE * 2 ? STAGES * STG : NW * RW * LDE * 2;
+    static_assert(LDS_EL * 2 <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) __bf16 lds[LDS_EL];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -79,36 +119,41 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     const int b = rest / MT;
     const int m0 = mt * BM, n0 = nt * BN;
 
-    // ---- DMA sources for this lane (16 rows x 4 chunks per piece; lane -> row lane>>2, chunk lane&3)
+    // ---- DMA sources for this lane (RPP rows x CPR chunks per piece; lane -> row lane/CPR, chunk lane%CPR)
+    const int prow = lane / CPR, pch = lane % CPR;
     const __bf16* __restrict__ Abase = reinterpret_cast<const __bf16*>(p.Ap) + (long long)b * p.a_bstride;
     __amdgpu_buffer_rsrc_t arsrc[NS];
 #pragma unroll
     for (int pl = 0; pl < NS; ++pl) arsrc[pl] = make_rsrc(Abase + (long long)pl * p.a_pstride, p.a_len * 2);
-    int aoff[APW];  // byte offset of this lane's chunk at k0 = 0 (may be negative: reads 0)
-#pragma unroll
-    for (int q = 0; q < APW; ++q) {
-        const int j = ldw + q * NLD;
-        const int rb = j % (BM / 16);
-        const int row = rb * 16 + (lane >> 2);
-        const int c = (lane & 3) ^ ((row >> 2) & 3);
-        const int m = m0 + row;
-        const long long e = p.a_off + (long long)m * p.a_rs + c * 8;
-        aoff[q] = (m < M) ? (int)(e * 2) : -16;  // rows past M load 0 (never stored)
-    }
+    // per piece slot q of this wave: piece j = ldw + q * NLD (wave-uniform), its LDS destination within a stage
+    // (elements) and this lane's source: a byte offset into A plane pl (may be negative or past the end: the
+    // buffer range check loads 0 -- the causal padding) or an element offset into the weight planes.
     const __bf16* __restrict__ Wp = reinterpret_cast<const __bf16*>(p.Wsplit);
-    const __bf16* bsrc[BPW];
+    int soff[PMAX];
 #pragma unroll
-    for (int q = 0; q < BPW; ++q) {
+    for (int q = 0; q < PMAX; ++q) {
         const int j = ldw + q * NLD;
-        const int pl = j / (BN / 16), rb = j % (BN / 16);
-        const int row = rb * 16 + (lane >> 2);
-        const int c = (lane & 3) ^ ((row >> 2) & 3);
-        int n = n0 + row;
-        n = n < N ? n : N - 1;  // rows past N only feed columns that are never stored
-        bsrc[q] = Wp + ((long long)pl * N + n) * K + c * 8;
+        soff[q] = 0;
+        if (j < TPA) {
+            const int rb = j % (BM / RPP);
+            const int row = rb * RPP + prow;
+            const int c = pch ^ chunk_swz<BK, MF>(row);
+            const int m = m0 + row;
+            const long long e = p.a_off + (long long)m * p.a_rs + c * 8;
+            soff[q] = (m < M) ? (int)(e * 2) : -16;  // rows past M load 0 or stale data (never stored)
+        } else if (j < TP) {
+            const int jb = j - TPA;
+            const int pl = jb / (BN / RPP), rb = jb % (BN / RPP);
+            const int row = rb * RPP + prow;
+            const int c = pch ^ chunk_swz<BK, MF>(row);
+            int n = n0 + row;
+            n = n < N ? n : N - 1;  // rows past N only feed columns that are never stored
+            soff[q] = (int)(((long long)pl * N + n) * K + c * 8);
+        }
     }
+    const int npieces = ldw < TP % NLD ? PMAX : PMIN;  // this wave's pieces per stage (wave-uniform)
 
-    KOrder ko;  // K steps are issued in order: the cursor follows the issues
+    KOrderT<BK> ko;  // K steps are issued in order: the cursor follows the issues
     ko.init(p);
     auto issue = [&](int stage) {
         __bf16* st = lds + stage * STG;
@@ -116,36 +161,56 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         ko.next();
         const int kb = k0 * 2;  // bytes
 #pragma unroll
-        for (int q = 0; q < APW; ++q) {
+        for (int q = 0; q < PMAX; ++q) {
             const int j = ldw + q * NLD;
-            const int pl = j / (BM / 16), rb = j % (BM / 16);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                arsrc[pl], (__attribute__((address_space(3))) void*)(st + pl * APL + rb * 16 * BK), 16,
-                aoff[q] + kb, 0, 0, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < BPW; ++q) {
-            const int j = ldw + q * NLD;
-            const int pl = j / (BN / 16), rb = j % (BN / 16);
-            __builtin_amdgcn_global_load_lds((const void*)(bsrc[q] + k0),
-                                             (__attribute__((address_space(3))) void*)(st + NS * APL + pl * BPL +
-                                                                                        rb * 16 * BK),
-                                             16, 0, 0);
+            if (j < TPA) {
+                const int pl = j / (BM / RPP), rb = j % (BM / RPP);
+                const __amdgpu_buffer_rsrc_t rs = pl == 0 ? arsrc[0] : (pl == 1 ? arsrc[1 % NS] : arsrc[NS - 1]);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(st + pl * APL + rb * RPP * BK), 16, soff[q] + kb, 0,
+                    0, 0);
+            } else if (j < TP) {
+                const int jb = j - TPA;
+                const int pl = jb / (BN / RPP), rb = jb % (BN / RPP);
+                __builtin_amdgcn_global_load_lds(
+                    (const void*)(Wp + soff[q] + k0),
+                    (__attribute__((address_space(3))) void*)(st + NS * APL + pl * BPL + rb * RPP * BK), 16, 0, 0);
+            }
         }
     };
 
-    f32x16 acc[TM][TN];
+    accT acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+            for (int r = 0; r < NACC; ++r) acc[i][j][r] = 0.0f;
 
     const int KT = K / BK;
-    const int arow = wm * TM * 32 + (lane & 31);
-    const int brow = wn * TN * 32 + (lane & 31);
-    const int hsel = lane >> 5;
+    const int arow = wm * TM * MF + (lane & (MF - 1));
+    const int brow = wn * TN * MF + (lane & (MF - 1));
+    const int hsel = MF == 32 ? lane >> 5 : lane >> 4;  // k chunk of the lane within an MFMA k-step
+
+    // fragments of MFMA k-step ks of the stage at As / Bs
+    auto read_frags = [&](const __bf16* As, const __bf16* Bs, int ks, bf16x8 (&af)[NS][TM], bf16x8 (&bf)[NS][TN]) {
+        const int lc = MF == 32 ? ks * 2 + hsel : hsel;
+#pragma unroll
+        for (int pl = 0; pl < NS; ++pl) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int row = arow + i * MF;
+                const int phys = (lc ^ chunk_swz<BK, MF>(row)) * 8;
+                af[pl][i] = *reinterpret_cast<const bf16x8*>(As + pl * APL + row * BK + phys);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int row = brow + j * MF;
+                const int phys = (lc ^ chunk_swz<BK, MF>(row)) * 8;
+                bf[pl][j] = *reinterpret_cast<const bf16x8*>(Bs + pl * BPL + row * BK + phys);
+            }
+        }
+    };
 
     if (loader) {
 #pragma unroll
@@ -158,58 +223,53 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
             // retire this wave's pieces of stage kt; the later stages stay in flight
             const int later = min(STAGES - 2, KT - 1 - kt);
             if (STAGES >= 4 && later >= 2) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+                if (PMAX == PMIN || npieces == PMAX)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PMAX) : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PMIN) : "memory");
             } else if (STAGES >= 3 && later >= 1) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+                if (PMAX == PMIN || npieces == PMAX)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PMAX) : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PMIN) : "memory");
             } else {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
         }
         __builtin_amdgcn_s_barrier();
+        const __bf16* As = lds + (kt % STAGES) * STG;
+        const __bf16* Bs = As + NS * APL;
+        bf16x8 af[NS][TM], bf[NS][TN];
+        if ((FL & FL_READFIRST) && compute) read_frags(As, Bs, 0, af, bf);
         // the stage consumed in step kt-1 is free: refill it with step kt + STAGES - 1
         if (loader && kt + STAGES - 1 < KT) issue((kt + STAGES - 1) % STAGES);
         if (!compute) continue;
-        const __bf16* As = lds + (kt % STAGES) * STG;
-        const __bf16* Bs = As + NS * APL;
+        if (FL & FL_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int kk = 0; kk < BK / 16; ++kk) {
-            bf16x8 af[NS][TM], bf[NS][TN];
-#pragma unroll
-            for (int pl = 0; pl < NS; ++pl) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    const int row = arow + i * 32;
-                    const int phys = ((kk * 2 + hsel) ^ ((row >> 2) & 3)) * 8;
-                    af[pl][i] = *reinterpret_cast<const bf16x8*>(As + pl * APL + row * BK + phys);
-                }
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int row = brow + j * 32;
-                    const int phys = ((kk * 2 + hsel) ^ ((row >> 2) & 3)) * 8;
-                    bf[pl][j] = *reinterpret_cast<const bf16x8*>(Bs + pl * BPL + row * BK + phys);
-                }
-            }
-            mma_split<NS, TM, TN>(acc, af, bf);
+        for (int ks = 0; ks < KSUB; ++ks) {
+            if (!(FL & FL_READFIRST) || ks > 0) read_frags(As, Bs, ks, af, bf);
+            mma_split<NS, TM, TN, F16>(acc, af, bf);
         }
+        if (FL & FL_PRIO) __builtin_amdgcn_s_setprio(0);
     }
 
-    // ---- epilogue.  Phase 1 (MFMA layout: lane holds col lane&31, rows (r&3) + 8(r>>2) + 4h of each 32x32
-    // tile): the epilogue math, into a wave-private fp32 tile in the (now idle) LDS ring.  Phase 2: each lane
-    // reads 8 consecutive columns of one row back and stores them as 2 x 16 B fp32 and / or one 16-B bf16x8
-    // per plane -- instead of one scattered 4-B (2-B per plane) store per value.
-    constexpr int CW = TN * 32, LDE = CW + 4, RW = TM * 32;
-    static_assert(NW * RW * LDE * 4 <= STAGES * STG * 2, "epilogue staging fits the ring");
+    // ---- epilogue.  Phase 1 (MFMA layout): the epilogue math, into a wave-private fp32 tile in the (now idle)
+    // LDS ring.  32x32 tiles: lane holds col lane&31, rows (r&3) + 8(r>>2) + 4(lane>>5); 16x16 tiles: col
+    // lane&15, rows 4(lane>>4) + r.  Phase 2: each lane reads 8 consecutive columns of one row back and
+    // stores them as 2 x 16 B fp32 and / or one 16-B bf16x8 per plane -- instead of one scattered 4-B (2-B
+    // per plane) store per value.
     __syncthreads();  // every wave is done with the ring
     if (!compute) return;
     float* stg = reinterpret_cast<float*>(lds) + wave * (RW * LDE);
     const float* __restrict__ Rb = p.R ? p.R + (long long)b * p.c_bstride : nullptr;
-    const int rbase = m0 + wm * RW + 4 * hsel;
-    const int cbase = n0 + wn * CW + (lane & 31);
+    const int rbase = m0 + wm * RW;
+    const int cbase = n0 + wn * CW + (lane & (MF - 1));
+    const float us = F16 ? p.unscale : 1.0f;  // 1 / (activation scale x weight scale): exact power of two
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const int col = cbase + j * 32;
+            const int col = cbase + j * MF;
             float bias = 0.0f, scale = 0.0f;
             if (col < N) {
                 if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU || EPI == EPI_BIAS_RES_ELU || EPI == EPI_BIAS_OUT)
@@ -217,11 +277,11 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                 if (EPI == EPI_SCALE_RES) scale = p.scale[col];
             }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int lrow = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
-                const int row = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
+            for (int r = 0; r < NACC; ++r) {
+                const int lrow = MF == 32 ? i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel : i * 16 + 4 * hsel + r;
+                const int row = rbase + lrow;
                 const bool ok = row < M && col < N;
-                float v = acc[i][j][r];
+                float v = F16 ? acc[i][j][r] * us : acc[i][j][r];
                 if (EPI == EPI_BIAS || EPI == EPI_BIAS_OUT) {
                     v = v + bias;
                 } else if (EPI == EPI_BIAS_ELU) {
@@ -234,29 +294,33 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                     v = scale * v;  // + R in phase 2
                 } else if (EPI == EPI_ROPE) {
                     if (ok && col < p.rope_cols) {
-                        const int d = col % 64;  // head_dim = 64: pairs (d, d + 32) sit in tiles j, j + 1
+                        // head_dim = 64: the pair (d, d + 32) sits in tiles j, j + 32/MF of the same lane
+                        constexpr int PJ = 32 / MF;
+                        const int d = col % 64;
                         const float c = p.rope_cos[(long long)row * 32 + (d & 31)];
                         const float sn = p.rope_sin[(long long)row * 32 + (d & 31)];
-                        if ((j & 1) == 0) {
-                            const float x2 = acc[i][j + 1][r];
+                        if (((j / PJ) & 1) == 0) {
+                            const float x2 = F16 ? acc[i][j + PJ][r] * us : acc[i][j + PJ][r];
                             v = v * c + (-x2) * sn;
                         } else {
-                            const float x1 = acc[i][j - 1][r];
+                            const float x1 = F16 ? acc[i][j - PJ][r] * us : acc[i][j - PJ][r];
                             v = v * c + x1 * sn;
                         }
                     }
                 }
-                stg[lrow * LDE + j * 32 + (lane & 31)] = v;
+                stg[lrow * LDE + j * MF + (lane & (MF - 1))] = v;
             }
         }
     }
     float* __restrict__ Cb = p.C ? p.C + (long long)b * p.c_bstride : nullptr;
+    static_assert(!F16 || ONS == 0 || ONS == 2, "fp16 output planes: 2");
     __bf16* __restrict__ Cpb = ONS ? reinterpret_cast<__bf16*>(p.Cp) + (long long)b * p.c_bstride : nullptr;
+    float omx = 0.0f;  // max|planes value| (fp16 planes: the engine's range check)
     constexpr int LPR = CW / 8;  // lanes per row
-    constexpr int RPP = 64 / LPR;  // rows per pass
+    constexpr int RPS = 64 / LPR;  // rows per pass
 #pragma unroll
-    for (int ps = 0; ps < RW / RPP; ++ps) {
-        const int lr = ps * RPP + lane / LPR, lc = (lane % LPR) * 8;
+    for (int ps = 0; ps < RW / RPS; ++ps) {
+        const int lr = ps * RPS + lane / LPR, lc = (lane % LPR) * 8;
         f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc);
         f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc + 4);
         const int row = m0 + wm * RW + lr, col = n0 + wn * CW + lc;
@@ -274,27 +338,19 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         }
         if (ONS) {
             // planes out (of ELU(v) when OELU: the next residual block's conv input), fp32 v beside
-            float rem[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+            float pv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
             if (OELU) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) rem[e] = elu1(rem[e]);
+                for (int e = 0; e < 8; ++e) pv[e] = elu1(pv[e]);
             }
-#pragma unroll
-            for (int pl = 0; pl < ONS; ++pl) {
-                bf16x8 hv;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    hv[e] = (__bf16)rem[e];
-                    rem[e] = rem[e] - (float)hv[e];
-                }
-                *reinterpret_cast<bf16x8*>(Cpb + pl * p.c_pstride + off) = hv;
-            }
+            store_act8(Cpb, p.c_pstride, ONS, off, pv, F16 ? p.out_scale : 0.0f, &omx);
         }
         if (Cb) {
             *reinterpret_cast<f32x4*>(Cb + off) = v0;
             *reinterpret_cast<f32x4*>(Cb + off + 4) = v1;
         }
     }
+    if (F16 && ONS) amax_commit(p.out_amax, omx);
 #endif
 }
 

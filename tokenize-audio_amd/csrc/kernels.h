@@ -16,13 +16,25 @@ __device__ __forceinline__ float elu_fast(float x) {
     return x > 0.0f ? x : e;
 }
 
-// Activation store in the consumer's format: fp32 (ns == 0) or ns bf16 planes x = x0 + x1 [+ x2] with
-// x_p = bf16(x - x0 - ... - x_{p-1}) (the split of gemm_kernel.h), plane p at planes + p * pstride.  The planes
-// feed gemm_planes_kernel, which then only moves bytes (gemm_planes.h).
+// Activation store in the consumer's format: fp32 (ns == 0), ns bf16 planes x = x0 + x1 [+ x2] with
+// x_p = bf16(x - x0 - ... - x_{p-1}) (the split of gemm_kernel.h), or -- hscale > 0, PREC_F16X3 -- 2 fp16 planes
+// of x * hscale (h0 = fp16(x * hscale), h1 = fp16(x * hscale - h0): 22-bit significand; hscale a power of two
+// chosen by the engine so that max|x| * hscale sits inside fp16's range, see engine.cpp "activation scales").
+// Plane p at planes + p * pstride.  The planes feed gemm_planes_kernel, which then only moves bytes
+// (gemm_planes.h).  In fp16 mode *mx accumulates max|x| for the engine's range check (amax_commit).
 __device__ __forceinline__ void store_act(float* f32, void* planes, long long pstride, int ns, long long idx,
-                                          float v) {
+                                          float v, float hscale = 0.0f, float* mx = nullptr) {
     if (ns == 0) {
         f32[idx] = v;
+        return;
+    }
+    if (hscale > 0.0f) {
+        _Float16* hp = reinterpret_cast<_Float16*>(planes) + idx;
+        const float t = v * hscale;
+        const _Float16 h0 = (_Float16)t;
+        hp[0] = h0;
+        hp[pstride] = (_Float16)(t - (float)h0);
+        *mx = fmaxf(*mx, fabsf(v));
         return;
     }
     __bf16* pp = reinterpret_cast<__bf16*>(planes) + idx;
@@ -33,6 +45,61 @@ __device__ __forceinline__ void store_act(float* f32, void* planes, long long ps
     pp[pstride] = h1;
     if (ns == 3) pp[2 * pstride] = (__bf16)(r1 - (float)h1);
 }
+
+// 8 consecutive values as planes (16-B stores per plane): bf16 (ns = 2/3) or scaled fp16 (hscale > 0)
+__device__ __forceinline__ void store_act8(void* planes, long long pstride, int ns, long long idx, const float (&v)[8],
+                                           float hscale, float* mx) {
+    typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+    typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+    if (hscale > 0.0f) {
+        f16x8_t a, b;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float t = v[e] * hscale;
+            a[e] = (_Float16)t;
+            b[e] = (_Float16)(t - (float)a[e]);
+            *mx = fmaxf(*mx, fabsf(v[e]));
+        }
+        _Float16* hp = reinterpret_cast<_Float16*>(planes) + idx;
+        *reinterpret_cast<f16x8_t*>(hp) = a;
+        *reinterpret_cast<f16x8_t*>(hp + pstride) = b;
+        return;
+    }
+    float rem[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) rem[e] = v[e];
+    __bf16* dst = reinterpret_cast<__bf16*>(planes) + idx;
+    for (int pl = 0; pl < ns; ++pl) {
+        bf16x8_t hv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            hv[e] = (__bf16)rem[e];
+            rem[e] = rem[e] - (float)hv[e];
+        }
+        *reinterpret_cast<bf16x8_t*>(dst + pl * pstride) = hv;
+    }
+}
+
+// max over the wave of the lanes' running max|x|, max-ed into one of AMAX_SUB sub-slots of the tensor's slot
+// (picked by workgroup, AMAX_STRIDE words apart) -- only when it exceeds what the sub-slot already holds, so
+// the thousands of waves of a launch do not serialise on one address (atomics execute at the memory side).
+// A stale read can only cost an unneeded atomic (the stored value only grows).  Non-negative floats order as
+// their bit patterns.  Every lane of the wave must call it; amax == null: no-op.  amax_reduce_kernel folds the
+// sub-slots.
+constexpr int AMAX_SUB = 64, AMAX_STRIDE = 16, AMAX_SLOT_WORDS = AMAX_SUB * AMAX_STRIDE;
+__device__ __forceinline__ void amax_commit(unsigned* amax, float mx) {
+    if (!amax) return;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if ((threadIdx.x & 63) == 0 && mx > 0.0f) {
+        unsigned* a = amax + ((blockIdx.x + 7 * blockIdx.y + 13 * blockIdx.z) & (AMAX_SUB - 1)) * AMAX_STRIDE;
+        const unsigned u = __float_as_uint(mx);
+        if (*reinterpret_cast<volatile unsigned*>(a) < u) atomicMax(a, u);
+    }
+}
+
+// out[i] = max over the AMAX_SUB sub-slots of slot i (one wave per slot)
+hipError_t launch_amax_reduce(const unsigned* amax, int nslots, unsigned* out, hipStream_t s);
 
 // Epilogues of the implicit-GEMM conv / linear kernel.
 enum Epi : int {
@@ -76,6 +143,12 @@ struct GemmArgs {
     int ldc;
     void* Cp;             // optional bf16 planes of the output (planes-out epilogues), plane stride c_pstride
     long long c_pstride;
+    // fp16-plane mode (PREC_F16X3, gemm_planes_kernel<..., F16 = true>): 1 / (activation scale x weight scale)
+    // applied to the accumulator before the epilogue (exact: powers of two); fp16 output planes hold
+    // out * out_scale and max|out| goes to *out_amax
+    float unscale;
+    float out_scale;
+    unsigned* out_amax;
 };
 
 // Launch the GEMM for a given conv/linear role (the role picks tile shape and template flags).
@@ -98,7 +171,8 @@ enum GemmRole : int {
 };
 // Arithmetic of the GEMMs: fp32 MFMA, or fp32 emulated on the bf16 matrix cores with 3 (6 products) or
 // 2 (3 products) bf16 planes per operand (gemm_kernel.h).
-enum Precision : int { PREC_F32 = 0, PREC_BF16X6 = 1, PREC_BF16X3 = 2 };
+// PREC_F16X3: 2 fp16 planes per operand (3 products) with power-of-two scales: 22-bit operands.
+enum Precision : int { PREC_F32 = 0, PREC_BF16X6 = 1, PREC_BF16X3 = 2, PREC_F16X3 = 3 };
 
 // *kname (optional) receives the kernel symbol as rocprofv3 prints it, for per-kernel profile aggregation.
 hipError_t launch_gemm(int role, const GemmArgs& a, hipStream_t s, const char** kname = nullptr,
@@ -120,6 +194,8 @@ struct ResArgs {
     void* yp;             // when yns > 0: y is written as yns bf16 planes (plane stride y_pstride) instead of fp32
     long long y_pstride;
     int yns;
+    float yscale;         // > 0: 2 fp16 planes of y * yscale (PREC_F16X3), max|y| into *yamax
+    unsigned* yamax;
     const float* w3frag;  // optional: W3 / W1 in MFMA-fragment order [ntile][kquad][64 lanes][4] (stage 0)
     const float* w1frag;
     const void* w3s;      // optional: W3 / W1 as 3 bf16 planes [3][N][K] (split-bf16 fused block, C = 128)
@@ -134,17 +210,18 @@ hipError_t launch_conv0(const float* x, long long L, int batch, const float* w /
 // LayerNorm over the last dim (C = 512) of rows; output fp32 (yns == 0) or yns bf16 planes.
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* y, long long rows,
                             int C, float eps, hipStream_t s, void* yp = nullptr, long long y_pstride = 0,
-                            int yns = 0);
+                            int yns = 0, float yscale = 0.0f, unsigned* yamax = nullptr);
 
 // Sliding-window causal attention on the fused qkv tensor [B][T][3*H*D] (q, k already rotated);
 // output [B][T][H*D].
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window,
                             float scale, hipStream_t s, void* outp = nullptr, long long out_pstride = 0,
-                            int outns = 0);
+                            int outns = 0, float oscale = 0.0f, unsigned* oamax = nullptr);
 
-// planes -> fp32 (x0 + x1 [+ x2]); used only to materialise per-stage taps of plane-format activations.
+// planes -> fp32 (x0 + x1 [+ x2], or (h0 + h1) / hscale for fp16 planes); used only to materialise per-stage
+// taps of plane-format activations.
 hipError_t launch_planes_to_f32(const void* planes, long long pstride, int ns, float* out, long long n,
-                                hipStream_t s);
+                                hipStream_t s, float hscale = 0.0f);
 
 // Split RVQ: proj [F][2*Dq] (semantic | acoustic projections), codebooks in fragment layout, codes
 // out[level][F] int32 (or [b][level][t] when frames_per_item > 0).

@@ -73,7 +73,8 @@ template <int C>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                         const float* __restrict__ bta, float* __restrict__ y,
                                                         long long rows, float eps, __bf16* __restrict__ yp,
-                                                        long long pstride, int yns) {
+                                                        long long pstride, int yns, float yscale,
+                                                        unsigned* __restrict__ yamax) {
     constexpr int PER = C / 64;  // floats per lane
     static_assert(PER % 4 == 0, "C multiple of 256");
     const int lane = threadIdx.x & 63;
@@ -101,6 +102,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     const float sc = rstd;
     const float bi = -rstd * mean;
     float* yr = y + row * C;
+    float mx = 0.0f;
 #pragma unroll
     for (int q = 0; q < PER / 4; ++q) {
         const int c0 = q * 256 + lane * 4;
@@ -113,6 +115,18 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
         o.w = (v[q * 4 + 3] * sc + bi) * gg.w + bb.w;
         if (yns == 0) {
             *reinterpret_cast<f32x4*>(yr + c0) = o;
+        } else if (yscale > 0.0f) {
+            // fp16 planes of o * yscale (PREC_F16X3)
+            typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+            _Float16* pr = reinterpret_cast<_Float16*>(yp) + row * C + c0;
+            const f32x4 t = o * yscale;
+            f16x4 h0, h1;
+            h0.x = (_Float16)t.x; h0.y = (_Float16)t.y; h0.z = (_Float16)t.z; h0.w = (_Float16)t.w;
+            h1.x = (_Float16)(t.x - (float)h0.x); h1.y = (_Float16)(t.y - (float)h0.y);
+            h1.z = (_Float16)(t.z - (float)h0.z); h1.w = (_Float16)(t.w - (float)h0.w);
+            *reinterpret_cast<f16x4*>(pr) = h0;
+            *reinterpret_cast<f16x4*>(pr + pstride) = h1;
+            mx = fmaxf(mx, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
         } else {
             // planes for the split-bf16 GEMMs that read this row (q/k/v, fc1)
             typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -126,13 +140,15 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
             }
         }
     }
+    amax_commit(yamax, mx);
 }
 
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* y, long long rows, int C,
-                            float eps, hipStream_t s, void* yp, long long y_pstride, int yns) {
-    if (C != 512 || (yns != 0 && !yp)) return hipErrorInvalidValue;
+                            float eps, hipStream_t s, void* yp, long long y_pstride, int yns, float yscale,
+                            unsigned* yamax) {
+    if (C != 512 || (yns != 0 && !yp) || (yscale > 0.0f && yns != 2)) return hipErrorInvalidValue;
     hipLaunchKernelGGL((layernorm_kernel<512>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, g, b, y,
-                       rows, eps, reinterpret_cast<__bf16*>(yp), y_pstride, yns);
+                       rows, eps, reinterpret_cast<__bf16*>(yp), y_pstride, yns, yscale, yamax);
     return hipGetLastError();
 }
 
@@ -208,7 +224,8 @@ __device__ __forceinline__ void attn_chunk(f32x16 (&o)[2], float& m, float& l, c
 
 __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict__ qkv, float* __restrict__ out,
                                                         int T, int H, int window, float scale,
-                                                        void* __restrict__ outp, long long pstride, int outns) {
+                                                        void* __restrict__ outp, long long pstride, int outns,
+                                                        float oscale, unsigned* __restrict__ oamax) {
     constexpr int D = 64;
     constexpr int KC = 32;
     constexpr int LDKS = D + 4;
@@ -287,10 +304,14 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
             ow[col * LDO + d] = o[t][r] * inv;
         }
     __syncthreads();
+    float mx = 0.0f;
     for (int qq = 0; qq < 32; ++qq) {
         const int q = qw + qq;
-        if (q < T) store_act(out, outp, pstride, outns, ((long long)b * T + q) * (H * D) + h * D + lane, ow[qq * LDO + lane]);
+        if (q < T)
+            store_act(out, outp, pstride, outns, ((long long)b * T + q) * (H * D) + h * D + lane, ow[qq * LDO + lane],
+                      oscale, &mx);
     }
+    amax_commit(oamax, mx);
 }
 
 // T <= 256 (every 10 s clip: T = 250): one workgroup per (head, batch item) with the item's whole K and V
@@ -298,7 +319,8 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
 // tile w (w < 4) or 11 - w, so the two waves sharing a SIMD (w, w + 4) own 9 causal chunks between them.
 __global__ __launch_bounds__(512) void attention_t256_kernel(const float* __restrict__ qkv, float* __restrict__ out,
                                                              int T, int H, int window, float scale,
-                                                             void* __restrict__ outp, long long pstride, int outns) {
+                                                             void* __restrict__ outp, long long pstride, int outns,
+                                                             float oscale, unsigned* __restrict__ oamax) {
     constexpr int D = 64, LDKS = D + 4, LDO = D + 1, TM = 256;
     __shared__ __attribute__((aligned(16))) float lds[TM * LDKS + TM * D];
     float* Ks = lds;
@@ -366,42 +388,66 @@ __global__ __launch_bounds__(512) void attention_t256_kernel(const float* __rest
             ow[col * LDO + d] = o[t][r] * inv;
         }
     // same wave wrote and reads its staging rows: LDS order, no barrier
+    float mx = 0.0f;
     for (int qq = 0; qq < 32; ++qq) {
         const int q = qw + qq;
         if (q < T)
-            store_act(out, outp, pstride, outns, ((long long)b * T + q) * (H * D) + h * D + lane, ow[qq * LDO + lane]);
+            store_act(out, outp, pstride, outns, ((long long)b * T + q) * (H * D) + h * D + lane, ow[qq * LDO + lane],
+                      oscale, &mx);
     }
+    amax_commit(oamax, mx);
 }
 
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window, float scale,
-                            hipStream_t s, void* outp, long long out_pstride, int outns) {
-    if (D != 64 || (outns != 0 && !outp)) return hipErrorInvalidValue;
+                            hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
+                            unsigned* oamax) {
+    if (D != 64 || (outns != 0 && !outp) || (oscale > 0.0f && outns != 2)) return hipErrorInvalidValue;
     if (T <= 256) {
         hipLaunchKernelGGL(attention_t256_kernel, dim3(H, batch), dim3(512), 0, s, qkv, out, T, H, window, scale,
-                           outp, out_pstride, outns);
+                           outp, out_pstride, outns, oscale, oamax);
         return hipGetLastError();
     }
     dim3 grid((T + 127) / 128, H, batch);
     hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, qkv, out, T, H, window, scale, outp, out_pstride,
-                       outns);
+                       outns, oscale, oamax);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(64) void amax_reduce_kernel(const unsigned* __restrict__ amax, unsigned* __restrict__ out) {
+    const unsigned* a = amax + (long long)blockIdx.x * AMAX_SLOT_WORDS;
+    unsigned v = threadIdx.x < AMAX_SUB ? a[threadIdx.x * AMAX_STRIDE] : 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
+    if (threadIdx.x == 0) out[blockIdx.x] = v;
+}
+
+hipError_t launch_amax_reduce(const unsigned* amax, int nslots, unsigned* out, hipStream_t s) {
+    if (nslots <= 0) return hipSuccess;
+    static_assert(AMAX_SUB <= 64, "one wave per slot");
+    hipLaunchKernelGGL(amax_reduce_kernel, dim3(nslots), dim3(64), 0, s, amax, out);
     return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void planes_to_f32_kernel(const __bf16* __restrict__ pl, long long pstride, int ns,
-                                                            float* __restrict__ out, long long n) {
+                                                            float* __restrict__ out, long long n, float hscale) {
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
+    if (hscale > 0.0f) {
+        const _Float16* hp = reinterpret_cast<const _Float16*>(pl);
+        out[i] = ((float)hp[i] + (float)hp[i + pstride]) / hscale;
+        return;
+    }
     float v = (float)pl[i] + (float)pl[i + pstride];
     if (ns == 3) v = v + (float)pl[i + 2 * pstride];
     out[i] = v;
 }
 
 hipError_t launch_planes_to_f32(const void* planes, long long pstride, int ns, float* out, long long n,
-                                hipStream_t s) {
+                                hipStream_t s, float hscale) {
     if (n <= 0) return hipSuccess;
-    if (ns != 2 && ns != 3) return hipErrorInvalidValue;
+    if ((ns != 2 && ns != 3) || (hscale > 0.0f && ns != 2)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(planes_to_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                       reinterpret_cast<const __bf16*>(planes), pstride, ns, out, n);
+                       reinterpret_cast<const __bf16*>(planes), pstride, ns, out, n, hscale);
     return hipGetLastError();
 }
 

@@ -55,8 +55,7 @@ __device__ __forceinline__ void mma_k32(f32x16 (&acc)[TM][TN], const float* A, i
 constexpr int YSTG_LD = 68;
 constexpr int YSTG_FLOATS = 8 * YSTG_LD;
 __device__ __forceinline__ void store_y_block(const ResArgs& p, float* stg, const f32x16 (&v)[2], long long ybase,
-                                              long long row0, int col0, int C, long long T, int lane) {
-    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+                                              long long row0, int col0, int C, long long T, int lane, float& mx) {
     const int h = lane >> 5, c = lane & 31;
     const int lr = lane >> 3, lc = (lane & 7) * 8;
 #pragma unroll
@@ -74,17 +73,8 @@ __device__ __forceinline__ void store_y_block(const ResArgs& p, float* stg, cons
                 *reinterpret_cast<f32x4*>(p.y + idx) = a0;
                 *reinterpret_cast<f32x4*>(p.y + idx + 4) = a1;
             } else {
-                float rem[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                __bf16* dst = reinterpret_cast<__bf16*>(p.yp) + idx;
-                for (int pl = 0; pl < p.yns; ++pl) {
-                    bf16x8 hv;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        hv[e] = (__bf16)rem[e];
-                        rem[e] = rem[e] - (float)hv[e];
-                    }
-                    *reinterpret_cast<bf16x8*>(dst + pl * p.y_pstride) = hv;
-                }
+                const float vv[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                store_act8(p.yp, p.y_pstride, p.yns, idx, vv, p.yscale, &mx);
             }
         }
     }
@@ -291,6 +281,7 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs p) {
 
     // ---------------- GEMM2: y = ELU(x + b1 + h . W1^T), NP columns per pass ----------------
     const long long ybase = (long long)b * T * C;
+    float ymx = 0.0f;  // max|y| (fp16 planes: the engine's range check)
     for (int n0 = 0; n0 < C; n0 += NP) {
         auto load2 = [&](int k0) {
 #pragma unroll
@@ -340,7 +331,7 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs p) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) v[j][r] = elu_f(xres[0][j][r] + (acc2[0][j][r] + bias));
             }
-            store_y_block(p, Xs + wave * YSTG_FLOATS, v, ybase, m0 + w2m * 32, n0 + w2n * 64, C, T, lane);
+            store_y_block(p, Xs + wave * YSTG_FLOATS, v, ybase, m0 + w2m * 32, n0 + w2n * 64, C, T, lane, ymx);
         } else {
 #pragma unroll
         for (int j = 0; j < TN2; ++j) {
@@ -354,13 +345,14 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs p) {
                     if (row < T) {
                         const float xr = FIRST ? Xs[(row - m0) * LDX + col] : xres[i][j][r];
                         store_act(p.y, p.yp, p.y_pstride, p.yns, ybase + row * C + col,
-                                  elu_f(xr + (acc2[i][j][r] + bias)));
+                                  elu_f(xr + (acc2[i][j][r] + bias)), p.yscale, &ymx);
                     }
                 }
         }
         }
         if (n0 + NP < C) prefetch_res(n0 + NP);
     }
+    amax_commit(p.yamax, ymx);
 }
 
 
@@ -489,7 +481,9 @@ __global__ __launch_bounds__(256) void resblock0_wave_kernel(ResArgs p) {
         }
     }
     static_assert(34 * LDX >= YSTG_FLOATS, "staging fits the slab");
-    store_y_block(p, Xw, v, ybase, r0, 0, C, T, lane);
+    float ymx = 0.0f;
+    store_y_block(p, Xw, v, ybase, r0, 0, C, T, lane, ymx);
+    amax_commit(p.yamax, ymx);
 }
 
 // ------------------------------------------------------------------------------------------------

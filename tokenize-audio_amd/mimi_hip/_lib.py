@@ -15,7 +15,7 @@ LIB_NAME = "libmimi_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 MIMI_OK = 0
-PRECISIONS = {"f32": 0, "bf16x6": 1, "bf16x3": 2}
+PRECISIONS = {"f32": 0, "bf16x6": 1, "bf16x3": 2, "f16x3": 3}
 STATUS_NAMES = {
     0: "MIMI_OK", 1: "MIMI_ERR_INVALID_ARGUMENT", 2: "MIMI_ERR_HIP", 3: "MIMI_ERR_OUT_OF_MEMORY",
     4: "MIMI_ERR_WEIGHTS", 5: "MIMI_ERR_UNSUPPORTED", 6: "MIMI_ERR_IO", 7: "MIMI_ERR_STATE",
@@ -24,7 +24,7 @@ STATUS_NAMES = {
 # every symbol include/mimi_hip.h declares (tests check the library exports exactly these)
 EXPORTED_SYMBOLS = (
     "mimi_config_default", "mimi_create", "mimi_set_weight", "mimi_load_safetensors", "mimi_finalize",
-    "mimi_encode", "mimi_rvq_encode", "mimi_set_precision", "mimi_get_precision", "mimi_encoded_length",
+    "mimi_encode", "mimi_rvq_encode", "mimi_set_precision", "mimi_get_precision", "mimi_f16_reruns", "mimi_encoded_length",
     "mimi_encoded_length_cfg",
     "mimi_workspace_bytes", "mimi_destroy", "mimi_last_error", "mimi_set_profiling", "mimi_profile_read",
     "mimi_profile_reset", "mimi_set_taps", "mimi_get_tap",
@@ -69,6 +69,7 @@ def _declare(lib):
         "mimi_rvq_encode": (c.c_int, [vp, vp, c.c_int64, c.c_int32, vp, vp]),
         "mimi_set_precision": (c.c_int, [vp, c.c_int32]),
         "mimi_get_precision": (c.c_int, [vp]),
+        "mimi_f16_reruns": (c.c_int64, [vp]),
         "mimi_encoded_length": (c.c_int64, [c.c_int64]),
         "mimi_encoded_length_cfg": (c.c_int64, [c.POINTER(MimiConfigC), c.c_int64]),
         "mimi_workspace_bytes": (c.c_int64, [vp, c.c_int32, c.c_int64]),

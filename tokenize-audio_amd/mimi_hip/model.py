@@ -221,14 +221,19 @@ class MimiHipModel:
 
     # ---- instrumentation ------------------------------------------------------------------------
     def set_precision(self, mode: str):
-        """'bf16x6' (default: fp32 emulated on the bf16 matrix cores, 3 planes), 'f32' (fp32 MFMA) or
-        'bf16x3' (2 planes, ~1e-5)."""
+        """'f16x3' (default: fp32 emulated on the fp16 matrix cores, 2 scaled planes with a range check),
+        'bf16x6' (3 bf16 planes), 'f32' (fp32 MFMA) or 'bf16x3' (2 bf16 planes, ~1e-5)."""
         _lib.check(self._lib.mimi_set_precision(self._h, _lib.PRECISIONS[mode]))
 
     @property
     def precision(self) -> str:
         v = self._lib.mimi_get_precision(self._h)
         return {i: k for k, i in _lib.PRECISIONS.items()}[v]
+
+    @property
+    def f16_reruns(self) -> int:
+        """Encodes re-run with corrected activation scales (f16x3 mode)."""
+        return int(self._lib.mimi_f16_reruns(self._h))
 
     def set_profiling(self, enable: bool = True):
         _lib.check(self._lib.mimi_set_profiling(self._h, int(enable)))

@@ -44,10 +44,11 @@ void launch_bf(const GemmArgs& a, hipStream_t s) {
                        dim3(WM * WN * 64), 0, s, a);
 }
 
-template <int BM, int BN, int WM, int WN, int NS, int ST, int LW = 0>
+template <int BM, int BN, int WM, int WN, int NS, int ST, int LW = 0, int BK = 32, int MF = 32, int FL = 0,
+          bool F16 = false>
 void launch_pl(const GemmArgs& a, hipStream_t s) {
     const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.batch;
-    hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI_BIAS, 0, 0, LW>), dim3(nwg),
+    hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI_BIAS, 0, 0, LW, BK, MF, FL, F16>), dim3(nwg),
                        dim3((WM * WN + LW) * 64), 0, s, a);
 }
 
@@ -62,11 +63,20 @@ __global__ void split_planes(const float* x, __bf16* out, long long n) {
     }
 }
 
+__global__ void split_planes_f16(const float* x, _Float16* out, long long n, float sc) {
+    const long long i = blockIdx.x * 256LL + threadIdx.x;
+    if (i >= n) return;
+    const float r = x[i] * sc;
+    const _Float16 h = (_Float16)r;
+    out[i] = h;
+    out[n + i] = (_Float16)(r - (float)h);
+}
+
 struct Variant {
     const char* name;
     LaunchFn fn;
     int bk;
-    int ns;  // 0 = fp32 weights, else bf16 planes
+    int ns;  // 0 = fp32 weights, else bf16 planes (2, 3) or fp16 planes (12)
 };
 
 static uint16_t f2bf(float f) {
@@ -93,13 +103,17 @@ int main(int argc, char** argv) {
     };
     Variant vars[] = {
         {"f32 128x128 bk32 nb1", launch<128, 128, 2, 2, 32, 1, false>, 32, 0},
-        {"planes3 256x128 8w s2", launch_pl<256, 128, 4, 2, 3, 2>, 32, 3},
-        {"planes3 256x128 8w s2 +4ld", launch_pl<256, 128, 4, 2, 3, 2, 4>, 32, 3},
-        {"planes3 256x128 8w s2 +2ld", launch_pl<256, 128, 4, 2, 3, 2, 2>, 32, 3},
-        {"planes3 128x128 8w s3", launch_pl<128, 128, 4, 2, 3, 3>, 32, 3},
-        {"planes3 128x128 8w s3 +4ld", launch_pl<128, 128, 4, 2, 3, 3, 4>, 32, 3},
-        {"planes3 128x128 4w s3 +4ld", launch_pl<128, 128, 2, 2, 3, 3, 4>, 32, 3},
-        {"planes3 256x128 4w s2 +4ld", launch_pl<256, 128, 2, 2, 3, 2, 4>, 32, 3},
+        {"pl3 256x128 8w s2", launch_pl<256, 128, 4, 2, 3, 2>, 32, 3},
+        {"pl3 256x128 8w mf16 s2", launch_pl<256, 128, 4, 2, 3, 2, 0, 32, 16, 0>, 32, 3},
+        {"pl2 256x128 8w s3", launch_pl<256, 128, 4, 2, 2, 3>, 32, 2},
+        {"h2 256x128 8w s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 32, 0, true>, 32, 12},
+        {"h2 256x128 8w mf16 s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
+        {"h2 256x128 8w s2", launch_pl<256, 128, 4, 2, 2, 2, 0, 32, 32, 0, true>, 32, 12},
+        {"pl3 128x128 8w s3", launch_pl<128, 128, 4, 2, 3, 3>, 32, 3},
+        {"pl3 128x128 4w+4ld s3", launch_pl<128, 128, 2, 2, 3, 3, 4>, 32, 3},
+        {"h2 128x128 8w s4", launch_pl<128, 128, 4, 2, 2, 4, 0, 32, 32, 0, true>, 32, 12},
+        {"h2 128x128 8w mf16 s4", launch_pl<128, 128, 4, 2, 2, 4, 0, 32, 16, 0, true>, 32, 12},
+        {"h2 128x128 4w+4ld s4", launch_pl<128, 128, 2, 2, 2, 4, 4, 32, 32, 0, true>, 32, 12},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
@@ -146,7 +160,24 @@ int main(int argc, char** argv) {
         CK(hipMalloc(&Apl, 3 * nA * 2));
         hipLaunchKernelGGL(split_planes, dim3((unsigned)((nA + 255) / 256)), dim3(256), 0, 0, A, Apl, (long long)nA);
         CK(hipDeviceSynchronize());
+        // fp16 planes (2) of A * sa and W * sw, sa / sw powers of two putting max|A| at 2^7, max|W| at 2^14
+        float amax = 0, wmax = 0;
+        for (float v : hA) amax = fmaxf(amax, fabsf(v));
+        for (float v : hW) wmax = fmaxf(wmax, fabsf(v));
+        const float sa = ldexpf(1.0f, 7 - (int)ceilf(log2f(amax))), sw = ldexpf(1.0f, 14 - (int)ceilf(log2f(wmax)));
+        _Float16 *Ah, *Wh;
+        float* unsc;
+        CK(hipMalloc(&Ah, 2 * nA * 2));
+        CK(hipMalloc(&Wh, 2 * nW * 2));
+        CK(hipMalloc(&unsc, sh.batch * 4));
         CK(hipMemcpy(W, hW.data(), nW * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(split_planes_f16, dim3((unsigned)((nA + 255) / 256)), dim3(256), 0, 0, A, Ah, (long long)nA, sa);
+        hipLaunchKernelGGL(split_planes_f16, dim3((unsigned)((nW + 255) / 256)), dim3(256), 0, 0, W, Wh, (long long)nW, sw);
+        {
+            std::vector<float> hu(sh.batch, 1.0f / (sa * sw));
+            CK(hipMemcpy(unsc, hu.data(), sh.batch * 4, hipMemcpyHostToDevice));
+        }
+        CK(hipDeviceSynchronize());
         CK(hipMemcpy(bias, hb.data(), sh.N * 4, hipMemcpyHostToDevice));
         GemmArgs a{};
         a.A = A;
@@ -172,6 +203,13 @@ int main(int argc, char** argv) {
             a.C = v == 0 ? Cref : C;
             a.W = W;
             a.Wsplit = Wp;
+            a.Ap = Apl;
+            a.unscale = 0.0f;
+            if (vars[v].ns == 12) {
+                a.Wsplit = Wh;
+                a.Ap = Ah;
+                a.unscale = 1.0f / (sa * sw);
+            }
             if (vars[v].ns == 2) {
                 // NS = 2 reads planes [2][N][K]: the first two planes of the 3-plane buffer are exactly that
             }
@@ -205,6 +243,7 @@ int main(int argc, char** argv) {
             fflush(stdout);
         }
         CK(hipFree(A)); CK(hipFree(Apl)); CK(hipFree(W)); CK(hipFree(Wp)); CK(hipFree(bias)); CK(hipFree(C)); CK(hipFree(Cref));
+        CK(hipFree(Ah)); CK(hipFree(Wh)); CK(hipFree(unsc));
     }
     return 0;
 }

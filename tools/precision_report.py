@@ -29,7 +29,7 @@ from test_gpu_parity import margin_audit, rel_err  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "precision_report.json"))
-    ap.add_argument("--modes", default="f32,bf16x6,bf16x3")
+    ap.add_argument("--modes", default="f32,bf16x6,f16x3,bf16x3")
     args = ap.parse_args()
     with np.load(os.path.join(ROOT, "tests", "golden", "golden.npz")) as z:
         g = {k: z[k] for k in z.files}
