@@ -186,6 +186,8 @@ struct mimi_engine {
     // is VALU/phase-bound at one workgroup per CU and measured 1.81 ms vs 1.69 ms for the fp32-MFMA fused
     // kernel at B = 32 x 10 s (profiles/r1_ab_res128.txt)
     bool res128_split = false;
+    // PREC_F16X3: stage 0 on the fp16-plane fused kernel (MIMI_HIP_RES0_H16=0 falls back to the fp32-MFMA one)
+    bool res0_h16_on = true;
 
     std::unordered_map<std::string, std::vector<float>> host_w;
     std::unordered_map<std::string, std::vector<int64_t>> expected;  // name -> shape
@@ -193,6 +195,9 @@ struct mimi_engine {
 
     DevConv conv0;
     std::vector<DevConv> res3, res1, down;
+    // PREC_F16X3 fused stage-0 block: conv0 / W3 / W1 fp16-plane A fragments (resblock.hip r0h) and their scales
+    void* res0_h16 = nullptr;
+    float res0_wsc[3] = {1.0f, 1.0f, 1.0f};
     DevConv final_conv;
     std::vector<DevXfmr> xf;
     DevConv ds;
@@ -301,6 +306,27 @@ static int upload_f16(mimi_engine* e, void** dst, const std::vector<float>& host
     return MIMI_OK;
 }
 
+// power of two putting max|w| s in [2^13, 2^14) (see upload_f16)
+static float f16_weight_scale(const std::vector<float>& w) {
+    float wmax = 0.0f;
+    for (float v : w) wmax = std::max(wmax, std::fabs(v));
+    return wmax > 0.0f && std::isfinite(wmax) ? std::ldexp(1.0f, 13 - std::ilogb(wmax)) : 1.0f;
+}
+
+// Appends W [M][K] (row-major) * sc as fp16 planes in 32x32x16-MFMA A-fragment order, [mt][ks][plane] 1-KB
+// fragments of [64 lanes][8 halves]: lane (i, h) holds W[32 mt + i][16 ks + 8 h + e].
+static void append_afrags_h16(std::vector<_Float16>& out, const std::vector<float>& w, int M, int K, float sc) {
+    for (int mt = 0; mt < M / 32; ++mt)
+        for (int ks = 0; ks < K / 16; ++ks)
+            for (int pl = 0; pl < 2; ++pl)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int e = 0; e < 8; ++e) {
+                        const float t = w[(size_t)(32 * mt + (lane & 31)) * K + 16 * ks + 8 * (lane >> 5) + e] * sc;
+                        const _Float16 h0 = (_Float16)t;
+                        out.push_back(pl == 0 ? h0 : (_Float16)(t - (float)h0));
+                    }
+}
+
 // W [N][K] -> Wf[nt][kq][lane][s] = W[32*nt + (lane & 31)][8*kq + 4*(lane >> 5) + s]: a wave's B fragment
 // for one 8-wide K quad of one 32-column tile is one contiguous 1 KB load.
 static std::vector<float> frag_layout(const std::vector<float>& w, int N, int K) {
@@ -401,6 +427,7 @@ extern "C" int mimi_create(const mimi_config* cfg, int device, mimi_engine** out
     e->device = device;
     if (const char* uf = std::getenv("MIMI_HIP_UNFUSE_FROM")) e->unfuse_from = std::atoi(uf);
     if (const char* rs = std::getenv("MIMI_HIP_RES128_SPLIT")) e->res128_split = std::atoi(rs) != 0;
+    if (const char* r0 = std::getenv("MIMI_HIP_RES0_H16")) e->res0_h16_on = std::atoi(r0) != 0;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipEventCreateWithFlags(&e->ws_free, hipEventDisableTiming));
     HIP_TRY(hipMalloc(&e->amax_dev, ((size_t)kMaxActSlots * AMAX_SLOT_WORDS + kMaxActSlots) * sizeof(unsigned)));
@@ -631,6 +658,47 @@ static std::vector<float> relayout_conv(const std::vector<float>& w, int cout, i
     return o;
 }
 
+// The stage-0 fp16 block's weight image (resblock.hip resblock0_h16_kernel): 4 conv0 fragments
+// [mt][variant] -- variant 0: every lane (i, h) holds w_hi[32 mt + i][0..6], 0; variant 1: lanes h = 0 hold
+// w_lo, lanes h = 1 zeros (against the audio taps' hi | lo planes: w_hi a_hi + w_hi a_lo, then w_lo a_hi) --
+// then W3 [32][192] and W1 [64][32] as append_afrags_h16.
+static int make_res0_h16(mimi_engine* e) {
+    const mimi_config& c = e->cfg;
+    if (c.num_filters != 64 || c.kernel_size != 7 || c.residual_kernel_size != 3 || c.compress != 2) return MIMI_OK;
+    std::vector<float>*w0, *w3, *w1;
+    int rc;
+    if ((rc = get_w(e, "encoder.layers.0.conv.weight", &w0)) || (rc = get_w(e, "encoder.layers.1.block.1.conv.weight", &w3)) ||
+        (rc = get_w(e, "encoder.layers.1.block.3.conv.weight", &w1)))
+        return rc;
+    const std::vector<float> w3l = relayout_conv(*w3, 32, 64, 3);  // [32][3*64], tap-major
+    const std::vector<float>& w1l = *w1;                            // [64][32][1]
+    const float s0 = f16_weight_scale(*w0), s3 = f16_weight_scale(w3l), s1 = f16_weight_scale(w1l);
+    std::vector<_Float16> img;
+    img.reserve((size_t)RES0_H16_FRAGS * 512);
+    for (int mt = 0; mt < 2; ++mt)
+        for (int var = 0; var < 2; ++var)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int k = 0; k < 8; ++k) {
+                    _Float16 v = (_Float16)0.0f;
+                    if (k < 7) {
+                        const float t = (*w0)[(size_t)(32 * mt + (lane & 31)) * 7 + k] * s0;
+                        const _Float16 h0 = (_Float16)t;
+                        if (var == 0) v = h0;
+                        else if ((lane >> 5) == 0) v = (_Float16)(t - (float)h0);
+                    }
+                    img.push_back(v);
+                }
+    append_afrags_h16(img, w3l, 32, 192, s3);
+    append_afrags_h16(img, w1l, 64, 32, s1);
+    if (img.size() != (size_t)RES0_H16_FRAGS * 512) return set_err(MIMI_ERR_WEIGHTS, "res0 fp16 image size");
+    if ((rc = dev_alloc(e, &e->res0_h16, img.size() * sizeof(_Float16)))) return rc;
+    HIP_TRY(hipMemcpy(e->res0_h16, img.data(), img.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    e->res0_wsc[0] = s0;
+    e->res0_wsc[1] = s3;
+    e->res0_wsc[2] = s1;
+    return MIMI_OK;
+}
+
 static int make_conv(mimi_engine* e, DevConv& dc, const std::string& prefix, int cin, int cout, int k, int stride,
                      bool bias) {
     std::vector<float>* w;
@@ -702,6 +770,7 @@ extern "C" int mimi_finalize(mimi_engine* e) {
         idx += 1;
         C *= 2;
     }
+    if ((rc = make_res0_h16(e))) return rc;
     idx += 1;
     if ((rc = make_conv(e, e->final_conv, "encoder.layers." + std::to_string(idx) + ".conv.", C, c.hidden_size,
                         c.last_kernel_size, 1, true)))
@@ -1132,6 +1201,21 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             yact = new_act();
             ra.yscale = yact.scale;
             ra.yamax = yact.amax;
+            if (si == 0 && h16 && e->res0_h16 && e->res0_h16_on &&
+                (unsigned long long)B * (unsigned long long)((T + 31) / 32) < (1ull << 32)) {
+                // fp16-plane stage-0 block: audio, ELU(x0) and ELU(h) are split in-kernel, each at its own scale
+                const Act aa = new_act(), xa = new_act(), ha = new_act();
+                ra.wh16 = e->res0_h16;
+                ra.ascale = aa.scale;
+                ra.xscale = xa.scale;
+                ra.hscale = ha.scale;
+                ra.unscale0 = 1.0f / (aa.scale * e->res0_wsc[0]);
+                ra.unscale1 = 1.0f / (xa.scale * e->res0_wsc[1]);
+                ra.unscale2 = 1.0f / (ha.scale * e->res0_wsc[2]);
+                ra.aamax = aa.amax;
+                ra.xamax = xa.amax;
+                ra.hamax = ha.amax;
+            }
             if (ns && !h16 && C == 128 && e->res128_split) {  // split-bf16 fused block (resblock.hip)
                 ra.w3s = e->res3[si].wsplit;
                 ra.w1s = e->res1[si].wsplit;

@@ -200,8 +200,19 @@ struct ResArgs {
     const float* w1frag;
     const void* w3s;      // optional: W3 / W1 as 3 bf16 planes [3][N][K] (split-bf16 fused block, C = 128)
     const void* w1s;
+    // PREC_F16X3 fused block (stage 0: resblock0_h16_kernel): weights as 2 scaled fp16 planes in 32x32x16-MFMA
+    // A-fragment order (layout in resblock.hip, built by engine.cpp make_res_h16).  The block's inputs and
+    // internal operands are split in-kernel at power-of-two scales chosen by the engine; each one's max|v| is
+    // max-reduced into its activation slot for the range check.  unscale* = 1 / (operand scale x weight scale).
+    const void* wh16;
+    float ascale, xscale, hscale;     // audio (conv0 input), ELU(x) (conv3 input), ELU(h) (conv1 input)
+    float unscale0, unscale1, unscale2;
+    unsigned *aamax, *xamax, *hamax;
 };
 hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** kname);
+
+// fp16-plane fused stage-0 block: fragment buffer size in halves ([frag][64 lanes][8])
+constexpr int RES0_H16_FRAGS = 36;
 
 // conv0: Cin = 1, k = 7 causal conv, channels-last output [B][T][64].
 hipError_t launch_conv0(const float* x, long long L, int batch, const float* w /*[64][7]*/,

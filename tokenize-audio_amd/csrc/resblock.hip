@@ -738,6 +738,260 @@ __global__ __launch_bounds__(256) void resblock128_split_kernel(ResArgs p) {
 #endif
 }
 
+// ------------------------------------------------------------------------------------------------
+// Stage 0 on the fp16 matrix cores (PREC_F16X3): conv0 (1 -> 64, k7) + residual block (64 -> 32 -> 64) + ELU,
+// persistent and wave-autonomous.  Every operand is 2 fp16 planes at a power-of-two scale (x s = h0 + h1,
+// 22-bit significand) and each GEMM takes the 3 significant plane products, on v_mfma_f32_32x32x16_f16.
+//
+// Everything is computed TRANSPOSED: the weights are the A operand (rows = output channels) and time is the
+// MFMA column, so a lane's accumulator holds one time step x 4 consecutive channels per 4-row group -- the
+// layout in which it writes the next operand (8-B LDS rows, 8-B y-plane stores) and in which conv0's output
+// is already the identity skip of the block (kept in registers, never re-read).
+//
+// One wave walks a contiguous range of 32-step tiles (8 waves per CU, one workgroup per CU); per tile:
+//   conv0   x0^T[64][32] = W0 . audio-taps^T: K = 16 = 7 taps of the audio's hi plane (lanes 0-31) | 7 of its
+//           lo plane (lanes 32-63): 2 MFMAs per 32 channels give w_hi a_hi + w_hi a_lo + w_lo a_hi
+//   slab    ELU(x0) -> planes, rows 2..33 of the wave's [34][64] slab; rows 0, 1 (causal halo) are the
+//           previous tile's rows 32, 33 (or zeros at t = 0, or conv0 of the preceding tile at a range start:
+//           the same arithmetic, so a row never depends on which wave computed it)
+//   GEMM1   h^T[32][32] = W3[32][192] . slab-windows^T (K = tap-major 3 x 64)    36 MFMAs
+//   h       ELU(h + b3) -> planes [32 t][32 ch] in LDS
+//   GEMM2   y^T[64][32] = W1[64][32] . h^T                                        12 MFMAs
+//   out     y = ELU(x0 + (acc + b1)) -> 2 fp16 planes of y * yscale (8-B stores)
+// No barrier after the weight load: waves drift apart, so one's VALU (ELU, splits) overlaps another's MFMAs.
+// LDS: weights 36 KB + biases + 8 x 14.75 KB per-wave slab / h / audio window = 154.6 KB.
+// ------------------------------------------------------------------------------------------------
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+namespace r0h {
+constexpr int SLD = 72, SROWS = 34, SPL = SROWS * SLD;  // slab [2 planes][34][72 halves]: 144-B rows, 36 dwords
+constexpr int HLD = 40, HPL = 32 * HLD;                 // h [2][32][40]: 80-B rows (both odd multiples of 16 B:
+                                                        // conflict-free ds_read_b128 column reads)
+constexpr int AUD = 48;                                 // audio window floats
+constexpr int WAVE_BYTES = 2 * SPL * 2 + 2 * HPL * 2 + AUD * 4;
+constexpr int NW = 8;
+constexpr int FR_W0 = 0, FR_W3 = 4, FR_W1 = 28, NFRAG = 36;  // 1-KB A fragments [64 lanes][8 halves]
+constexpr int BIAS = 64 + 32 + 64;                           // b0 | b3 | b1
+constexpr int LDS_BYTES = NFRAG * 1024 + BIAS * 4 + NW * WAVE_BYTES;
+static_assert(NFRAG == RES0_H16_FRAGS, "fragment count");
+static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+}  // namespace r0h
+
+__device__ __forceinline__ f32x16 mfma_h(f16x8 a, f16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// 4 values -> fp16 planes of v * s (hi = fp16(v s), lo = fp16(v s - hi)); packed conversions
+__device__ __forceinline__ void split4_h(const float (&v)[4], float s, f16x4& hi, f16x4& lo) {
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {
+        const f32x2 t = {v[q] * s, v[q + 1] * s};
+        const f16x2 h = __builtin_convertvector(t, f16x2);
+        const f16x2 l = __builtin_convertvector(t - __builtin_convertvector(h, f32x2), f16x2);
+        hi[q] = h[0];
+        hi[q + 1] = h[1];
+        lo[q] = l[0];
+        lo[q + 1] = l[1];
+    }
+}
+
+__global__ __launch_bounds__(512) void resblock0_h16_kernel(ResArgs p) {
+    using namespace r0h;
+    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(p.wh16);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (int i = tid; i < NFRAG * 64; i += 512) dst[i] = src[i];
+        float* bw = reinterpret_cast<float*>(lds + NFRAG * 1024);
+        if (tid < 64) {
+            bw[tid] = p.b0[tid];
+            bw[96 + tid] = p.b1[tid];
+        }
+        if (tid < 32) bw[64 + tid] = p.b3[tid];
+    }
+    __syncthreads();
+    const f16x8* wf = reinterpret_cast<const f16x8*>(lds);
+    const float* bl = reinterpret_cast<const float*>(lds + NFRAG * 1024);
+    char* wb = lds + NFRAG * 1024 + BIAS * 4 + wave * WAVE_BYTES;
+    _Float16* slab = reinterpret_cast<_Float16*>(wb);
+    _Float16* hb = slab + 2 * SPL;
+    float* aud = reinterpret_cast<float*>(hb + 2 * HPL);
+
+    const long long T = p.T;
+    const unsigned tpi = (unsigned)((T + 31) >> 5);  // tiles per item (host checks B x tpi < 2^32)
+    const unsigned long long NT = (unsigned long long)tpi * p.batch;
+    const unsigned long long W = (unsigned long long)gridDim.x * NW;
+    const unsigned long long wid = (unsigned long long)blockIdx.x * NW + wave;
+    const unsigned g0 = (unsigned)(wid * NT / W), g1 = (unsigned)((wid + 1) * NT / W);
+    const int j = lane & 31, hh = lane >> 5;
+    const float sa = p.ascale, sx = p.xscale, sh = p.hscale, sy = p.yscale;
+    const float u0 = p.unscale0, u1 = p.unscale1, u2 = p.unscale2;
+    float mxa = 0.0f, mxx = 0.0f, mxh = 0.0f, mxy = 0.0f;
+
+    // x0^T for the 32 steps t0 .. t0+31 (lane column j = step t0 + j), + b0
+    auto conv0 = [&](unsigned b, long long t0, f32x16 (&x0)[2]) {
+        if (lane < AUD) {
+            const long long pos = t0 - 8 + lane;
+            const float v = (pos >= 0 && pos < T) ? p.audio[(long long)b * T + pos] : 0.0f;
+            mxa = fmaxf(mxa, fabsf(v));
+            aud[lane] = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        f16x8 bq;  // taps audio[t - 6 + k], k = 0..7 (k = 7 has zero weight): hi plane (hh = 0) | lo plane
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+            const f32x2 t = {aud[j + 2 + k] * sa, aud[j + 3 + k] * sa};
+            const f16x2 h = __builtin_convertvector(t, f16x2);
+            const f16x2 l = __builtin_convertvector(t - __builtin_convertvector(h, f32x2), f16x2);
+            bq[k] = hh ? l[0] : h[0];
+            bq[k + 1] = hh ? l[1] : h[1];
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+            acc = mfma_h(wf[(FR_W0 + 2 * mt + 1) * 64 + lane], bq, acc);  // w_lo a_hi
+            acc = mfma_h(wf[(FR_W0 + 2 * mt) * 64 + lane], bq, acc);      // w_hi a_hi + w_hi a_lo
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 32 * mt + 8 * g + 4 * hh);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) x0[mt][4 * g + q] = acc[4 * g + q] * u0 + bb[q];
+            }
+        }
+    };
+    // ELU(x0) planes -> slab row j + rowoff (rows outside [0, 34) skipped)
+    auto slab_put = [&](const f32x16 (&x0)[2], int rowoff) {
+        const int row = j + rowoff;
+        if (row < 0 || row >= SROWS) return;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float e[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    e[q] = elu_f(x0[mt][4 * g + q]);
+                    mxx = fmaxf(mxx, fabsf(e[q]));
+                }
+                f16x4 hi, lo;
+                split4_h(e, sx, hi, lo);
+                const int o = row * SLD + 32 * mt + 8 * g + 4 * hh;
+                *reinterpret_cast<f16x4*>(slab + o) = hi;
+                *reinterpret_cast<f16x4*>(slab + SPL + o) = lo;
+            }
+    };
+    // 2 slab rows per plane: lane -> (plane, row, 4 halves)
+    const int cpl = lane >> 5, crow = (lane >> 4) & 1, cc = (lane & 15) * 4;
+
+    for (unsigned g = g0; g < g1; ++g) {
+        const unsigned b = g / tpi;
+        const long long t0 = (long long)(g - b * tpi) * 32;
+        if (t0 == 0) {  // causal zero padding of ELU(x0) before t = 0
+            const f16x4 z = {0, 0, 0, 0};
+            *reinterpret_cast<f16x4*>(slab + cpl * SPL + crow * SLD + cc) = z;
+        } else if (g == g0) {  // range start inside an item: halo rows from the preceding tile's conv0
+            f32x16 xp[2];
+            conv0(b, t0 - 32, xp);
+            slab_put(xp, -30);
+        }
+        f32x16 x0[2];
+        conv0(b, t0, x0);
+        slab_put(x0, 2);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+        // ---- GEMM1: h^T = W3 . windows^T, k = 16 ks + 8 hh + e -> tap ks / 4, channel 16 (ks % 4) + 8 hh + e
+        f32x16 acc1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc1[r] = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < 12; ++ks) {
+            const int o = (j + (ks >> 2)) * SLD + (ks & 3) * 16 + 8 * hh;
+            const f16x8 bx0 = *reinterpret_cast<const f16x8*>(slab + o);
+            const f16x8 bx1 = *reinterpret_cast<const f16x8*>(slab + SPL + o);
+            const f16x8 aw0 = wf[(FR_W3 + 2 * ks) * 64 + lane];
+            const f16x8 aw1 = wf[(FR_W3 + 2 * ks + 1) * 64 + lane];
+            acc1 = mfma_h(aw1, bx0, acc1);
+            acc1 = mfma_h(aw0, bx1, acc1);
+            acc1 = mfma_h(aw0, bx0, acc1);
+        }
+        // ---- h = ELU(acc + b3) -> planes, row j, channels 8g + 4hh .. +3
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 64 + 8 * gq + 4 * hh);
+            float e[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                e[q] = elu_f(acc1[4 * gq + q] * u1 + bb[q]);
+                mxh = fmaxf(mxh, fabsf(e[q]));
+            }
+            f16x4 hi, lo;
+            split4_h(e, sh, hi, lo);
+            const int o = j * HLD + 8 * gq + 4 * hh;
+            *reinterpret_cast<f16x4*>(hb + o) = hi;
+            *reinterpret_cast<f16x4*>(hb + HPL + o) = lo;
+        }
+        // halo for the next tile: slab rows 32, 33 -> 0, 1 (GEMM1's reads of them have been consumed)
+        {
+            _Float16* sp = slab + cpl * SPL;
+            const f16x4 v = *reinterpret_cast<const f16x4*>(sp + (32 + crow) * SLD + cc);
+            *reinterpret_cast<f16x4*>(sp + crow * SLD + cc) = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+        // ---- GEMM2: y^T = W1 . h^T
+        f32x16 acc2[2];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc2[mt][r] = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int o = j * HLD + ks * 16 + 8 * hh;
+            const f16x8 bh0 = *reinterpret_cast<const f16x8*>(hb + o);
+            const f16x8 bh1 = *reinterpret_cast<const f16x8*>(hb + HPL + o);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                const f16x8 aw0 = wf[(FR_W1 + (mt * 2 + ks) * 2) * 64 + lane];
+                const f16x8 aw1 = wf[(FR_W1 + (mt * 2 + ks) * 2 + 1) * 64 + lane];
+                acc2[mt] = mfma_h(aw1, bh0, acc2[mt]);
+                acc2[mt] = mfma_h(aw0, bh1, acc2[mt]);
+                acc2[mt] = mfma_h(aw0, bh0, acc2[mt]);
+            }
+        }
+        // ---- y = ELU(x0 + (acc + b1)) -> 2 fp16 planes of y * yscale
+        const long long row = t0 + j;
+        if (row < T) {
+            _Float16* yb = reinterpret_cast<_Float16*>(p.yp) + ((long long)b * T + row) * 64 + 4 * hh;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int gq = 0; gq < 4; ++gq) {
+                    const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 96 + 32 * mt + 8 * gq + 4 * hh);
+                    float e[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        e[q] = elu_f(x0[mt][4 * gq + q] + (acc2[mt][4 * gq + q] * u2 + bb[q]));
+                        mxy = fmaxf(mxy, fabsf(e[q]));
+                    }
+                    f16x4 hi, lo;
+                    split4_h(e, sy, hi, lo);
+                    *reinterpret_cast<f16x4*>(yb + 32 * mt + 8 * gq) = hi;
+                    *reinterpret_cast<f16x4*>(yb + p.y_pstride + 32 * mt + 8 * gq) = lo;
+                }
+        }
+    }
+    amax_commit(p.aamax, mxa);
+    amax_commit(p.xamax, mxx);
+    amax_commit(p.hamax, mxh);
+    amax_commit(p.yamax, mxy);
+}
+
 template <int C, int BM, bool WINDOW, bool FIRST, int W1M, int W1N, int W2M, int W2N, int NP>
 static hipError_t run_res(const ResArgs& a, hipStream_t s, const char** kname) {
     static char name[160];
@@ -754,6 +1008,16 @@ hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** 
     if (a.T <= 0 || a.batch <= 0) return hipErrorInvalidValue;
     switch (C) {
         case 64:
+            if (a.audio && a.wh16) {
+                static const char* nm = "mimi::resblock0_h16_kernel(mimi::ResArgs)";
+                if (kname) *kname = nm;
+                // persistent: one workgroup (8 waves, 154.6 KB of LDS) per CU, each wave a range of tiles
+                int dev = 0, ncu = 256;
+                (void)hipGetDevice(&dev);
+                (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+                hipLaunchKernelGGL(resblock0_h16_kernel, dim3((unsigned)ncu), dim3(512), 0, s, a);
+                return hipGetLastError();
+            }
             if (a.audio && a.w3frag && a.w1frag) {
                 static const char* nm = "mimi::resblock0_wave_kernel(mimi::ResArgs)";
                 if (kname) *kname = nm;
