@@ -1213,6 +1213,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                 ra.unscale1 = 1.0f / (xa.scale * e->res0_wsc[1]);
                 ra.unscale2 = 1.0f / (ha.scale * e->res0_wsc[2]);
                 ra.aamax = aa.amax;
+                if (const char* d = std::getenv("MIMI_HIP_DBG")) ra.dbg = std::atoi(d);
                 ra.xamax = xa.amax;
                 ra.hamax = ha.amax;
             }

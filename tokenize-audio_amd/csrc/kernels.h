@@ -208,6 +208,7 @@ struct ResArgs {
     float ascale, xscale, hscale;     // audio (conv0 input), ELU(x) (conv3 input), ELU(h) (conv1 input)
     float unscale0, unscale1, unscale2;
     unsigned *aamax, *xamax, *hamax;
+    int dbg;  // experiment flags (MIMI_HIP_DBG), 0 in production
 };
 hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** kname);
 

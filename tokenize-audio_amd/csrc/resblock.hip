@@ -755,11 +755,11 @@ __global__ __launch_bounds__(256) void resblock128_split_kernel(ResArgs p) {
 //           previous tile's rows 32, 33 (or zeros at t = 0, or conv0 of the preceding tile at a range start:
 //           the same arithmetic, so a row never depends on which wave computed it)
 //   GEMM1   h^T[32][32] = W3[32][192] . slab-windows^T (K = tap-major 3 x 64)    36 MFMAs
-//   h       ELU(h + b3) -> planes [32 t][32 ch] in LDS
+//   h       ELU(h + b3) -> planes [32 t][32 ch] in LDS, over slab rows 2..33 (after the halo is copied)
 //   GEMM2   y^T[64][32] = W1[64][32] . h^T                                        12 MFMAs
-//   out     y = ELU(x0 + (acc + b1)) -> 2 fp16 planes of y * yscale (8-B stores)
+//   out     y = ELU(x0 + (acc + b1)) -> 2 fp16 planes of y * yscale, staged in LDS -> 1-KB row stores
 // No barrier after the weight load: waves drift apart, so one's VALU (ELU, splits) overlaps another's MFMAs.
-// LDS: weights 36 KB + biases + 8 x 14.75 KB per-wave slab / h / audio window = 154.6 KB.
+// LDS: weights 36 KB + biases + 8 x 9.75 KB per-wave slab / audio window = 114.6 KB.
 // ------------------------------------------------------------------------------------------------
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -767,10 +767,10 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace r0h {
 constexpr int SLD = 72, SROWS = 34, SPL = SROWS * SLD;  // slab [2 planes][34][72 halves]: 144-B rows, 36 dwords
-constexpr int HLD = 40, HPL = 32 * HLD;                 // h [2][32][40]: 80-B rows (both odd multiples of 16 B:
-                                                        // conflict-free ds_read_b128 column reads)
+                                                        // (an odd multiple of 16 B: conflict-free ds_read_b128
+                                                        // column reads); h [2][32][32] reuses rows 2..33
 constexpr int AUD = 48;                                 // audio window floats
-constexpr int WAVE_BYTES = 2 * SPL * 2 + 2 * HPL * 2 + AUD * 4;
+constexpr int WAVE_BYTES = 2 * SPL * 2 + AUD * 4;
 constexpr int NW = 8;
 constexpr int FR_W0 = 0, FR_W3 = 4, FR_W1 = 28, NFRAG = 36;  // 1-KB A fragments [64 lanes][8 halves]
 constexpr int BIAS = 64 + 32 + 64;                           // b0 | b3 | b1
@@ -783,17 +783,43 @@ __device__ __forceinline__ f32x16 mfma_h(f16x8 a, f16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-// 4 values -> fp16 planes of v * s (hi = fp16(v s), lo = fp16(v s - hi)); packed conversions
-__device__ __forceinline__ void split4_h(const float (&v)[4], float s, f16x4& hi, f16x4& lo) {
+// fp16 planes of 4 already-scaled values t: hi = fp16(t) (packed converts), lo = fp16(t - hi), the difference
+// taken exactly in fp32 and rounded once by v_fma_mix{lo,hi}_f16 (the same bits as fp16(t - (float)hi), 2
+// instructions instead of 4 per pair)
+__device__ __forceinline__ void split4_t(const float (&t)[4], uint2& hi, uint2& lo) {
+    unsigned hu[2], lu[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const f16x2 h = __builtin_convertvector((f32x2){t[2 * q], t[2 * q + 1]}, f16x2);
+        hu[q] = __builtin_bit_cast(unsigned, h);
+        asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+            "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+            : "=&v"(lu[q])
+            : "v"(hu[q]), "v"(t[2 * q]), "v"(t[2 * q + 1]));
+    }
+    hi = make_uint2(hu[0], hu[1]);
+    lo = make_uint2(lu[0], lu[1]);
+}
+
+// ELU(z) * s for a power-of-two s, two values at a time: med3(z s, fma(exp(z), s, -s), 0).  For z > 0 the
+// median is z s (exp(z) - 1 > z); for z <= 0 it is (exp(z) - 1) s (z <= exp(z) - 1 <= 0).  That is elu_fast's
+// select (exp as v_exp_f32 of z log2(e)) followed by an exact scaling, bit for bit, with no compare.
+__device__ __forceinline__ f32x2 elu_s2(f32x2 z, float s) {
+    const f32x2 l = z * 1.44269504f;
+    const f32x2 e = {__builtin_amdgcn_exp2f(l[0]), __builtin_amdgcn_exp2f(l[1])};
+    const f32x2 n = __builtin_elementwise_fma(e, (f32x2){s, s}, (f32x2){-s, -s});
+    const f32x2 zs = z * s;
+    return (f32x2){__builtin_amdgcn_fmed3f(zs[0], n[0], 0.0f), __builtin_amdgcn_fmed3f(zs[1], n[1], 0.0f)};
+}
+
+// 4 values z -> t = ELU(z) * s, max |t| into mx
+__device__ __forceinline__ void elu_s4(const float (&z)[4], float s, float (&t)[4], float& mx) {
 #pragma unroll
     for (int q = 0; q < 4; q += 2) {
-        const f32x2 t = {v[q] * s, v[q + 1] * s};
-        const f16x2 h = __builtin_convertvector(t, f16x2);
-        const f16x2 l = __builtin_convertvector(t - __builtin_convertvector(h, f32x2), f16x2);
-        hi[q] = h[0];
-        hi[q + 1] = h[1];
-        lo[q] = l[0];
-        lo[q + 1] = l[1];
+        const f32x2 r = elu_s2((f32x2){z[q], z[q + 1]}, s);
+        t[q] = r[0];
+        t[q + 1] = r[1];
+        asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(r[0]), "v"(r[1]));
     }
 }
 
@@ -805,7 +831,7 @@ __global__ __launch_bounds__(512) void resblock0_h16_kernel(ResArgs p) {
     {
         const uint4* src = reinterpret_cast<const uint4*>(p.wh16);
         uint4* dst = reinterpret_cast<uint4*>(lds);
-        for (int i = tid; i < NFRAG * 64; i += 512) dst[i] = src[i];
+        for (int i = tid; i < NFRAG * 64; i += NW * 64) dst[i] = src[i];
         float* bw = reinterpret_cast<float*>(lds + NFRAG * 1024);
         if (tid < 64) {
             bw[tid] = p.b0[tid];
@@ -818,8 +844,8 @@ __global__ __launch_bounds__(512) void resblock0_h16_kernel(ResArgs p) {
     const float* bl = reinterpret_cast<const float*>(lds + NFRAG * 1024);
     char* wb = lds + NFRAG * 1024 + BIAS * 4 + wave * WAVE_BYTES;
     _Float16* slab = reinterpret_cast<_Float16*>(wb);
-    _Float16* hb = slab + 2 * SPL;
-    float* aud = reinterpret_cast<float*>(hb + 2 * HPL);
+    _Float16* hb = slab + 2 * SLD;  // h plane p, row j at hb + p * SPL + j * SLD (after GEMM1)
+    float* aud = reinterpret_cast<float*>(slab + 2 * SPL);
 
     const long long T = p.T;
     const unsigned tpi = (unsigned)((T + 31) >> 5);  // tiles per item (host checks B x tpi < 2^32)
@@ -830,15 +856,19 @@ __global__ __launch_bounds__(512) void resblock0_h16_kernel(ResArgs p) {
     const int j = lane & 31, hh = lane >> 5;
     const float sa = p.ascale, sx = p.xscale, sh = p.hscale, sy = p.yscale;
     const float u0 = p.unscale0, u1 = p.unscale1, u2 = p.unscale2;
-    float mxa = 0.0f, mxx = 0.0f, mxh = 0.0f, mxy = 0.0f;
+    float mxa = 0.0f, mxx = 0.0f, mxh = 0.0f, mxy = 0.0f;  // max |audio|, then max |scaled operand|
 
-    // x0^T for the 32 steps t0 .. t0+31 (lane column j = step t0 + j), + b0
-    auto conv0 = [&](unsigned b, long long t0, f32x16 (&x0)[2]) {
+    // lane's audio-window value of tile gg: audio[t0 - 8 + lane] (lanes < AUD; zero outside [0, T))
+    auto aload = [&](unsigned gg) {
+        const unsigned bb = gg / tpi;
+        const long long pos = (long long)(gg - bb * tpi) * 32 - 8 + lane;
+        return (lane < AUD && pos >= 0 && pos < T) ? p.audio[(long long)bb * T + pos] : 0.0f;
+    };
+    // x0^T for the tile's 32 steps (lane column j = step t0 + j) from its audio window value av, + b0
+    auto conv0 = [&](float av, f32x16 (&x0)[2]) {
         if (lane < AUD) {
-            const long long pos = t0 - 8 + lane;
-            const float v = (pos >= 0 && pos < T) ? p.audio[(long long)b * T + pos] : 0.0f;
-            mxa = fmaxf(mxa, fabsf(v));
-            aud[lane] = v;
+            mxa = fmaxf(mxa, fabsf(av));
+            aud[lane] = av;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         f16x8 bq;  // taps audio[t - 6 + k], k = 0..7 (k = 7 has zero weight): hi plane (hh = 0) | lo plane
@@ -861,7 +891,7 @@ __global__ __launch_bounds__(512) void resblock0_h16_kernel(ResArgs p) {
             for (int g = 0; g < 4; ++g) {
                 const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 32 * mt + 8 * g + 4 * hh);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) x0[mt][4 * g + q] = acc[4 * g + q] * u0 + bb[q];
+                for (int q = 0; q < 4; ++q) x0[mt][4 * g + q] = __builtin_fmaf(acc[4 * g + q], u0, bb[q]);  // acc u0 exact
             }
         }
     };
@@ -873,35 +903,34 @@ __global__ __launch_bounds__(512) void resblock0_h16_kernel(ResArgs p) {
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                float e[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    e[q] = elu_f(x0[mt][4 * g + q]);
-                    mxx = fmaxf(mxx, fabsf(e[q]));
-                }
-                f16x4 hi, lo;
-                split4_h(e, sx, hi, lo);
+                const float z[4] = {x0[mt][4 * g], x0[mt][4 * g + 1], x0[mt][4 * g + 2], x0[mt][4 * g + 3]};
+                float t[4];
+                elu_s4(z, sx, t, mxx);
+                uint2 hi, lo;
+                split4_t(t, hi, lo);
                 const int o = row * SLD + 32 * mt + 8 * g + 4 * hh;
-                *reinterpret_cast<f16x4*>(slab + o) = hi;
-                *reinterpret_cast<f16x4*>(slab + SPL + o) = lo;
+                *reinterpret_cast<uint2*>(slab + o) = hi;
+                *reinterpret_cast<uint2*>(slab + SPL + o) = lo;
             }
     };
     // 2 slab rows per plane: lane -> (plane, row, 4 halves)
     const int cpl = lane >> 5, crow = (lane >> 4) & 1, cc = (lane & 15) * 4;
 
+    float anext = g0 < g1 ? aload(g0) : 0.0f;
     for (unsigned g = g0; g < g1; ++g) {
         const unsigned b = g / tpi;
         const long long t0 = (long long)(g - b * tpi) * 32;
         if (t0 == 0) {  // causal zero padding of ELU(x0) before t = 0
-            const f16x4 z = {0, 0, 0, 0};
-            *reinterpret_cast<f16x4*>(slab + cpl * SPL + crow * SLD + cc) = z;
+            *reinterpret_cast<uint2*>(slab + cpl * SPL + crow * SLD + cc) = make_uint2(0u, 0u);
         } else if (g == g0) {  // range start inside an item: halo rows from the preceding tile's conv0
             f32x16 xp[2];
-            conv0(b, t0 - 32, xp);
+            conv0(aload(g - 1), xp);
             slab_put(xp, -30);
         }
+        const float acur = anext;
+        if (g + 1 < g1) anext = aload(g + 1);  // the next tile's audio flies under this tile
         f32x16 x0[2];
-        conv0(b, t0, x0);
+        conv0(acur, x0);
         slab_put(x0, 2);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
@@ -920,27 +949,27 @@ __global__ __launch_bounds__(512) void resblock0_h16_kernel(ResArgs p) {
             acc1 = mfma_h(aw0, bx1, acc1);
             acc1 = mfma_h(aw0, bx0, acc1);
         }
+        // halo for the next tile: slab rows 32, 33 -> 0, 1 (GEMM1's reads of the slab have been
+        // consumed); then h overwrites rows 2..33
+        {
+            _Float16* sp = slab + cpl * SPL;
+            const uint2 v = *reinterpret_cast<const uint2*>(sp + (32 + crow) * SLD + cc);
+            *reinterpret_cast<uint2*>(sp + crow * SLD + cc) = v;
+        }
+        asm volatile("" ::: "memory");
         // ---- h = ELU(acc + b3) -> planes, row j, channels 8g + 4hh .. +3
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
             const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 64 + 8 * gq + 4 * hh);
-            float e[4];
+            float z[4], t[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                e[q] = elu_f(acc1[4 * gq + q] * u1 + bb[q]);
-                mxh = fmaxf(mxh, fabsf(e[q]));
-            }
-            f16x4 hi, lo;
-            split4_h(e, sh, hi, lo);
-            const int o = j * HLD + 8 * gq + 4 * hh;
-            *reinterpret_cast<f16x4*>(hb + o) = hi;
-            *reinterpret_cast<f16x4*>(hb + HPL + o) = lo;
-        }
-        // halo for the next tile: slab rows 32, 33 -> 0, 1 (GEMM1's reads of them have been consumed)
-        {
-            _Float16* sp = slab + cpl * SPL;
-            const f16x4 v = *reinterpret_cast<const f16x4*>(sp + (32 + crow) * SLD + cc);
-            *reinterpret_cast<f16x4*>(sp + crow * SLD + cc) = v;
+            for (int q = 0; q < 4; ++q) z[q] = __builtin_fmaf(acc1[4 * gq + q], u1, bb[q]);
+            elu_s4(z, sh, t, mxh);
+            uint2 hi, lo;
+            split4_t(t, hi, lo);
+            const int o = j * SLD + 8 * gq + 4 * hh;
+            *reinterpret_cast<uint2*>(hb + o) = hi;
+            *reinterpret_cast<uint2*>(hb + SPL + o) = lo;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
@@ -952,9 +981,9 @@ __global__ __launch_bounds__(512) void resblock0_h16_kernel(ResArgs p) {
             for (int r = 0; r < 16; ++r) acc2[mt][r] = 0.0f;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            const int o = j * HLD + ks * 16 + 8 * hh;
+            const int o = j * SLD + ks * 16 + 8 * hh;
             const f16x8 bh0 = *reinterpret_cast<const f16x8*>(hb + o);
-            const f16x8 bh1 = *reinterpret_cast<const f16x8*>(hb + HPL + o);
+            const f16x8 bh1 = *reinterpret_cast<const f16x8*>(hb + SPL + o);
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 const f16x8 aw0 = wf[(FR_W1 + (mt * 2 + ks) * 2) * 64 + lane];
@@ -964,32 +993,45 @@ __global__ __launch_bounds__(512) void resblock0_h16_kernel(ResArgs p) {
                 acc2[mt] = mfma_h(aw0, bh0, acc2[mt]);
             }
         }
-        // ---- y = ELU(x0 + (acc + b1)) -> 2 fp16 planes of y * yscale
-        const long long row = t0 + j;
-        if (row < T) {
-            _Float16* yb = reinterpret_cast<_Float16*>(p.yp) + ((long long)b * T + row) * 64 + 4 * hh;
+        // ---- y = ELU(x0 + (acc + b1)) -> 2 fp16 planes of y * yscale, staged in slab rows 2..33 (h has been
+        // consumed), then written as whole 128-B rows: each store instruction covers 8 consecutive steps = 1 KB
+        float tmy = 0.0f;
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+        for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 96 + 32 * mt + 8 * gq + 4 * hh);
-                    float e[4];
+            for (int gq = 0; gq < 4; ++gq) {
+                const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 96 + 32 * mt + 8 * gq + 4 * hh);
+                float z[4], t[4];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        e[q] = elu_f(x0[mt][4 * gq + q] + (acc2[mt][4 * gq + q] * u2 + bb[q]));
-                        mxy = fmaxf(mxy, fabsf(e[q]));
-                    }
-                    f16x4 hi, lo;
-                    split4_h(e, sy, hi, lo);
-                    *reinterpret_cast<f16x4*>(yb + 32 * mt + 8 * gq) = hi;
-                    *reinterpret_cast<f16x4*>(yb + p.y_pstride + 32 * mt + 8 * gq) = lo;
+                for (int q = 0; q < 4; ++q) z[q] = x0[mt][4 * gq + q] + __builtin_fmaf(acc2[mt][4 * gq + q], u2, bb[q]);
+                elu_s4(z, sy, t, tmy);
+                uint2 hi, lo;
+                split4_t(t, hi, lo);
+                const int o = j * SLD + 32 * mt + 8 * gq + 4 * hh;
+                *reinterpret_cast<uint2*>(hb + o) = hi;
+                *reinterpret_cast<uint2*>(hb + SPL + o) = lo;
+            }
+        if (t0 + j < T) mxy = fmaxf(mxy, tmy);  // steps past the end are not stored, not in max|y|
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (!(p.dbg & 1)) {
+            const int sr = lane >> 3, sc = (lane & 7) * 8;
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+                for (int it = 0; it < 4; ++it) {
+                    const int r = it * 8 + sr;
+                    const uint4 v = *reinterpret_cast<const uint4*>(hb + pl * SPL + r * SLD + sc);
+                    if (t0 + r < T)
+                        *reinterpret_cast<uint4*>(reinterpret_cast<_Float16*>(p.yp) + pl * p.y_pstride +
+                                                  ((long long)b * T + t0 + r) * 64 + sc) = v;
                 }
         }
+        asm volatile("" ::: "memory");
     }
     amax_commit(p.aamax, mxa);
-    amax_commit(p.xamax, mxx);
-    amax_commit(p.hamax, mxh);
-    amax_commit(p.yamax, mxy);
+    amax_commit(p.xamax, mxx * (1.0f / sx));  // exact: the scales are powers of two
+    amax_commit(p.hamax, mxh * (1.0f / sh));
+    amax_commit(p.yamax, mxy * (1.0f / sy));
 }
 
 template <int C, int BM, bool WINDOW, bool FIRST, int W1M, int W1N, int W2M, int W2N, int NP>
@@ -1011,11 +1053,11 @@ hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** 
             if (a.audio && a.wh16) {
                 static const char* nm = "mimi::resblock0_h16_kernel(mimi::ResArgs)";
                 if (kname) *kname = nm;
-                // persistent: one workgroup (8 waves, 154.6 KB of LDS) per CU, each wave a range of tiles
+                // persistent: one workgroup (8 waves, 114.6 KB of LDS) per CU, each wave a range of tiles
                 int dev = 0, ncu = 256;
                 (void)hipGetDevice(&dev);
                 (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-                hipLaunchKernelGGL(resblock0_h16_kernel, dim3((unsigned)ncu), dim3(512), 0, s, a);
+                hipLaunchKernelGGL(resblock0_h16_kernel, dim3((unsigned)ncu), dim3(64 * r0h::NW), 0, s, a);
                 return hipGetLastError();
             }
             if (a.audio && a.w3frag && a.w1frag) {
