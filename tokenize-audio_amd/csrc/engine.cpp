@@ -188,6 +188,7 @@ struct mimi_engine {
     bool res128_split = false;
     // PREC_F16X3: stage 0 on the fp16-plane fused kernel (MIMI_HIP_RES0_H16=0 falls back to the fp32-MFMA one)
     bool res0_h16_on = true;
+    bool res1_h16_on = true;  // MIMI_HIP_RES1_H16=0: stage 1 on the fp32-MFMA fused kernel
 
     std::unordered_map<std::string, std::vector<float>> host_w;
     std::unordered_map<std::string, std::vector<int64_t>> expected;  // name -> shape
@@ -198,6 +199,9 @@ struct mimi_engine {
     // PREC_F16X3 fused stage-0 block: conv0 / W3 / W1 fp16-plane A fragments (resblock.hip r0h) and their scales
     void* res0_h16 = nullptr;
     float res0_wsc[3] = {1.0f, 1.0f, 1.0f};
+    // ... and the stage-1 (C = 128) block: W3 / W1 16x16x32 fragments and scales
+    void* res1_h16 = nullptr;
+    float res1_wsc[2] = {1.0f, 1.0f};
     DevConv final_conv;
     std::vector<DevXfmr> xf;
     DevConv ds;
@@ -428,6 +432,7 @@ extern "C" int mimi_create(const mimi_config* cfg, int device, mimi_engine** out
     if (const char* uf = std::getenv("MIMI_HIP_UNFUSE_FROM")) e->unfuse_from = std::atoi(uf);
     if (const char* rs = std::getenv("MIMI_HIP_RES128_SPLIT")) e->res128_split = std::atoi(rs) != 0;
     if (const char* r0 = std::getenv("MIMI_HIP_RES0_H16")) e->res0_h16_on = std::atoi(r0) != 0;
+    if (const char* r1 = std::getenv("MIMI_HIP_RES1_H16")) e->res1_h16_on = std::atoi(r1) != 0;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipEventCreateWithFlags(&e->ws_free, hipEventDisableTiming));
     HIP_TRY(hipMalloc(&e->amax_dev, ((size_t)kMaxActSlots * AMAX_SLOT_WORDS + kMaxActSlots) * sizeof(unsigned)));
@@ -658,6 +663,45 @@ static std::vector<float> relayout_conv(const std::vector<float>& w, int cout, i
     return o;
 }
 
+// As append_afrags_h16 for the 16x16x32 MFMA: fragments [mt][ks][plane], lane (i, q) holding
+// W[16 mt + i][32 ks + 8 q + e] (i = lane & 15, q = lane >> 4).
+static void append_afrags16_h16(std::vector<_Float16>& out, const std::vector<float>& w, int M, int K, float sc) {
+    for (int mt = 0; mt < M / 16; ++mt)
+        for (int ks = 0; ks < K / 32; ++ks)
+            for (int pl = 0; pl < 2; ++pl)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int e = 0; e < 8; ++e) {
+                        const float t = w[(size_t)(16 * mt + (lane & 15)) * K + 32 * ks + 8 * (lane >> 4) + e] * sc;
+                        const _Float16 h0 = (_Float16)t;
+                        out.push_back(pl == 0 ? h0 : (_Float16)(t - (float)h0));
+                    }
+}
+
+// The stage-1 (C = 128) fp16 block's weight image (resblock.hip resblock128_h16_kernel): W3 [64][384] then
+// W1 [128][64] as 16x16x32 A fragments.
+static int make_res1_h16(mimi_engine* e) {
+    const mimi_config& c = e->cfg;
+    if (c.num_filters != 64 || c.residual_kernel_size != 3 || c.compress != 2 || c.num_ratios < 2) return MIMI_OK;
+    std::vector<float>*w3, *w1;
+    int rc;
+    if ((rc = get_w(e, "encoder.layers.4.block.1.conv.weight", &w3)) ||
+        (rc = get_w(e, "encoder.layers.4.block.3.conv.weight", &w1)))
+        return rc;
+    const std::vector<float> w3l = relayout_conv(*w3, 64, 128, 3);  // [64][3*128], tap-major
+    const std::vector<float>& w1l = *w1;                             // [128][64][1]
+    const float s3 = f16_weight_scale(w3l), s1 = f16_weight_scale(w1l);
+    std::vector<_Float16> img;
+    img.reserve((size_t)RES1_H16_FRAGS * 512);
+    append_afrags16_h16(img, w3l, 64, 384, s3);
+    append_afrags16_h16(img, w1l, 128, 64, s1);
+    if (img.size() != (size_t)RES1_H16_FRAGS * 512) return set_err(MIMI_ERR_WEIGHTS, "res1 fp16 image size");
+    if ((rc = dev_alloc(e, &e->res1_h16, img.size() * sizeof(_Float16)))) return rc;
+    HIP_TRY(hipMemcpy(e->res1_h16, img.data(), img.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    e->res1_wsc[0] = s3;
+    e->res1_wsc[1] = s1;
+    return MIMI_OK;
+}
+
 // The stage-0 fp16 block's weight image (resblock.hip resblock0_h16_kernel): 4 conv0 fragments
 // [mt][variant] -- variant 0: every lane (i, h) holds w_hi[32 mt + i][0..6], 0; variant 1: lanes h = 0 hold
 // w_lo, lanes h = 1 zeros (against the audio taps' hi | lo planes: w_hi a_hi + w_hi a_lo, then w_lo a_hi) --
@@ -770,7 +814,7 @@ extern "C" int mimi_finalize(mimi_engine* e) {
         idx += 1;
         C *= 2;
     }
-    if ((rc = make_res0_h16(e))) return rc;
+    if ((rc = make_res0_h16(e)) || (rc = make_res1_h16(e))) return rc;
     idx += 1;
     if ((rc = make_conv(e, e->final_conv, "encoder.layers." + std::to_string(idx) + ".conv.", C, c.hidden_size,
                         c.last_kernel_size, 1, true)))
@@ -1214,6 +1258,18 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                 ra.unscale2 = 1.0f / (ha.scale * e->res0_wsc[2]);
                 ra.aamax = aa.amax;
                 if (const char* d = std::getenv("MIMI_HIP_DBG")) ra.dbg = std::atoi(d);
+                ra.xamax = xa.amax;
+                ra.hamax = ha.amax;
+            }
+            if (si == 1 && C == 128 && h16 && e->res1_h16 && e->res1_h16_on &&
+                (unsigned long long)B * (unsigned long long)((T + 31) / 32) < (1ull << 32)) {
+                // fp16-plane stage-1 block: ELU(x) and ELU(h) split in-kernel at their own scales
+                const Act xa = new_act(), ha = new_act();
+                ra.wh16 = e->res1_h16;
+                ra.xscale = xa.scale;
+                ra.hscale = ha.scale;
+                ra.unscale1 = 1.0f / (xa.scale * e->res1_wsc[0]);
+                ra.unscale2 = 1.0f / (ha.scale * e->res1_wsc[1]);
                 ra.xamax = xa.amax;
                 ra.hamax = ha.amax;
             }

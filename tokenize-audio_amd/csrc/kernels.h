@@ -214,6 +214,8 @@ hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** 
 
 // fp16-plane fused stage-0 block: fragment buffer size in halves ([frag][64 lanes][8])
 constexpr int RES0_H16_FRAGS = 36;
+// fp16-plane fused stage-1 block (C = 128): W3 [4][12][2] + W1 [8][2][2] 16x16x32 A fragments
+constexpr int RES1_H16_FRAGS = 128;
 
 // conv0: Cin = 1, k = 7 causal conv, channels-last output [B][T][64].
 hipError_t launch_conv0(const float* x, long long L, int batch, const float* w /*[64][7]*/,

@@ -1034,6 +1034,216 @@ __global__ __launch_bounds__(512) void resblock0_h16_kernel(ResArgs p) {
     amax_commit(p.yamax, mxy * (1.0f / sy));
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Stage 1 (C = 128, H = 64) on the fp16 matrix cores (PREC_F16X3): residual block + ELU, persistent, one
+// workgroup of 8 waves per CU walking a contiguous range of 32-step blocks.  Both weight images stay resident
+// in LDS (W3 96 KB + W1 32 KB, 16x16x32 A fragments); per block:
+//   load    x[t0 .. t0+31][128] fp32, each lane 2 float4 in the GEMM2 output layout (time t = 16n + lane&15,
+//           channels 16m + 4(lane>>4) .. +3) -- they stay in registers as the identity skip; the next block's
+//           x is prefetched under this one
+//   slab    ELU(x) -> 2 fp16 planes, rows 2..33 of the [34][128] slab (rows 0, 1: causal halo, kept in the
+//           registers of the lanes that own steps 30, 31 of the previous block, zeros at t = 0, loaded at a
+//           range start)                                                                     barrier
+//   GEMM1   h^T[64][32] = W3 . windows^T: wave w computes the 16x16 tile (hch 16(w>>1), t 16(w&1)),
+//           K = 384 = 12 x 32, 36 MFMAs;  h = ELU(acc + b3) -> planes [32 t][64]                 barrier
+//   GEMM2   y^T[128][32] = W1 . h^T: wave w, tiles (ch 16(2(w>>1)+i), t 16(w&1)), 12 MFMAs
+//   out     y = ELU(x + (acc + b1)) -> planes staged over slab rows 2..33                     barrier
+//           -> 1-KB row stores (256-B rows, 4 per wave instruction)                           barrier
+// Slab rows are 288 B (72 dwords = 8 mod 64) and h rows 160 B: the 16x16x32 fragment reads (row lane&15,
+// 16-B chunk lane>>4) are conflict-free.  LDS: 128 KB weights + 19.1 KB slab + 10 KB h + biases = 157.9 KB.
+// ------------------------------------------------------------------------------------------------
+namespace r1h {
+constexpr int C = 128, H = 64, BM = 32, NW = 8;
+constexpr int SLD = 144, SROWS = BM + 2, SPL = SROWS * SLD;  // halves
+constexpr int HLD = 80, HPL = BM * HLD;
+constexpr int FR_W3 = 0, FR_W1 = 96, NFRAG = 128;  // W3 [mt 4][ks 12][pl 2], W1 [mt 8][ks 2][pl 2]
+constexpr int BIAS = H + C;                         // b3 | b1
+constexpr int LDS_BYTES = NFRAG * 1024 + 2 * SPL * 2 + 2 * HPL * 2 + BIAS * 4;
+static_assert(NFRAG == RES1_H16_FRAGS, "fragment count");
+static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+}  // namespace r1h
+
+__device__ __forceinline__ f32x4 mfma_h16(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
+    using namespace r1h;
+    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    _Float16* slab = reinterpret_cast<_Float16*>(lds + NFRAG * 1024);
+    _Float16* hb = slab + 2 * SPL;
+    float* bl = reinterpret_cast<float*>(hb + 2 * HPL);
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(p.wh16);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (int i = tid; i < NFRAG * 64; i += NW * 64) dst[i] = src[i];
+        if (tid < H) bl[tid] = p.b3[tid];
+        if (tid < C) bl[H + tid] = p.b1[tid];
+    }
+    const f16x8* wf = reinterpret_cast<const f16x8*>(lds);
+
+    const long long T = p.T;
+    const unsigned tpi = (unsigned)((T + BM - 1) / BM);  // blocks per item (host checks B x tpi < 2^32)
+    const unsigned long long NB = (unsigned long long)tpi * p.batch;
+    const unsigned g0 = (unsigned)((unsigned long long)blockIdx.x * NB / gridDim.x);
+    const unsigned g1 = (unsigned)((unsigned long long)(blockIdx.x + 1) * NB / gridDim.x);
+    const int li = lane & 15, lq = lane >> 4;
+    const int n = wave & 1, mp = wave >> 1;  // N-tile (16 steps), M-tile pair
+    const int t = 16 * n + li;                // this lane's step inside a block (E layout)
+    const float sx = p.xscale, sh = p.hscale, sy = p.yscale;
+    const float u1 = p.unscale1, u2 = p.unscale2;
+    float mxx = 0.0f, mxh = 0.0f, mxy = 0.0f;
+
+    // x of block g, step t, channels 16(2mp + i) + 4lq .. +3 (zero past T)
+    auto xload = [&](unsigned g, long long off, f32x4 (&xv)[2]) {
+        const unsigned b = g / tpi;
+        const long long row = (long long)(g - b * tpi) * BM + off;
+        const bool ok = row >= 0 && row < T;
+        const float* xr = p.x + ((long long)b * T + (ok ? row : 0)) * C + 4 * lq;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(xr + 16 * (2 * mp + i));
+            xv[i] = ok ? v : (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    // ELU(x) planes of this lane's 2 x 4 channels
+    auto xsplit = [&](const f32x4 (&xv)[2], uint2 (&hi)[2], uint2 (&lo)[2]) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float z[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+            float tt[4];
+            elu_s4(z, sx, tt, mxx);
+            split4_t(tt, hi[i], lo[i]);
+        }
+    };
+    auto slab_row_put = [&](int row, const uint2 (&hi)[2], const uint2 (&lo)[2]) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int o = row * SLD + 16 * (2 * mp + i) + 4 * lq;
+            *reinterpret_cast<uint2*>(slab + o) = hi[i];
+            *reinterpret_cast<uint2*>(slab + SPL + o) = lo[i];
+        }
+    };
+
+    uint2 hhi[2], hlo[2];  // lanes with t >= 30: the halo planes for the next block
+    f32x4 xn[2];
+    if (g0 < g1) xload(g0, t, xn);
+    __syncthreads();  // weights and biases resident
+    for (unsigned g = g0; g < g1; ++g) {
+        const unsigned b = g / tpi;
+        const long long t0 = (long long)(g - b * tpi) * BM;
+        f32x4 xc[2] = {xn[0], xn[1]};
+        if (g + 1 < g1) xload(g + 1, t, xn);  // flies under this block
+        // ---- slab: halo rows 0, 1 (lanes t = 30, 31), rows 2 + t
+        if (t >= BM - 2) {
+            if (t0 == 0) {
+                hhi[0] = hhi[1] = hlo[0] = hlo[1] = make_uint2(0u, 0u);
+            } else if (g == g0) {
+                f32x4 xh[2];
+                xload(g, t - BM, xh);  // steps t0 - 2, t0 - 1
+                xsplit(xh, hhi, hlo);
+            }
+            slab_row_put(t - (BM - 2), hhi, hlo);
+        }
+        {
+            uint2 hi[2], lo[2];
+            xsplit(xc, hi, lo);
+            slab_row_put(2 + t, hi, lo);
+            if (t >= BM - 2) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    hhi[i] = hi[i];
+                    hlo[i] = lo[i];
+                }
+            }
+        }
+        __syncthreads();  // B1: slab complete
+
+        // ---- GEMM1: tile (hch 16 mp, steps 16 n); k = 32 ks + 8 lq + e -> tap ks / 4, channel 32 (ks % 4) + 8 lq + e
+        f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 12; ++ks) {
+            const int o = (16 * n + li + (ks >> 2)) * SLD + (ks & 3) * 32 + 8 * lq;
+            const f16x8 bx0 = *reinterpret_cast<const f16x8*>(slab + o);
+            const f16x8 bx1 = *reinterpret_cast<const f16x8*>(slab + SPL + o);
+            const f16x8 aw0 = wf[(FR_W3 + (mp * 12 + ks) * 2) * 64 + lane];
+            const f16x8 aw1 = wf[(FR_W3 + (mp * 12 + ks) * 2 + 1) * 64 + lane];
+            acc1 = mfma_h16(aw1, bx0, acc1);
+            acc1 = mfma_h16(aw0, bx1, acc1);
+            acc1 = mfma_h16(aw0, bx0, acc1);
+        }
+        {  // h = ELU(acc + b3): step t, hch 16 mp + 4 lq .. +3
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 16 * mp + 4 * lq);
+            float z[4], tt[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) z[q] = __builtin_fmaf(acc1[q], u1, bb[q]);
+            elu_s4(z, sh, tt, mxh);
+            uint2 hi, lo;
+            split4_t(tt, hi, lo);
+            const int o = t * HLD + 16 * mp + 4 * lq;
+            *reinterpret_cast<uint2*>(hb + o) = hi;
+            *reinterpret_cast<uint2*>(hb + HPL + o) = lo;
+        }
+        __syncthreads();  // B2: h complete, every wave done reading the slab
+
+        // ---- GEMM2: tiles (channels 16 (2 mp + i), steps 16 n), K = 64
+        f32x4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int o = (16 * n + li) * HLD + ks * 32 + 8 * lq;
+            const f16x8 bh0 = *reinterpret_cast<const f16x8*>(hb + o);
+            const f16x8 bh1 = *reinterpret_cast<const f16x8*>(hb + HPL + o);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int m = 2 * mp + i;
+                const f16x8 aw0 = wf[(FR_W1 + (m * 2 + ks) * 2) * 64 + lane];
+                const f16x8 aw1 = wf[(FR_W1 + (m * 2 + ks) * 2 + 1) * 64 + lane];
+                acc2[i] = mfma_h16(aw1, bh0, acc2[i]);
+                acc2[i] = mfma_h16(aw0, bh1, acc2[i]);
+                acc2[i] = mfma_h16(aw0, bh0, acc2[i]);
+            }
+        }
+        // ---- y = ELU(x + (acc + b1)) -> planes, staged over slab rows 2..33
+        {
+            float tmy = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int ch = 16 * (2 * mp + i) + 4 * lq;
+                const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + H + ch);
+                float z[4], tt[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) z[q] = xc[i][q] + __builtin_fmaf(acc2[i][q], u2, bb[q]);
+                elu_s4(z, sy, tt, tmy);
+                uint2 hi, lo;
+                split4_t(tt, hi, lo);
+                const int o = (2 + t) * SLD + ch;
+                *reinterpret_cast<uint2*>(slab + o) = hi;
+                *reinterpret_cast<uint2*>(slab + SPL + o) = lo;
+            }
+            if (t0 + t < T) mxy = fmaxf(mxy, tmy);  // steps past the end are not stored, not in max|y|
+        }
+        __syncthreads();  // B3: staging complete
+        {  // 2 planes x 32 rows x 16 chunks of 16 B = 1024 chunks, 2 per thread
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int idx = tid + k * NW * 64;
+                const int pl = idx >> 9, r = (idx >> 4) & 31, c = (idx & 15) * 8;
+                const uint4 v = *reinterpret_cast<const uint4*>(slab + pl * SPL + (2 + r) * SLD + c);
+                if (t0 + r < T)
+                    *reinterpret_cast<uint4*>(reinterpret_cast<_Float16*>(p.yp) + pl * p.y_pstride +
+                                              ((long long)b * T + t0 + r) * C + c) = v;
+            }
+        }
+        __syncthreads();  // B4: staging consumed before the next slab
+    }
+    amax_commit(p.xamax, mxx * (1.0f / sx));
+    amax_commit(p.hamax, mxh * (1.0f / sh));
+    amax_commit(p.yamax, mxy * (1.0f / sy));
+}
+
 template <int C, int BM, bool WINDOW, bool FIRST, int W1M, int W1N, int W2M, int W2N, int NP>
 static hipError_t run_res(const ResArgs& a, hipStream_t s, const char** kname) {
     static char name[160];
@@ -1073,6 +1283,16 @@ hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** 
             if (a.audio) return run_res<64, 128, true, true, 4, 1, 4, 1, 64>(a, s, kname);
             return run_res<64, 128, true, false, 4, 1, 4, 1, 64>(a, s, kname);
         case 128:
+            if (a.wh16) {
+                static const char* nm = "mimi::resblock128_h16_kernel(mimi::ResArgs)";
+                if (kname) *kname = nm;
+                // persistent: one workgroup (8 waves, 157.9 KB of LDS) per CU, each a range of 32-step blocks
+                int dev = 0, ncu = 256;
+                (void)hipGetDevice(&dev);
+                (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+                hipLaunchKernelGGL(resblock128_h16_kernel, dim3((unsigned)ncu), dim3(64 * r1h::NW), 0, s, a);
+                return hipGetLastError();
+            }
             if (a.w3s && a.w1s) {
                 static const char* nm = "mimi::resblock128_split_kernel(mimi::ResArgs)";
                 if (kname) *kname = nm;
