@@ -102,18 +102,11 @@ int main(int argc, char** argv) {
         {"o_proj", 512, 1, 1, 8000, 8000, 1, 512},
     };
     Variant vars[] = {
-        {"f32 128x128 bk32 nb1", launch<128, 128, 2, 2, 32, 1, false>, 32, 0},
-        {"pl3 256x128 8w s2", launch_pl<256, 128, 4, 2, 3, 2>, 32, 3},
-        {"pl3 256x128 8w mf16 s2", launch_pl<256, 128, 4, 2, 3, 2, 0, 32, 16, 0>, 32, 3},
-        {"pl2 256x128 8w s3", launch_pl<256, 128, 4, 2, 2, 3>, 32, 2},
-        {"h2 256x128 8w s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 32, 0, true>, 32, 12},
         {"h2 256x128 8w mf16 s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
-        {"h2 256x128 8w s2", launch_pl<256, 128, 4, 2, 2, 2, 0, 32, 32, 0, true>, 32, 12},
-        {"pl3 128x128 8w s3", launch_pl<128, 128, 4, 2, 3, 3>, 32, 3},
-        {"pl3 128x128 4w+4ld s3", launch_pl<128, 128, 2, 2, 3, 3, 4>, 32, 3},
-        {"h2 128x128 8w s4", launch_pl<128, 128, 4, 2, 2, 4, 0, 32, 32, 0, true>, 32, 12},
+        {"h2 256x128 8w bk16 s4", launch_pl<256, 128, 4, 2, 2, 4, 0, 16, 32, 0, true>, 16, 12},
+        {"h2 128x256 8w bk16 s4", launch_pl<128, 256, 2, 4, 2, 4, 0, 16, 32, 0, true>, 16, 12},
         {"h2 128x128 8w mf16 s4", launch_pl<128, 128, 4, 2, 2, 4, 0, 32, 16, 0, true>, 32, 12},
-        {"h2 128x128 4w+4ld s4", launch_pl<128, 128, 2, 2, 2, 4, 4, 32, 32, 0, true>, 32, 12},
+        {"h2 128x128 8w bk16 s4", launch_pl<128, 128, 4, 2, 2, 4, 0, 16, 32, 0, true>, 16, 12},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
