@@ -150,9 +150,32 @@ hipError_t launch_gemm(int role, const GemmArgs& a, hipStream_t s, const char** 
     return e;
 }
 
+// A k = 2s conv in the KOrder chain layout (gemm_planes.h FL_PAIR): taps j, j + s read the same input lines
+static bool pair_ok(const GemmArgs& a) {
+    if (a.a_cin <= 0 || a.a_cin % 64 || a.K % a.a_cin || a.a_rs % a.a_cin) return false;
+    const int k = a.K / a.a_cin, st = a.a_rs / a.a_cin;
+    return st > 0 && k == 2 * st && a.K % 64 == 0;
+}
+
+// fp16 down convs: 256x128 tiles, tap-pair stages (2 x 67.6 KiB), A's LDS-DMA halved: -6..-16 % against the
+// 3-stage ring (profiles/r1j_gemm_bench_pair.log)
+template <int EPI, int OUTP, int TAG>
+static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
+    if (pair_ok(a)) return run_planes<256, 128, 4, 2, 2, 2, EPI, OUTP, TAG, 0, 32, 16, FL_PAIR, true>(a, s);
+    return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP, TAG, 0, 32, 16, 0, true>(a, s);
+}
+
 static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
     const int prec = g_prec;
     if (prec != PREC_BF16X6 && prec != PREC_BF16X3 && prec != PREC_F16X3) return hipErrorInvalidValue;
+    if (prec == PREC_F16X3) {
+        switch (role) {
+            case ROLE_DOWN: return run_planes_down_h16<EPI_BIAS, 0, 2>(a, s);
+            case ROLE_DOWN_ELU: return run_planes_down_h16<EPI_BIAS_ELU, 2, 3>(a, s);
+            case ROLE_DOWN_XE: return run_planes_down_h16<EPI_BIAS, 2 | 8, 11>(a, s);
+            default: break;
+        }
+    }
     switch (role) {
         case ROLE_DOWN: return run_planes_big<EPI_BIAS, 0, 0, 2>(a, s, prec);
         case ROLE_DOWN_ELU: return run_planes_big_ld<EPI_BIAS_ELU, 3, 2, 3>(a, s, prec);  // planes out: final conv

@@ -242,8 +242,10 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 template <int BK>
 struct KOrderT {
     int cin, s, cl, nhi, nlo, j, hi, c, lo;
-    __device__ __forceinline__ void init(const GemmArgs& p) {
+    bool pair;  // visit only the first tap of each chain (gemm_planes FL_PAIR: the chain is 2 taps)
+    __device__ __forceinline__ void init(const GemmArgs& p, bool pr = false) {
         j = hi = c = lo = 0;
+        pair = pr;
         const int k = p.a_cin > 0 ? p.K / p.a_cin : 0;
         const int st = p.a_cin > 0 ? p.a_rs / p.a_cin : 0;
         if (p.a_cin % 64 == 0 && k * p.a_cin == p.K && st > 0 && st * p.a_cin == p.a_rs && k % st == 0) {
@@ -263,7 +265,7 @@ struct KOrderT {
     __device__ __forceinline__ void next() {
         if (++lo < nlo) return;
         lo = 0;
-        if (++c < cl) return;
+        if (!pair && ++c < cl) return;
         c = 0;
         if (++hi < nhi) return;
         hi = 0;

@@ -61,8 +61,12 @@ __device__ __forceinline__ int chunk_swz(int row) {
 //   F16:    the planes are fp16 (2 planes, 3 products, PREC_F16X3) scaled by powers of two; the accumulator is
 //           multiplied by p.unscale before the epilogue; fp16 output planes hold out * p.out_scale.
 //   FL:     FL_READFIRST -- a K step's first fragment reads are issued before its DMA refill;
-//           FL_PRIO -- s_setprio(1) over the MFMA section.
-enum : int { FL_READFIRST = 1, FL_PRIO = 2 };
+//           FL_PRIO -- s_setprio(1) over the MFMA section;
+//           FL_PAIR -- tap pairs of a k = 2s conv (the down convs): taps j and j+s of row m read the same
+//           input line (A(m, (j+s)Cin + c) = A(m+1, j Cin + c)), so a stage holds ONE A image of BM + RPP rows
+//           and the B images of both taps, and the second K step reads the A image one row down.  A's
+//           LDS-DMA bytes halve (stage = 2 K steps; KOrder visits the chains' first taps only).
+enum : int { FL_READFIRST = 1, FL_PRIO = 2, FL_PAIR = 4 };
 
 template <int BM, int BN, int WM, int WN, int NS, int STAGES, int EPI, int OUTP, int TAG, int LW = 0, int BK = 32,
           int MF = 32, int FL = 0, bool F16 = false>
@@ -75,10 +79,15 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     constexpr int TM = BM / WM / MF;
     constexpr int TN = BN / WN / MF;
     constexpr int KSUB = MF == 32 ? BK / 16 : BK / 32;  // MFMA k-steps per K step
-    constexpr int APL = BM * BK, BPL = BN * BK;  // bf16 per plane image
-    constexpr int STG = NS * (APL + BPL);        // bf16 per stage
-    // DMA pieces of a stage: A planes [0, TPA), then B planes; piece j is issued by loading wave j % NLD
-    constexpr int TPA = NS * BM / RPP, TP = TPA + NS * BN / RPP;
+    constexpr bool PAIR = (FL & FL_PAIR) != 0;
+    constexpr int XR = PAIR ? RPP : 0;           // extra A image rows (PAIR: row BM, rounded to a piece)
+    constexpr int NB = PAIR ? 2 : 1;             // B images (K steps) per stage
+    constexpr int AR = BM + XR;                  // A image rows
+    constexpr int APL = AR * BK, BPL = BN * BK;  // bf16 per plane image
+    constexpr int STG = NS * (APL + NB * BPL);   // bf16 per stage
+    // DMA pieces of a stage: A planes [0, TPA), then B [plane][image] images; piece j is issued by loading wave
+    // j % NLD
+    constexpr int TPA = NS * AR / RPP, TP = TPA + NS * NB * BN / RPP;
     constexpr int PMAX = (TP + NLD - 1) / NLD;   // pieces per loading wave per stage (the first TP % NLD waves)
     constexpr int PMIN = TP / NLD;               // (the others)
     static_assert(BK == 32 || (BK == 16 && MF == 32), "BK");
@@ -135,15 +144,17 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         const int j = ldw + q * NLD;
         soff[q] = 0;
         if (j < TPA) {
-            const int rb = j % (BM / RPP);
+            const int rb = j % (AR / RPP);
             const int row = rb * RPP + prow;
             const int c = pch ^ chunk_swz<BK, MF>(row);
             const int m = m0 + row;
             const long long e = p.a_off + (long long)m * p.a_rs + c * 8;
-            soff[q] = (m < M) ? (int)(e * 2) : -16;  // rows past M load 0 or stale data (never stored)
+            // rows past M load 0 or stale data (never stored) -- except row M in PAIR mode, the second tap of
+            // row M - 1 (its address is the real one; the buffer range check zeroes what lies past the input)
+            soff[q] = (m < M + (PAIR ? 1 : 0)) ? (int)(e * 2) : -16;
         } else if (j < TP) {
             const int jb = j - TPA;
-            const int pl = jb / (BN / RPP), rb = jb % (BN / RPP);
+            const int pl = jb / (NB * BN / RPP), rb = jb % (BN / RPP);
             const int row = rb * RPP + prow;
             const int c = pch ^ chunk_swz<BK, MF>(row);
             int n = n0 + row;
@@ -154,7 +165,8 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     const int npieces = ldw < TP % NLD ? PMAX : PMIN;  // this wave's pieces per stage (wave-uniform)
 
     KOrderT<BK> ko;  // K steps are issued in order: the cursor follows the issues
-    ko.init(p);
+    ko.init(p, PAIR);
+    const int kimg = PAIR ? ko.s * ko.cin : 0;  // K offset of a stage's second tap
     auto issue = [&](int stage) {
         __bf16* st = lds + stage * STG;
         const int k0 = ko.offset();
@@ -164,17 +176,18 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         for (int q = 0; q < PMAX; ++q) {
             const int j = ldw + q * NLD;
             if (j < TPA) {
-                const int pl = j / (BM / RPP), rb = j % (BM / RPP);
+                const int pl = j / (AR / RPP), rb = j % (AR / RPP);
                 const __amdgpu_buffer_rsrc_t rs = pl == 0 ? arsrc[0] : (pl == 1 ? arsrc[1 % NS] : arsrc[NS - 1]);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                     rs, (__attribute__((address_space(3))) void*)(st + pl * APL + rb * RPP * BK), 16, soff[q] + kb, 0,
                     0, 0);
             } else if (j < TP) {
                 const int jb = j - TPA;
-                const int pl = jb / (BN / RPP), rb = jb % (BN / RPP);
+                const int pi = jb / (BN / RPP), rb = jb % (BN / RPP);  // pi = plane * NB + image
+                const int img = pi % NB;
                 __builtin_amdgcn_global_load_lds(
-                    (const void*)(Wp + soff[q] + k0),
-                    (__attribute__((address_space(3))) void*)(st + NS * APL + pl * BPL + rb * RPP * BK), 16, 0, 0);
+                    (const void*)(Wp + soff[q] + k0 + img * kimg),
+                    (__attribute__((address_space(3))) void*)(st + NS * APL + pi * BPL + rb * RPP * BK), 16, 0, 0);
             }
         }
     };
@@ -187,19 +200,20 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
 #pragma unroll
             for (int r = 0; r < NACC; ++r) acc[i][j][r] = 0.0f;
 
-    const int KT = K / BK;
+    const int KT = K / BK / NB;
     const int arow = wm * TM * MF + (lane & (MF - 1));
     const int brow = wn * TN * MF + (lane & (MF - 1));
     const int hsel = MF == 32 ? lane >> 5 : lane >> 4;  // k chunk of the lane within an MFMA k-step
 
-    // fragments of MFMA k-step ks of the stage at As / Bs
-    auto read_frags = [&](const __bf16* As, const __bf16* Bs, int ks, bf16x8 (&af)[NS][TM], bf16x8 (&bf)[NS][TN]) {
+    // fragments of MFMA k-step ks of the stage at As / Bs (B image `img`, A rows shifted down by img)
+    auto read_frags = [&](const __bf16* As, const __bf16* Bs, int ks, bf16x8 (&af)[NS][TM], bf16x8 (&bf)[NS][TN],
+                          int img = 0) {
         const int lc = MF == 32 ? ks * 2 + hsel : hsel;
 #pragma unroll
         for (int pl = 0; pl < NS; ++pl) {
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                const int row = arow + i * MF;
+                const int row = arow + i * MF + img;
                 const int phys = (lc ^ chunk_swz<BK, MF>(row)) * 8;
                 af[pl][i] = *reinterpret_cast<const bf16x8*>(As + pl * APL + row * BK + phys);
             }
@@ -207,7 +221,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
             for (int j = 0; j < TN; ++j) {
                 const int row = brow + j * MF;
                 const int phys = (lc ^ chunk_swz<BK, MF>(row)) * 8;
-                bf[pl][j] = *reinterpret_cast<const bf16x8*>(Bs + pl * BPL + row * BK + phys);
+                bf[pl][j] = *reinterpret_cast<const bf16x8*>(Bs + (pl * NB + img) * BPL + row * BK + phys);
             }
         }
     };
@@ -246,10 +260,12 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         if (!compute) continue;
         if (FL & FL_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int ks = 0; ks < KSUB; ++ks) {
-            if (!(FL & FL_READFIRST) || ks > 0) read_frags(As, Bs, ks, af, bf);
-            mma_split<NS, TM, TN, F16>(acc, af, bf);
-        }
+        for (int img = 0; img < NB; ++img)
+#pragma unroll
+            for (int ks = 0; ks < KSUB; ++ks) {
+                if (!(FL & FL_READFIRST) || ks > 0 || img > 0) read_frags(As, Bs, ks, af, bf, img);
+                mma_split<NS, TM, TN, F16>(acc, af, bf);
+            }
         if (FL & FL_PRIO) __builtin_amdgcn_s_setprio(0);
     }
 

@@ -77,6 +77,7 @@ struct Variant {
     LaunchFn fn;
     int bk;
     int ns;  // 0 = fp32 weights, else bf16 planes (2, 3) or fp16 planes (12)
+    bool pair = false;  // FL_PAIR: k = 2s convs only
 };
 
 static uint16_t f2bf(float f) {
@@ -103,10 +104,10 @@ int main(int argc, char** argv) {
     };
     Variant vars[] = {
         {"h2 256x128 8w mf16 s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
-        {"h2 256x128 8w bk16 s4", launch_pl<256, 128, 4, 2, 2, 4, 0, 16, 32, 0, true>, 16, 12},
-        {"h2 128x256 8w bk16 s4", launch_pl<128, 256, 2, 4, 2, 4, 0, 16, 32, 0, true>, 16, 12},
+        {"h2 256x128 8w mf16 s2 pair", launch_pl<256, 128, 4, 2, 2, 2, 0, 32, 16, FL_PAIR, true>, 64, 12, true},
+        {"h2 256x128 8w bk16 s4 pair", launch_pl<256, 128, 4, 2, 2, 4, 0, 16, 32, FL_PAIR, true>, 32, 12, true},
+        {"h2 128x128 8w mf16 s3 pair", launch_pl<128, 128, 4, 2, 2, 3, 0, 32, 16, FL_PAIR, true>, 64, 12, true},
         {"h2 128x128 8w mf16 s4", launch_pl<128, 128, 4, 2, 2, 4, 0, 32, 16, 0, true>, 32, 12},
-        {"h2 128x128 8w bk16 s4", launch_pl<128, 128, 4, 2, 2, 4, 0, 16, 32, 0, true>, 16, 12},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
@@ -193,6 +194,7 @@ int main(int argc, char** argv) {
         std::vector<float> ref(nC), out(nC);
         for (int v = 0; v < nv; ++v) {
             if (K % vars[v].bk) continue;
+            if (vars[v].pair && sh.k != 2 * sh.s) continue;
             a.C = v == 0 ? Cref : C;
             a.W = W;
             a.Wsplit = Wp;
