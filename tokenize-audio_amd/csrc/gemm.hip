@@ -87,8 +87,9 @@ static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
 //   big_ld: 256x128, 4 compute waves of 128x64 + 4 loader waves (warp-specialised DMA): down_s3
 //   small:  128x128, 8 compute waves of 32x64, 3 stages: final conv, q/k/v (M = B*250 rows)
 //   small_ld: 128x128, 4 compute waves of 64x64 + 4 loader waves, 3 stages: o_proj, fc2
-// fp16 planes (PREC_F16X3, 2 planes): 16x16x32 MFMAs; big = 256x128 x 3 stages (every big / big_ld role),
-// small = 128x128 x 4 stages (every small / small_ld role).
+// fp16 planes (PREC_F16X3, 2 planes): 16x16x32 MFMAs; big = 256x128 x 3 stages (fc1, k3 convs; the down
+// convs take run_planes_down_h16), small = 128x128 x 4 stages (q/k/v), small_ld = 128x128 x 4 stages with 4
+// compute + 4 loader waves (o_proj, fc2, final conv).
 template <int EPI, int OUTP3, int OUTP2, int TAG>
 static hipError_t run_planes_big(const GemmArgs& a, hipStream_t s, int prec) {
     if (prec == PREC_F16X3) return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP2, TAG, 0, 32, 16, 0, true>(a, s);
@@ -109,7 +110,7 @@ static hipError_t run_planes_small(const GemmArgs& a, hipStream_t s, int prec) {
 }
 template <int EPI, int TAG>
 static hipError_t run_planes_small_ld(const GemmArgs& a, hipStream_t s, int prec) {
-    if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 4, EPI, 0, TAG, 0, 32, 16, 0, true>(a, s);
+    if (prec == PREC_F16X3) return run_planes<128, 128, 2, 2, 2, 4, EPI, 0, TAG, 4, 32, 16, 0, true>(a, s);
     if (prec == PREC_BF16X6) return run_planes<128, 128, 2, 2, 3, 3, EPI, 0, TAG, 4>(a, s);
     return run_planes<128, 128, 2, 2, 2, 3, EPI, 0, TAG, 4>(a, s);
 }
@@ -157,11 +158,12 @@ static bool pair_ok(const GemmArgs& a) {
     return st > 0 && k == 2 * st && a.K % 64 == 0;
 }
 
-// fp16 down convs: 256x128 tiles, tap-pair stages (2 x 67.6 KiB), A's LDS-DMA halved: -6..-16 % against the
-// 3-stage ring (profiles/r1j_gemm_bench_pair.log)
+// fp16 down convs: 256x128 tiles, tap-pair stages (2 x 67.6 KiB), A's LDS-DMA halved, issued by 4 loader
+// waves beside the 8 compute waves: -4..-15 % against the 3-stage ring without loaders
+// (profiles/r1j_gemm_bench_pair.log, r1j_gemm_bench_ld.log)
 template <int EPI, int OUTP, int TAG>
 static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
-    if (pair_ok(a)) return run_planes<256, 128, 4, 2, 2, 2, EPI, OUTP, TAG, 0, 32, 16, FL_PAIR, true>(a, s);
+    if (pair_ok(a)) return run_planes<256, 128, 4, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR, true>(a, s);
     return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP, TAG, 0, 32, 16, 0, true>(a, s);
 }
 
@@ -179,7 +181,7 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
     switch (role) {
         case ROLE_DOWN: return run_planes_big<EPI_BIAS, 0, 0, 2>(a, s, prec);
         case ROLE_DOWN_ELU: return run_planes_big_ld<EPI_BIAS_ELU, 3, 2, 3>(a, s, prec);  // planes out: final conv
-        case ROLE_FINAL: return run_planes_small<EPI_BIAS_OUT, 4>(a, s, prec);
+        case ROLE_FINAL: return run_planes_small_ld<EPI_BIAS_OUT, 4>(a, s, prec);
         case ROLE_QKV: return run_planes_small<EPI_ROPE, 5>(a, s, prec);
         case ROLE_OPROJ: return run_planes_small_ld<EPI_SCALE_RES, 6>(a, s, prec);
         case ROLE_FC1: return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);  // planes out: fc2
