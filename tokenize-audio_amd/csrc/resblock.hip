@@ -748,7 +748,7 @@ __global__ __launch_bounds__(256) void resblock128_split_kernel(ResArgs p) {
 // layout in which it writes the next operand (8-B LDS rows, 8-B y-plane stores) and in which conv0's output
 // is already the identity skip of the block (kept in registers, never re-read).
 //
-// One wave walks a contiguous range of 32-step tiles (8 waves per CU, one workgroup per CU); per tile:
+// One wave walks a contiguous range of 32-step tiles (12 waves per CU, one workgroup per CU); per tile:
 //   conv0   x0^T[64][32] = W0 . audio-taps^T: K = 16 = 7 taps of the audio's hi plane (lanes 0-31) | 7 of its
 //           lo plane (lanes 32-63): 2 MFMAs per 32 channels give w_hi a_hi + w_hi a_lo + w_lo a_hi
 //   slab    ELU(x0) -> planes, rows 2..33 of the wave's [34][64] slab; rows 0, 1 (causal halo) are the
@@ -759,7 +759,8 @@ __global__ __launch_bounds__(256) void resblock128_split_kernel(ResArgs p) {
 //   GEMM2   y^T[64][32] = W1[64][32] . h^T                                        12 MFMAs
 //   out     y = ELU(x0 + (acc + b1)) -> 2 fp16 planes of y * yscale, staged in LDS -> 1-KB row stores
 // No barrier after the weight load: waves drift apart, so one's VALU (ELU, splits) overlaps another's MFMAs.
-// LDS: weights 36 KB + biases + 8 x 9.75 KB per-wave slab / audio window = 114.6 KB.
+// LDS: weights 36 KB + biases + 12 x 9.75 KB per-wave slab / audio window = 153.6 KB.  12 waves (3 per SIMD, 168
+// VGPRs) beat 8: 0.70 vs 0.75 ms.
 // ------------------------------------------------------------------------------------------------
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -771,7 +772,7 @@ constexpr int SLD = 72, SROWS = 34, SPL = SROWS * SLD;  // slab [2 planes][34][7
                                                         // column reads); h [2][32][32] reuses rows 2..33
 constexpr int AUD = 48;                                 // audio window floats
 constexpr int WAVE_BYTES = 2 * SPL * 2 + AUD * 4;
-constexpr int NW = 8;
+constexpr int NW = 12;
 constexpr int FR_W0 = 0, FR_W3 = 4, FR_W1 = 28, NFRAG = 36;  // 1-KB A fragments [64 lanes][8 halves]
 constexpr int BIAS = 64 + 32 + 64;                           // b0 | b3 | b1
 constexpr int LDS_BYTES = NFRAG * 1024 + BIAS * 4 + NW * WAVE_BYTES;
@@ -823,7 +824,7 @@ __device__ __forceinline__ void elu_s4(const float (&z)[4], float s, float (&t)[
     }
 }
 
-__global__ __launch_bounds__(512) void resblock0_h16_kernel(ResArgs p) {
+__global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
     using namespace r0h;
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1263,7 +1264,7 @@ hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** 
             if (a.audio && a.wh16) {
                 static const char* nm = "mimi::resblock0_h16_kernel(mimi::ResArgs)";
                 if (kname) *kname = nm;
-                // persistent: one workgroup (8 waves, 114.6 KB of LDS) per CU, each wave a range of tiles
+                // persistent: one workgroup (12 waves, 153.6 KB of LDS) per CU, each wave a range of tiles
                 int dev = 0, ncu = 256;
                 (void)hipGetDevice(&dev);
                 (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
