@@ -1069,6 +1069,14 @@ __device__ __forceinline__ f32x4 mfma_h16(f16x8 a, f16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
+// Workgroup barrier for LDS hand-offs only: this wave's LDS operations complete, then s_barrier.  Unlike
+// __syncthreads() it does not drain vmcnt, so prefetched global loads and y stores stay in flight across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
     using namespace r1h;
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
@@ -1161,7 +1169,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
                 }
             }
         }
-        __syncthreads();  // B1: slab complete
+        lds_barrier();  // B1: slab complete
 
         // ---- GEMM1: tile (hch 16 mp, steps 16 n); k = 32 ks + 8 lq + e -> tap ks / 4, channel 32 (ks % 4) + 8 lq + e
         f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -1188,7 +1196,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
             *reinterpret_cast<uint2*>(hb + o) = hi;
             *reinterpret_cast<uint2*>(hb + HPL + o) = lo;
         }
-        __syncthreads();  // B2: h complete, every wave done reading the slab
+        lds_barrier();  // B2: h complete, every wave done reading the slab
 
         // ---- GEMM2: tiles (channels 16 (2 mp + i), steps 16 n), K = 64
         f32x4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -1226,7 +1234,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
             }
             if (t0 + t < T) mxy = fmaxf(mxy, tmy);  // steps past the end are not stored, not in max|y|
         }
-        __syncthreads();  // B3: staging complete
+        lds_barrier();  // B3: staging complete
         {  // 2 planes x 32 rows x 16 chunks of 16 B = 1024 chunks, 2 per thread
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
@@ -1238,7 +1246,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
                                               ((long long)b * T + t0 + r) * C + c) = v;
             }
         }
-        __syncthreads();  // B4: staging consumed before the next slab
+        lds_barrier();  // B4: staging consumed before the next slab
     }
     amax_commit(p.xamax, mxx * (1.0f / sx));
     amax_commit(p.hamax, mxh * (1.0f / sh));
