@@ -1362,7 +1362,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1a.scale,
                                     t1a.amax),
                    "ln1");
-        rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512>");
+        rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
         GemmArgs aq = linear_args(w.t1, T, Hd, x.wqkv, 3 * H * Dh, w.qkv);
         aq.Wsplit = x.wqkv_s;
         aq.batch = B;
@@ -1392,7 +1392,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1b.scale,
                                     t1b.amax),
                    "ln2");
-        rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512>");
+        rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
         GemmArgs a1 = linear_args(w.t1, rows, Hd, x.w1, c.intermediate_size, w.ff);
         a1.Wsplit = x.w1_s;
         Act ffa;

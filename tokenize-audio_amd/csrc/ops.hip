@@ -69,8 +69,9 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-template <int C>
-__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ g,
+// RPW rows per wave, all loads in flight before the first reduction; 8 waves per workgroup.
+template <int C, int RPW>
+__global__ __launch_bounds__(512) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                         const float* __restrict__ bta, float* __restrict__ y,
                                                         long long rows, float eps, __bf16* __restrict__ yp,
                                                         long long pstride, int yns, float yscale,
@@ -78,15 +79,24 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     constexpr int PER = C / 64;  // floats per lane
     static_assert(PER % 4 == 0, "C multiple of 256");
     const int lane = threadIdx.x & 63;
-    const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= rows) return;
-    const float* xr = x + row * C;
-    float v[PER];
+    const long long row0 = ((long long)blockIdx.x * 8 + (threadIdx.x >> 6)) * RPW;
+    float vr[RPW][PER];
 #pragma unroll
-    for (int q = 0; q < PER / 4; ++q) {
-        f32x4 t = *reinterpret_cast<const f32x4*>(xr + q * 256 + lane * 4);
-        v[q * 4 + 0] = t.x; v[q * 4 + 1] = t.y; v[q * 4 + 2] = t.z; v[q * 4 + 3] = t.w;
+    for (int rr = 0; rr < RPW; ++rr) {
+        const long long row = row0 + rr < rows ? row0 + rr : rows - 1;
+        const float* xr = x + row * C;
+#pragma unroll
+        for (int q = 0; q < PER / 4; ++q) {
+            f32x4 t = *reinterpret_cast<const f32x4*>(xr + q * 256 + lane * 4);
+            vr[rr][q * 4 + 0] = t.x; vr[rr][q * 4 + 1] = t.y; vr[rr][q * 4 + 2] = t.z; vr[rr][q * 4 + 3] = t.w;
+        }
     }
+    float mx = 0.0f;
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+    const long long row = row0 + rr;
+    if (row >= rows) break;
+    float (&v)[PER] = vr[rr];
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < PER; ++i) s += v[i];
@@ -102,7 +112,6 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     const float sc = rstd;
     const float bi = -rstd * mean;
     float* yr = y + row * C;
-    float mx = 0.0f;
 #pragma unroll
     for (int q = 0; q < PER / 4; ++q) {
         const int c0 = q * 256 + lane * 4;
@@ -140,6 +149,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
             }
         }
     }
+    }
     amax_commit(yamax, mx);
 }
 
@@ -147,7 +157,9 @@ hipError_t launch_layernorm(const float* x, const float* g, const float* b, floa
                             float eps, hipStream_t s, void* yp, long long y_pstride, int yns, float yscale,
                             unsigned* yamax) {
     if (C != 512 || (yns != 0 && !yp) || (yscale > 0.0f && yns != 2)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((layernorm_kernel<512>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, g, b, y,
+    constexpr int RPW = 2;  // 16 rows per workgroup
+    hipLaunchKernelGGL((layernorm_kernel<512, RPW>), dim3((unsigned)((rows + 8 * RPW - 1) / (8 * RPW))), dim3(512), 0, s,
+                       x, g, b, y,
                        rows, eps, reinterpret_cast<__bf16*>(yp), y_pstride, yns, yscale, yamax);
     return hipGetLastError();
 }
