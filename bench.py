@@ -43,7 +43,7 @@ def mfma_peak_for(kernel: str):
         kind = "fp16" if targs[-1] == "true" else "bf16"
         return BF16_PEAK_TFLOPS / products, (f"{kind} MFMA dense peak (= bf16 rate) / {products} products "
                                              f"(split-{kind}, {ns} planes)")
-    if "_h16_kernel" in kernel:  # fused fp16-plane residual blocks (resblock.hip): 3 fp16 products per MAC
+    if "_h16_kernel" in kernel:  # fp16-plane fused blocks / attention: 3 fp16 products per MAC
         return BF16_PEAK_TFLOPS / 3, "fp16 MFMA dense peak (= bf16 rate) / 3 products (split-fp16, 2 planes)"
     return FP32_PEAK_TFLOPS, "fp32 MFMA peak"
 

@@ -1379,7 +1379,9 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh), s,
                                     w.att, nact, ns, atta.scale, atta.amax),
                    "attention");
-        rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4, "mimi::attention_kernel");
+        rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4,
+                 T <= 256 ? (atta.scale > 0.0f && ns == 2 ? "mimi::attention_t256_h16_kernel" : "mimi::attention_t256_kernel")
+                          : "mimi::attention_kernel");
         GemmArgs ao = linear_args(w.att, rows, H * Dh, x.wo, Hd, w.t0);
         ao.Wsplit = x.wo_s;
         ao.R = w.t0;

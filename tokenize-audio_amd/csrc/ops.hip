@@ -410,10 +410,246 @@ __global__ __launch_bounds__(512) void attention_t256_kernel(const float* __rest
     amax_commit(oamax, mx);
 }
 
+// ------------------------------------------------------------------------------------------------
+// T <= 256 attention on the fp16 matrix cores (PREC_F16X3 engines, fp16-plane output).  Same schedule as
+// attention_t256_kernel (one workgroup per (batch, head), 8 waves with balanced causal 32-query tiles, fp32
+// online softmax), but both products run as 3 fp16 plane products on v_mfma_f32_32x32x16_f16:
+//   S^T = K . Q^T   K planes [256 keys][64] in LDS (rows of 144 B), Q planes in registers
+//   O^T += V^T . P^T  V^T planes [64][256 keys] in LDS (rows of 528 B), P = softmax numerators in [0, 1]
+//                    split at 2^14 straight from the S^T accumulator registers
+// The k index of the P . V product runs over a chunk's keys in the order the S^T accumulator holds them
+// (lane half h, element e <-> key (e & 3) + 8 (e >> 2) + 4 h of each 16), so V^T is stored with that
+// permutation and P needs no shuffle.  Scales are chosen in-kernel (powers of two): K and V from the head's
+// max |.| (workgroup reduction), Q from the wave's max; max |.| s lands in [2^13, 2^14).
+// ------------------------------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ float pow2_scale(float mx) {
+    return mx > 0.0f && mx < INFINITY ? ldexpf(1.0f, 13 - ilogbf(mx)) : 1.0f;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+// hi / lo fp16 planes of 8 scaled values
+__device__ __forceinline__ void split8_h(const float (&v)[8], float sc, f16x8& hi, f16x8& lo) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float t = v[e] * sc;
+        hi[e] = (_Float16)t;
+        lo[e] = (_Float16)(t - (float)hi[e]);
+    }
+}
+
+__global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __restrict__ qkv, int T, int H,
+                                                                 int window, float scale, void* __restrict__ outp,
+                                                                 long long pstride, float oscale,
+                                                                 unsigned* __restrict__ oamax) {
+    constexpr int D = 64, TM = 256, LDO = D + 1;
+    constexpr int KLD = 72, KPL = TM * KLD;  // K planes: [256][72 halves]
+    constexpr int VLD = 264, VPL = D * VLD;  // V^T planes: [64][264 halves]
+    __shared__ __attribute__((aligned(16))) _Float16 lds[2 * KPL + 2 * VPL];
+    __shared__ float red[2][8];
+    _Float16* Ks = lds;
+    _Float16* Vt = lds + 2 * KPL;
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hf = lane >> 5, col = lane & 31;
+    const long long ld = 3LL * H * D;
+    const float* base = qkv + (long long)b * T * ld;
+    // K / V rows 0 .. 255 (zeros past T) -> registers, head max |K|, |V|
+    constexpr int PER = TM * (D / 4) / 512;  // 8
+    f32x4 kv[PER], vv[PER];
+    float mk = 0.0f, mv = 0.0f;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int idx = tid + q * 512;
+        const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
+        const int rr = r < T ? r : T - 1;
+        const f32x4 k4 = *reinterpret_cast<const f32x4*>(base + (long long)rr * ld + H * D + h * D + c);
+        const f32x4 v4 = *reinterpret_cast<const f32x4*>(base + (long long)rr * ld + 2 * H * D + h * D + c);
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        kv[q] = r < T ? k4 : z;
+        vv[q] = r < T ? v4 : z;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            mk = fmaxf(mk, fabsf(kv[q][e]));
+            mv = fmaxf(mv, fabsf(vv[q][e]));
+        }
+    }
+    mk = wave_max(mk);
+    mv = wave_max(mv);
+    if (lane == 0) {
+        red[0][wave] = mk;
+        red[1][wave] = mv;
+    }
+    // this wave's 32 queries: lane (query col, half hf) holds dims 16 ks + 8 hf .. +7 (Q pre-scaled by 1/8)
+    const int qt = wave < 4 ? wave : 11 - wave;
+    const int qw = qt * 32;
+    const int qi = qw + col;
+    float qv[4][8];
+    float mq = 0.0f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f}, c = {0.f, 0.f, 0.f, 0.f};
+        if (qi < T) {
+            const float* qr = base + (long long)qi * ld + h * D + 16 * ks + 8 * hf;
+            a = *reinterpret_cast<const f32x4*>(qr);
+            c = *reinterpret_cast<const f32x4*>(qr + 4);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            qv[ks][e] = a[e] * scale;
+            qv[ks][4 + e] = c[e] * scale;
+            mq = fmaxf(mq, fmaxf(fabsf(qv[ks][e]), fabsf(qv[ks][4 + e])));
+        }
+    }
+    const float sq = pow2_scale(wave_max(mq));
+    f16x8 qf[4][2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) split8_h(qv[ks], sq, qf[ks][0], qf[ks][1]);
+    __syncthreads();
+    mk = red[0][0];
+    mv = red[1][0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) {
+        mk = fmaxf(mk, red[0][w]);
+        mv = fmaxf(mv, red[1][w]);
+    }
+    const float sk = pow2_scale(mk), sv = pow2_scale(mv);
+    // K planes (rows as loaded) and V^T planes (keys permuted inside each 16: see above)
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int idx = tid + q * 512;
+        const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
+        typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+        f16x4 h0, h1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float t = kv[q][e] * sk;
+            h0[e] = (_Float16)t;
+            h1[e] = (_Float16)(t - (float)h0[e]);
+        }
+        *reinterpret_cast<f16x4*>(Ks + r * KLD + c) = h0;
+        *reinterpret_cast<f16x4*>(Ks + KPL + r * KLD + c) = h1;
+        const int k = r & 15;
+        const int pr = (r & ~15) + 8 * ((k >> 2) & 1) + (k & 3) + 4 * ((k >> 3) & 1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float t = vv[q][e] * sv;
+            const _Float16 a0 = (_Float16)t;
+            Vt[(c + e) * VLD + pr] = a0;
+            Vt[VPL + (c + e) * VLD + pr] = (_Float16)(t - (float)a0);
+        }
+    }
+    const float us = 1.0f / (sk * sq);                // S^T accumulator -> scores (exact)
+    const float uo = 1.0f / (16384.0f * sv);          // O^T accumulator -> P V (exact)
+    f32x16 o[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    __syncthreads();
+    const int kend = min(T - 1, qw + 31);
+    if (qw < T) {
+        const int kstart = max(0, qw - window + 1) & ~31;
+        for (int c0 = kstart; c0 <= kend; c0 += 32) {
+            // S^T[key][query] = K . Q^T
+            f32x16 st;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) st[r] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                const int ko = (c0 + col) * KLD + 16 * ks + 8 * hf;
+                const f16x8 k0 = *reinterpret_cast<const f16x8*>(Ks + ko);
+                const f16x8 k1 = *reinterpret_cast<const f16x8*>(Ks + KPL + ko);
+                st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, qf[ks][0], st, 0, 0, 0);
+                st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, qf[ks][1], st, 0, 0, 0);
+                st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, qf[ks][0], st, 0, 0, 0);
+            }
+            // mask + online softmax for this lane's query (fp32, as attn_chunk)
+            float cmax = -INFINITY;
+            const bool full = c0 + 31 <= qw && c0 > qw + 31 - window && c0 + 31 <= kend;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float v = st[r] * us;
+                if (!full) {
+                    const int key = c0 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+                    const bool ok = key <= qi && key > qi - window && key <= kend;
+                    v = ok ? v : -INFINITY;
+                }
+                st[r] = v;
+                cmax = fmaxf(cmax, v);
+            }
+            cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
+            const float mnew = fmaxf(m, cmax);
+            const float corr = (m == -INFINITY) ? 0.f : __expf(m - mnew);
+            float psum = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float pv = (st[r] == -INFINITY) ? 0.f : __expf(st[r] - mnew);
+                st[r] = pv;
+                psum += pv;
+            }
+            psum += __shfl_xor(psum, 32);
+            l = l * corr + psum;
+            m = mnew;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[t][r] *= corr;
+            // O^T[d][query] += V^T . P^T: k-step ks = keys 16 ks .. +15 of the chunk, lane half hf element e =
+            // st[8 ks + e] (key (e & 3) + 8 (e >> 2) + 4 hf)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                float pe[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) pe[e] = st[8 * ks + e];
+                f16x8 p0, p1;
+                split8_h(pe, 16384.0f, p0, p1);
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const int vo = (32 * t + col) * VLD + c0 + 16 * ks + 8 * hf;
+                    const f16x8 v0 = *reinterpret_cast<const f16x8*>(Vt + vo);
+                    const f16x8 v1 = *reinterpret_cast<const f16x8*>(Vt + VPL + vo);
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1, p0, o[t], 0, 0, 0);
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0, p1, o[t], 0, 0, 0);
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0, p0, o[t], 0, 0, 0);
+                }
+            }
+        }
+    }
+    __syncthreads();  // K / V dead: the output staging reuses the LDS
+    float* ow = reinterpret_cast<float*>(lds) + wave * 32 * LDO;
+    const float inv = (l > 0.f) ? uo / l : 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            ow[col * LDO + d] = o[t][r] * inv;
+        }
+    float mx = 0.0f;
+    for (int qq = 0; qq < 32; ++qq) {
+        const int q = qw + qq;
+        if (q < T)
+            store_act(nullptr, outp, pstride, 2, ((long long)b * T + q) * (H * D) + h * D + lane, ow[qq * LDO + lane],
+                      oscale, &mx);
+    }
+    amax_commit(oamax, mx);
+}
+
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window, float scale,
                             hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
                             unsigned* oamax) {
     if (D != 64 || (outns != 0 && !outp) || (oscale > 0.0f && outns != 2)) return hipErrorInvalidValue;
+    if (T <= 256 && oscale > 0.0f && outns == 2) {  // fp16-plane output: the PREC_F16X3 engine
+        hipLaunchKernelGGL(attention_t256_h16_kernel, dim3(H, batch), dim3(512), 0, s, qkv, T, H, window, scale, outp,
+                           out_pstride, oscale, oamax);
+        return hipGetLastError();
+    }
     if (T <= 256) {
         hipLaunchKernelGGL(attention_t256_kernel, dim3(H, batch), dim3(512), 0, s, qkv, out, T, H, window, scale,
                            outp, out_pstride, outns, oscale, oamax);
