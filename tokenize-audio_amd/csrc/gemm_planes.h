@@ -105,8 +105,12 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     typedef typename std::conditional<MF == 32, f32x16, f32x4>::type accT;
     constexpr int NACC = MF == 32 ? 16 : 4;
 
-    // epilogue staging (wave-private fp32 tiles) reuses the ring
-    constexpr int CW = TN * MF, LDE = CW + 4, RW = TM * MF;
+    // epilogue staging (wave-private fp32 tiles) reuses the ring; a wave's CW columns go through it in JH
+    // passes of CWC when the whole tile would not fit (256x256 tiles)
+    constexpr int CW = TN * MF, RW = TM * MF;
+    constexpr int JH = NW * RW * (CW + 4) * 4 <= 160 * 1024 ? 1 : 2;
+    constexpr int TNC = TN / JH, CWC = TNC * MF, LDE = CWC + 4;
+    static_assert(TNC * JH == TN, "epilogue passes");  // (RoPE pairs are read from acc, not from the staging)
     constexpr int LDS_EL = STAGES * STG > NW * RW * LDE * 2 ? STAGES * STG : NW * RW * LDE * 2;
     static_assert(LDS_EL * 2 <= 160 * 1024, "LDS");
     __shared__ __attribute__((aligned(16))) __bf16 lds[LDS_EL];
@@ -281,10 +285,13 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     const int rbase = m0 + wm * RW;
     const int cbase = n0 + wn * CW + (lane & (MF - 1));
     const float us = F16 ? p.unscale : 1.0f;  // 1 / (activation scale x weight scale): exact power of two
+    float omx = 0.0f;  // max|planes value| (fp16 planes: the engine's range check)
+#pragma unroll
+    for (int jh = 0; jh < JH; ++jh) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
+        for (int j = jh * TNC; j < (jh + 1) * TNC; ++j) {
             const int col = cbase + j * MF;
             float bias = 0.0f, scale = 0.0f;
             if (col < N) {
@@ -324,22 +331,21 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                         }
                     }
                 }
-                stg[lrow * LDE + j * MF + (lane & (MF - 1))] = v;
+                stg[lrow * LDE + (j - jh * TNC) * MF + (lane & (MF - 1))] = v;
             }
         }
     }
     float* __restrict__ Cb = p.C ? p.C + (long long)b * p.c_bstride : nullptr;
     static_assert(!F16 || ONS == 0 || ONS == 2, "fp16 output planes: 2");
     __bf16* __restrict__ Cpb = ONS ? reinterpret_cast<__bf16*>(p.Cp) + (long long)b * p.c_bstride : nullptr;
-    float omx = 0.0f;  // max|planes value| (fp16 planes: the engine's range check)
-    constexpr int LPR = CW / 8;  // lanes per row
+    constexpr int LPR = CWC / 8;  // lanes per row
     constexpr int RPS = 64 / LPR;  // rows per pass
 #pragma unroll
     for (int ps = 0; ps < RW / RPS; ++ps) {
         const int lr = ps * RPS + lane / LPR, lc = (lane % LPR) * 8;
         f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc);
         f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc + 4);
-        const int row = m0 + wm * RW + lr, col = n0 + wn * CW + lc;
+        const int row = m0 + wm * RW + lr, col = n0 + wn * CW + jh * CWC + lc;
         if (row >= M || col >= N) continue;  // N % 8 == 0: a lane's 8 columns are all in or all out
         const long long off = (long long)row * p.ldc + col;
         if (EPI == EPI_BIAS_RES_ELU || EPI == EPI_SCALE_RES) {
@@ -365,6 +371,8 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
             *reinterpret_cast<f32x4*>(Cb + off) = v0;
             *reinterpret_cast<f32x4*>(Cb + off + 4) = v1;
         }
+    }
+    asm volatile("" ::: "memory");  // this pass's staging reads precede the next pass's writes (same wave)
     }
     if (F16 && ONS) amax_commit(p.out_amax, omx);
 #endif

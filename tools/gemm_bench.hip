@@ -104,10 +104,10 @@ int main(int argc, char** argv) {
     };
     Variant vars[] = {
         {"h2 256x128 8w mf16 s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
-        {"h2 256x128 8w mf16 s2 pair", launch_pl<256, 128, 4, 2, 2, 2, 0, 32, 16, FL_PAIR, true>, 64, 12, true},
-        {"h2 256x128 8w bk16 s4 pair", launch_pl<256, 128, 4, 2, 2, 4, 0, 16, 32, FL_PAIR, true>, 32, 12, true},
-        {"h2 128x128 8w mf16 s3 pair", launch_pl<128, 128, 4, 2, 2, 3, 0, 32, 16, FL_PAIR, true>, 64, 12, true},
-        {"h2 128x128 8w mf16 s4", launch_pl<128, 128, 4, 2, 2, 4, 0, 32, 16, 0, true>, 32, 12},
+        {"h2 256x128 8w+4ld s2 pair", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR, true>, 64, 12, true},
+        {"h2 128x128 4w+4ld mf16 s4", launch_pl<128, 128, 2, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
+        {"h2 256x256 8w mf16 s2", launch_pl<256, 256, 4, 2, 2, 2, 0, 32, 16, 0, true>, 32, 12},
+        {"h2 256x256 8w bk16 s2 pair", launch_pl<256, 256, 4, 2, 2, 2, 0, 16, 32, FL_PAIR, true>, 32, 12, true},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
