@@ -873,11 +873,15 @@ __global__ __launch_bounds__(512) void rvq_level_kernel(RvqArgs p, int L) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
     const f32x4* bp = reinterpret_cast<const f32x4*>(cbf + (long long)(code0 / 32) * nu * 256) + lane;
-    f32x4 bnext = bp[0];
-#pragma unroll 2
+    // codebook fragments 4 k-quads ahead (an L2 hit takes longer than one quad's 8 MFMAs)
+    constexpr int PF = 4;
+    f32x4 bq[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) bq[q] = bp[q * 64];
+#pragma unroll PF
     for (int u = 0; u < nu; ++u) {
-        const f32x4 bv = bnext;
-        if (u + 1 < nu) bnext = bp[(u + 1) * 64];  // in flight under this step's 16 MFMAs
+        const f32x4 bv = bq[u % PF];
+        if (u + PF < nu) bq[u % PF] = bp[(u + PF) * 64];
         f32x4 av[RT];
 #pragma unroll
         for (int i = 0; i < RT; ++i) av[i] = *reinterpret_cast<const f32x4*>(&img[h][i * 32 + (lane & 31)][u * 4]);
