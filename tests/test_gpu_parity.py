@@ -294,3 +294,45 @@ def test_f16_scales_follow_the_signal(state_dict, gain):
         assert reruns >= 1
     else:
         assert (c16 == c6).mean() > 0.99
+
+
+def test_segmenter_on_engine(engine):
+    """YODAS2 segmenter (mimi_hip.segmenter) driving the HIP encoder on the golden 'mixed' entry: the reference's
+    exact call sequence (tests/golden/segmenter.json), codes of the right shapes, and the throughput mode
+    (length-bucketed batches) agreeing with parity mode on every frame but each chunk's last."""
+    import json
+    import os
+
+    from mimi_hip.encoder import MimiEncoder
+    from mimi_hip.segmenter import process_audio_entry
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "segmenter.json")) as f:
+        case = next(c for c in json.load(f)["cases"] if c["name"] == "mixed")
+    enc = MimiEncoder(device="cuda:0", model=engine)
+    calls = []
+
+    class Logged:
+        def encode_audio_chunk(self, a, sample_rate=24000):
+            calls.append(["chunk", [len(a)]])
+            return enc.encode_audio_chunk(a, sample_rate)
+
+        def encode_audio_batch(self, arrs, sample_rate=24000):
+            calls.append(["batch", [len(a) for a in arrs]])
+            return enc.encode_audio_batch(arrs, sample_rate)
+
+    wave = np.random.default_rng(case["seed"]).normal(0.0, 0.1, case["n"]).astype(np.float32)
+    kw = dict(batch_size=case["batch_size"], max_chunk_duration=case["max_chunk_duration"], as_lists=False)
+    par = process_audio_entry({"audio_id": case["audio_id"], "text": case["text"]}, wave, Logged(), **kw)["codes"]
+    assert calls == case["calls"]
+    buck = process_audio_entry({"audio_id": case["audio_id"], "text": case["text"]}, wave, enc, bucketed=True,
+                               **kw)["codes"]
+    assert list(par) == list(buck) == list(case["codes"])
+    same = total = 0
+    for cid, c in par.items():
+        # K = 32 (the wrapper's default num_quantizers); T as the reference's slicing gives it
+        assert c.dtype == np.uint16 and c.shape == (32, np.asarray(case["codes"][cid]).shape[1])
+        assert int(c.max()) < 2048
+        if c.shape[1] > 1:
+            same += int((c[:, :-1] == buck[cid][:, :-1]).sum())
+            total += c[:, :-1].size
+    assert total > 0 and same / total > 0.99, same / total
