@@ -128,6 +128,21 @@ int64_t mimi_f16_reruns(const mimi_engine* e);
 int64_t mimi_encoded_length(int64_t length);
 int64_t mimi_encoded_length_cfg(const mimi_config* cfg, int64_t length);
 
+/*
+ * Host-ingest resampler (replaces the resampling inside librosa.load(path, sr=24000):
+ * librispeech-mimi/utils.py:84-87, emilia-mimi/process_shard.py:479-482, yodas2-mimi/process_shard.py:389),
+ * bit-exact with librosa's res_type='polyphase' = scipy.signal.resample_poly on float32 input.  nclips clips
+ * packed in dev_in at dev_in_off[i] (dev_in_len[i] samples) -> dev_out at dev_out_off[i] (dev_out_len[i]
+ * samples, max_out = their maximum), all int64 arrays on the device.  dev_filter: the up-scaled Kaiser(5.0)
+ * low-pass with its zero pre-padding (filter_len taps, <= MIMI_RESAMPLE_MAX_TAPS); pre_remove: leading
+ * outputs of the full upfirdn skipped (resample_poly's n_pre_remove).  No engine handle needed.
+ */
+#define MIMI_RESAMPLE_MAX_TAPS 8192
+int mimi_resample_poly(const float* dev_in, const int64_t* dev_in_off, const int64_t* dev_in_len, int32_t nclips,
+                       float* dev_out, const int64_t* dev_out_off, const int64_t* dev_out_len, int64_t max_out,
+                       const float* dev_filter, int32_t filter_len, int32_t up, int32_t down, int64_t pre_remove,
+                       void* stream);
+
 /* Device bytes the workspace needs for (batch, length); the engine grows it on demand. */
 int64_t mimi_workspace_bytes(const mimi_engine* e, int32_t batch, int64_t length);
 

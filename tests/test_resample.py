@@ -1,0 +1,132 @@
+"""Host-ingest resampler: the HIP kernel (mimi_hip.ingest.resample -> mimi_resample_poly) bit-exact with
+scipy.signal.resample_poly (librosa's res_type='polyphase'), pinned by tests/golden/resample.npz; the oracle
+restatement (oracle/resample_ref.py) checked against scipy and the fixtures; WAV loading semantics."""
+import math
+import os
+import wave
+
+import numpy as np
+import pytest
+import torch
+
+from mimi_hip import ingest
+from oracle.resample_ref import design_filter, librosa_polyphase_ref, resample_poly_ref
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+RATES = [16000, 8000, 22050, 44100, 48000]
+LENGTHS = [1, 2, 3, 37, 1001, 16001]
+
+
+def _clip(rate, n):  # as tests/golden/make_resample_golden.py
+    return np.random.default_rng(rate * 100003 + n).normal(0.0, 0.3, n).astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def gold():
+    with np.load(os.path.join(GOLDEN, "resample.npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def bits_equal(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("rate", RATES)
+def test_oracle_matches_golden(gold, rate):
+    for n in LENGTHS:
+        assert bits_equal(librosa_polyphase_ref(_clip(rate, n), rate, 24000), gold[f"r{rate}_n{n}"]), (rate, n)
+
+
+def test_oracle_matches_scipy_live():
+    from scipy.signal import resample_poly
+    rng = np.random.default_rng(1)
+    for up, down in [(3, 2), (1, 2), (160, 147), (3, 1), (2, 3)]:
+        for n in [5, 999, 4097]:
+            x = rng.normal(0, 1, n).astype(np.float32)
+            assert bits_equal(resample_poly_ref(x, up, down), resample_poly(x, up, down)), (up, down, n)
+
+
+def test_plan_matches_scipy_design():
+    for r in RATES:
+        up, down, hp, pre = ingest.resample_plan(r, 24000)
+        g = math.gcd(r, 24000)
+        assert (up, down) == (24000 // g, r // g)
+        h, n_pre_pad, half_len = design_filter(up, down)
+        assert bits_equal(hp, np.concatenate([np.zeros(n_pre_pad, np.float32), h]))
+        assert pre == (half_len + n_pre_pad) // down
+    with pytest.raises(ValueError):
+        ingest.resample_plan(16000.5, 24000)
+
+
+def test_resample_refuses_cpu_device():
+    with pytest.raises(ValueError, match="HIP device only"):
+        ingest.resample([np.zeros(10, np.float32)], 16000, 24000, device="cpu")
+
+
+def _write_wav(path, data, sr, sampwidth):
+    with wave.open(path, "wb") as w:
+        w.setnchannels(1 if data.ndim == 1 else data.shape[1])
+        w.setsampwidth(sampwidth)
+        w.setframerate(sr)
+        w.writeframes(data.tobytes())
+
+
+def test_load_wav_formats(tmp_path):
+    rng = np.random.default_rng(3)
+    pcm16 = rng.integers(-32768, 32767, (500, 2), dtype=np.int16)
+    p = str(tmp_path / "s16.wav")
+    _write_wav(p, pcm16, 16000, 2)
+    y, sr = ingest.load_wav(p)
+    assert sr == 16000 and y.dtype == np.float32 and y.shape == (500,)
+    f = pcm16.astype(np.float32) / 32768.0
+    assert bits_equal(y, (f[:, 0] + f[:, 1]) / np.float32(2))       # librosa.to_mono: channel mean
+    u8 = rng.integers(0, 255, 300, dtype=np.uint8)
+    p = str(tmp_path / "u8.wav")
+    _write_wav(p, u8, 8000, 1)
+    y, sr = ingest.load_wav(p)
+    assert sr == 8000 and bits_equal(y, (u8.astype(np.float32) - 128) / 128)
+    from scipy.io import wavfile
+    fl = rng.normal(0, 0.2, 700).astype(np.float32)
+    p = str(tmp_path / "f32.wav")
+    wavfile.write(p, 24000, fl)
+    y, sr = ingest.load_wav(p)
+    assert sr == 24000 and bits_equal(y, fl)
+
+
+@pytest.mark.gpu
+def test_resample_kernel_bit_exact(gold):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    for rate in RATES:
+        clips = [_clip(rate, n) for n in LENGTHS]
+        outs = ingest.resample(clips, rate, 24000, device="cuda:0")   # ragged batch: one launch
+        for n, o in zip(LENGTHS, outs):
+            assert o.is_cuda and o.dtype == torch.float32
+            assert bits_equal(o.cpu().numpy(), gold[f"r{rate}_n{n}"]), (rate, n)
+
+
+@pytest.mark.gpu
+def test_resample_kernel_full_size_vs_scipy():
+    """A 60 s LibriSpeech-rate clip (the YODAS2 maximum chunk) and an empty clip in one batch; scipy live."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from scipy.signal import resample_poly
+    x = np.random.default_rng(11).normal(0, 0.1, 16000 * 60).astype(np.float32)
+    outs = ingest.resample([x, np.zeros(0, np.float32), x[:7]], 16000, 24000, device="cuda:0")
+    assert outs[1].numel() == 0
+    assert bits_equal(outs[0].cpu().numpy(), resample_poly(x, 3, 2))
+    assert bits_equal(outs[2].cpu().numpy(), resample_poly(x[:7], 3, 2))
+
+
+@pytest.mark.gpu
+def test_load_then_encode(tmp_path):
+    """WAV at 16 kHz -> GPU resample -> the same samples librosa's polyphase mode gives (restated)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    pcm = np.random.default_rng(5).integers(-20000, 20000, 16000 * 3, dtype=np.int16)
+    p = str(tmp_path / "a.wav")
+    _write_wav(p, pcm, 16000, 2)
+    y, sr = ingest.load(p, sr=24000, device="cuda:0")
+    assert sr == 24000 and len(y) == 72000
+    assert bits_equal(y, librosa_polyphase_ref(pcm.astype(np.float32) / 32768.0, 16000, 24000))

@@ -138,6 +138,31 @@ extern "C" int64_t mimi_encoded_length_cfg(const mimi_config* cfg, int64_t lengt
 extern "C" int64_t mimi_encoded_length(int64_t length) { return mimi_encoded_length_cfg(nullptr, length); }
 
 // ------------------------------------------------------------------------------------------------
+// host-ingest resampler (no engine handle: pure function of its device buffers)
+// ------------------------------------------------------------------------------------------------
+extern "C" int mimi_resample_poly(const float* dev_in, const int64_t* dev_in_off, const int64_t* dev_in_len,
+                                  int32_t nclips, float* dev_out, const int64_t* dev_out_off,
+                                  const int64_t* dev_out_len, int64_t max_out, const float* dev_filter,
+                                  int32_t filter_len, int32_t up, int32_t down, int64_t pre_remove, void* stream) {
+    if (nclips < 0 || up < 1 || down < 1 || pre_remove < 0 || max_out < 0)
+        return set_err(MIMI_ERR_INVALID_ARGUMENT, "mimi_resample_poly: bad sizes (nclips %d, up %d, down %d)",
+                       nclips, up, down);
+    if (filter_len < 1 || filter_len > MIMI_RESAMPLE_MAX_TAPS)
+        return set_err(MIMI_ERR_UNSUPPORTED, "mimi_resample_poly: filter of %d taps (max %d)", filter_len,
+                       MIMI_RESAMPLE_MAX_TAPS);
+    if (nclips == 0 || max_out == 0) return MIMI_OK;
+    if (!dev_in || !dev_in_off || !dev_in_len || !dev_out || !dev_out_off || !dev_out_len || !dev_filter)
+        return set_err(MIMI_ERR_INVALID_ARGUMENT, "mimi_resample_poly: null buffer");
+    const hipError_t e = launch_resample_poly(dev_in, reinterpret_cast<const long long*>(dev_in_off),
+                                              reinterpret_cast<const long long*>(dev_in_len), nclips, dev_out,
+                                              reinterpret_cast<const long long*>(dev_out_off),
+                                              reinterpret_cast<const long long*>(dev_out_len), max_out, dev_filter,
+                                              filter_len, up, down, pre_remove, (hipStream_t)stream);
+    if (e != hipSuccess) return set_err(MIMI_ERR_HIP, "resample_poly launch: %s", hipGetErrorString(e));
+    return MIMI_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
 // engine
 // ------------------------------------------------------------------------------------------------
 struct DevConv {

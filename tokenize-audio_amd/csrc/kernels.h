@@ -256,4 +256,9 @@ struct RvqArgs {
 size_t rvq_work_bytes(long long frames);
 hipError_t launch_rvq(const RvqArgs& a, hipStream_t s);
 
+// polyphase resampler (resample.hip): clips packed at in_off / out_off (device int64 arrays), one launch
+hipError_t launch_resample_poly(const float* x, const long long* in_off, const long long* in_len, int nclips,
+                                float* y, const long long* out_off, const long long* out_len, long long max_out,
+                                const float* h, int lh, int up, int down, long long pre_remove, hipStream_t s);
+
 }  // namespace mimi

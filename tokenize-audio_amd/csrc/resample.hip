@@ -1,0 +1,92 @@
+// Host-ingest resampler on the GPU: the polyphase (upfirdn) resampling of librosa's res_type='polyphase'
+// (= scipy.signal.resample_poly, Kaiser(5.0) low-pass of 2*10*max(up,down)+1 taps), bit-exact with scipy on
+// float32 input.  Ref call sites: librosa.load(path, sr=24000) in librispeech-mimi/utils.py:84-87,
+// emilia-mimi/process_shard.py:479-482, yodas2-mimi/process_shard.py:389 (their default soxr_hq mode is
+// libsoxr, absent here: unpinned).
+//
+// Output m of a clip sits at up-sampled position p = (m + pre_remove) * down and is the sum over input
+// samples j in [ceil((p - (lh-1)) / up), min(p / up, n_in - 1)] of x[j] * h[p - j*up], added in ASCENDING j
+// to a 0-initialised fp32 accumulator with one rounding per product and per add -- the inner-loop order of
+// scipy's upfirdn (_upfirdn_apply.pyx), which is what makes the result bitwise equal.
+//
+// HBM-bound byte work: 4 B read per input sample, 4 B written per output (x re-reads of neighbouring outputs
+// are served from LDS: each pass stages its input window once, coalesced); the filter sits in LDS too.  One
+// thread per output sample, consecutive outputs on consecutive lanes (coalesced stores); blockIdx.y = clip, so
+// a batch of ragged clips is one launch.
+#include "kernels.h"
+
+namespace mimi {
+
+constexpr int RS_BLOCK = 256;  // outputs per workgroup pass (one per thread)
+
+// input samples one pass's 256 consecutive outputs touch: ((256-1) * down + lh - 1) / up + 2
+__host__ __device__ inline long long resample_window(int lh, int up, int down) {
+    return ((long long)(RS_BLOCK - 1) * down + lh - 1) / up + 2;
+}
+
+__global__ __launch_bounds__(RS_BLOCK) void resample_poly_kernel(const float* __restrict__ x,
+                                                                 const long long* __restrict__ in_off,
+                                                                 const long long* __restrict__ in_len,
+                                                                 float* __restrict__ y,
+                                                                 const long long* __restrict__ out_off,
+                                                                 const long long* __restrict__ out_len,
+                                                                 const float* __restrict__ h, int lh, int up,
+                                                                 int down, long long pre_remove) {
+    extern __shared__ float lds[];
+    float* hs = lds;           // the filter, lh taps
+    float* xs = lds + lh;      // this pass's input window
+    const int W = (int)resample_window(lh, up, down);
+    for (int i = threadIdx.x; i < lh; i += RS_BLOCK) hs[i] = h[i];
+    const int c = blockIdx.y;
+    const long long n_in = in_len[c], n_out = out_len[c];
+    const float* __restrict__ xc = x + in_off[c];
+    float* __restrict__ yc = y + out_off[c];
+    // jlo(p) = max(ceil((p - (lh-1)) / up), 0), jhi(p) = min(floor(p / up), n_in - 1).  64-bit divisions only
+    // once per pass (wave-uniform); per output, p = q0*up + pr with pr = r0 + tid*down < 2^31, so the rest is
+    // 32-bit: ceil((pr - (lh-1)) / up) = (pr - (lh-1) + kc*up + up-1) / up - kc with kc*up >= lh-1
+    const int kc = (lh - 1 + up - 1) / up;
+    const int tid = threadIdx.x;
+    for (long long m0 = (long long)blockIdx.x * RS_BLOCK; m0 < n_out; m0 += (long long)gridDim.x * RS_BLOCK) {
+        const long long p0 = (m0 + pre_remove) * down;
+        const long long q0 = p0 / up;
+        const int r0 = (int)(p0 - q0 * up);
+        const long long w0 = max(q0 + (r0 - (lh - 1) + kc * up + up - 1) / up - kc, 0LL);  // jlo of output m0
+        __syncthreads();  // previous pass done with xs (and hs written, first pass)
+        for (int i = tid; i < W; i += RS_BLOCK) {
+            const long long j = w0 + i;
+            xs[i] = j < n_in ? xc[j] : 0.0f;
+        }
+        __syncthreads();
+        const long long m = m0 + tid;
+        if (m < n_out) {
+            const int pr = r0 + tid * down;
+            const long long jhi = min(q0 + pr / up, n_in - 1);
+            const long long jlo = max(q0 + (pr - (lh - 1) + kc * up + up - 1) / up - kc, 0LL);
+            float acc = 0.0f;
+            int k = pr - (int)(jlo - q0) * up;  // filter index of the first term (< lh)
+            const float* xp = xs + (int)(jlo - w0);
+            const int cnt = (int)(jhi - jlo + 1);
+#pragma unroll 4
+            for (int t = 0; t < cnt; ++t) acc = __fadd_rn(acc, __fmul_rn(xp[t], hs[k - t * up]));
+            yc[m] = acc;
+        }
+    }
+}
+
+hipError_t launch_resample_poly(const float* x, const long long* in_off, const long long* in_len, int nclips,
+                                float* y, const long long* out_off, const long long* out_len, long long max_out,
+                                const float* h, int lh, int up, int down, long long pre_remove, hipStream_t s) {
+    if (nclips <= 0 || max_out <= 0) return hipSuccess;
+    const long long lds_bytes = (lh + resample_window(lh, up, down)) * 4;
+    if (lds_bytes > 64 * 1024) return hipErrorInvalidValue;  // default dynamic-LDS limit
+    // ~4096 workgroups in all (16 per CU), each sweeping many 256-output passes of one clip: a workgroup per
+    // pass would spend more time being dispatched and loading the filter than resampling
+    long long bx = (max_out + RS_BLOCK - 1) / RS_BLOCK;
+    const long long cap = (4096 + nclips - 1) / nclips;
+    if (bx > cap) bx = cap;
+    hipLaunchKernelGGL(resample_poly_kernel, dim3((unsigned)bx, (unsigned)nclips), dim3(RS_BLOCK), (size_t)lds_bytes,
+                       s, x, in_off, in_len, y, out_off, out_len, h, lh, up, down, pre_remove);
+    return hipGetLastError();
+}
+
+}  // namespace mimi

@@ -27,8 +27,9 @@ EXPORTED_SYMBOLS = (
     "mimi_encode", "mimi_rvq_encode", "mimi_set_precision", "mimi_get_precision", "mimi_f16_reruns", "mimi_encoded_length",
     "mimi_encoded_length_cfg",
     "mimi_workspace_bytes", "mimi_destroy", "mimi_last_error", "mimi_set_profiling", "mimi_profile_read",
-    "mimi_profile_reset", "mimi_set_taps", "mimi_get_tap",
+    "mimi_profile_reset", "mimi_set_taps", "mimi_get_tap", "mimi_resample_poly",
 )
+RESAMPLE_MAX_TAPS = 8192  # MIMI_RESAMPLE_MAX_TAPS
 
 
 class MimiConfigC(ctypes.Structure):
@@ -81,6 +82,8 @@ def _declare(lib):
         "mimi_profile_reset": (c.c_int, [vp]),
         "mimi_set_taps": (c.c_int, [vp, c.c_int]),
         "mimi_get_tap": (c.c_int, [vp, c.c_char_p, vp, c.c_int64, c.POINTER(c.c_int64), c.POINTER(c.c_int64)]),
+        "mimi_resample_poly": (c.c_int, [vp, vp, vp, c.c_int32, vp, vp, vp, c.c_int64, vp, c.c_int32, c.c_int32,
+                                         c.c_int32, c.c_int64, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -1,0 +1,148 @@
+"""Host ingest: waveform loading and resampling to the codec's 24 kHz, with the resampling on the GPU.
+
+Replaces ``librosa.load(path, sr=24000)`` on the shard scripts' load path (``librispeech-mimi/utils.py:84-87``,
+``emilia-mimi/process_shard.py:479-482``, ``yodas2-mimi/process_shard.py:389``) for PCM / float WAV files:
+
+* ``load_wav``: libsndfile's float conversion as librosa gets it through soundfile (integer PCM divided by
+  2^(bits-1), unsigned 8-bit re-centred first) and librosa's ``to_mono`` (mean over channels in float32);
+* ``resample``: librosa's ``res_type='polyphase'`` (= ``scipy.signal.resample_poly`` plus ``fix_length`` to
+  ``ceil(n * target_sr / orig_sr)``), computed by the HIP kernel ``resample_poly_kernel`` through the C ABI
+  (``mimi_resample_poly``), bit-exact with scipy on float32 input.  Ragged clips go in ONE launch.
+
+Parity limits: librosa is not installed, so its DEFAULT mode (``soxr_hq``, libsoxr) is
+unpinned -- a script that wants bit-identical inputs to an existing soxr-resampled shard must keep librosa;
+what is pinned is the polyphase mode, against scipy itself.  Compressed formats (flac / mp3 / opus) need a
+decoder this image lacks and are out of scope.
+
+Only the filter design (61 taps for 16 -> 24 kHz) runs on the host, with ``scipy.signal.firwin`` exactly as
+``resample_poly`` designs it; there is no CPU resampling path.
+"""
+import math
+from typing import List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import _lib
+
+__all__ = ["resample_plan", "resample", "resample_packed", "load_wav", "load"]
+
+
+def resample_plan(orig_sr: int, target_sr: int) -> Tuple[int, int, np.ndarray, int]:
+    """(up, down, filter with its zero pre-padding, n_pre_remove) as ``scipy.signal.resample_poly`` builds them
+    for float32 input (scipy 1.15 ``_signaltools.py``: half_len = 10 max(up, down), Kaiser(5.0), x up)."""
+    from scipy.signal import firwin
+    if int(orig_sr) != orig_sr or int(target_sr) != target_sr or orig_sr <= 0 or target_sr <= 0:
+        raise ValueError("polyphase resampling requires positive integer sample rates")
+    g = math.gcd(int(orig_sr), int(target_sr))
+    up, down = int(target_sr) // g, int(orig_sr) // g
+    max_rate = max(up, down)
+    half_len = 10 * max_rate
+    h = firwin(2 * half_len + 1, 1.0 / max_rate, window=("kaiser", 5.0)).astype(np.float32)
+    h *= up
+    n_pre_pad = down - half_len % down
+    hp = np.concatenate([np.zeros(n_pre_pad, np.float32), h])
+    if len(hp) > _lib.RESAMPLE_MAX_TAPS:
+        raise ValueError(f"resampling {orig_sr} -> {target_sr} Hz needs a {len(hp)}-tap filter "
+                         f"(the kernel keeps at most {_lib.RESAMPLE_MAX_TAPS} in LDS)")
+    return up, down, hp, (half_len + n_pre_pad) // down
+
+
+def _device(device) -> torch.device:
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise ValueError("resampling runs on the HIP device only (no CPU path); pass device='cuda[:i]'")
+    return d
+
+
+_FILTERS = {}  # (orig_sr, target_sr, device) -> (up, down, device filter, taps, n_pre_remove)
+
+
+def _plan_on(orig_sr: int, target_sr: int, dev: torch.device):
+    key = (int(orig_sr), int(target_sr), str(dev))
+    if key not in _FILTERS:
+        up, down, hp, pre = resample_plan(orig_sr, target_sr)
+        _FILTERS[key] = (up, down, torch.from_numpy(hp).to(dev), len(hp), pre)
+    return _FILTERS[key]
+
+
+def resample_packed(x: torch.Tensor, lengths: Sequence[int], orig_sr: int, target_sr: int = 24000
+                    ) -> Tuple[torch.Tensor, List[int]]:
+    """The kernel call: ``x`` is a device float32 buffer holding the clips back to back (``lengths``).
+    Returns (packed output, output lengths = ``ceil(len * target_sr / orig_sr)``, librosa's fix_length)."""
+    dev = _device(x.device)
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        raise ValueError("x must be a contiguous float32 device tensor")
+    n_in = [int(n) for n in lengths]
+    if sum(n_in) > x.numel():
+        raise ValueError("lengths exceed the packed buffer")
+    ratio = float(target_sr) / orig_sr
+    n_fix = [int(math.ceil(n * ratio)) for n in n_in]                  # librosa fix_length target
+    if orig_sr == target_sr:
+        return x[:sum(n_in)].clone(), n_fix
+    up, down, filt, taps, pre_remove = _plan_on(orig_sr, target_sr, dev)
+    n_poly = [-(-n * up // down) for n in n_in]                         # resample_poly's own length
+    n_run = [min(a, b) for a, b in zip(n_fix, n_poly)]                  # longer fix_length: zero tail
+    in_off = np.concatenate([[0], np.cumsum(n_in)[:-1]]).astype(np.int64) if n_in else np.zeros(0, np.int64)
+    out_off = np.concatenate([[0], np.cumsum(n_fix)[:-1]]).astype(np.int64) if n_fix else np.zeros(0, np.int64)
+    out = torch.empty(max(1, sum(n_fix)), dtype=torch.float32, device=dev)
+    for o, a, b in zip(out_off.tolist(), n_run, n_fix):
+        if b > a:
+            out[o + a:o + b].zero_()
+    if not n_in or max(n_run) == 0:
+        return out, n_fix
+    meta = torch.from_numpy(np.stack([in_off, np.asarray(n_in, np.int64), out_off,
+                                      np.asarray(n_run, np.int64)])).to(dev, non_blocking=False)
+    lib = _lib.load()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(lib.mimi_resample_poly(x.data_ptr(), meta[0].data_ptr(), meta[1].data_ptr(), len(n_in),
+                                      out.data_ptr(), meta[2].data_ptr(), meta[3].data_ptr(), max(n_run),
+                                      filt.data_ptr(), taps, up, down, pre_remove, stream))
+    return out, n_fix
+
+
+def resample(clips: Sequence[Union[np.ndarray, torch.Tensor]], orig_sr: int, target_sr: int = 24000,
+             device: Union[str, torch.device] = "cuda") -> List[torch.Tensor]:
+    """Resample ragged mono clips (numpy or torch, any float dtype -> float32) in one launch.  Returns device
+    float32 tensors of ``ceil(len * target_sr / orig_sr)`` samples (librosa's length), views into one
+    packed buffer."""
+    dev = _device(device)
+    xs = [torch.as_tensor(np.asarray(c, dtype=np.float32) if isinstance(c, np.ndarray) else c)
+          .to(device=dev, dtype=torch.float32).reshape(-1) for c in clips]
+    if not xs:
+        return []
+    xin = torch.cat(xs) if len(xs) > 1 else xs[0].contiguous()
+    out, n_fix = resample_packed(xin, [x.numel() for x in xs], orig_sr, target_sr)
+    offs = np.concatenate([[0], np.cumsum(n_fix)[:-1]]).tolist()
+    return [out[o:o + n] for o, n in zip(offs, n_fix)]
+
+
+def load_wav(path: str) -> Tuple[np.ndarray, int]:
+    """WAV file -> (float32 mono samples, sample rate), as librosa.load(path, sr=None) returns it."""
+    from scipy.io import wavfile
+    sr, data = wavfile.read(path)
+    if data.dtype == np.uint8:
+        y = (data.astype(np.float32) - 128.0) / 128.0
+    elif data.dtype == np.int16:
+        y = data.astype(np.float32) / 32768.0
+    elif data.dtype == np.int32:   # 24-bit PCM is left-justified into int32 by scipy
+        y = (data.astype(np.float64) / 2147483648.0).astype(np.float32)
+    elif data.dtype in (np.float32, np.float64):
+        y = data.astype(np.float32)
+    else:
+        raise ValueError(f"unsupported WAV sample type {data.dtype}")
+    if y.ndim == 2:
+        y = np.mean(y, axis=1, dtype=np.float32)    # librosa.to_mono
+    return np.ascontiguousarray(y), int(sr)
+
+
+def load(path: str, sr: Optional[int] = 24000, device: Union[str, torch.device] = "cuda",
+         as_numpy: bool = True):
+    """``librosa.load(path, sr=sr, res_type='polyphase')`` for WAV: returns (samples, sr).  Samples are a numpy
+    float32 array (``as_numpy``) or the device tensor, ready for ``MimiHipModel.encode``."""
+    y, file_sr = load_wav(path)
+    if sr is None or sr == file_sr:
+        t = torch.from_numpy(y)
+        return (y if as_numpy else t.to(_device(device))), file_sr
+    out = resample([y], file_sr, sr, device)[0]
+    return (out.cpu().numpy() if as_numpy else out), sr
