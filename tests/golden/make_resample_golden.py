@@ -27,7 +27,7 @@ def main():
         g = math.gcd(r, TARGET)
         for n in LENGTHS:
             y = resample_poly(clip(r, n), TARGET // g, r // g)
-            m = int(math.ceil(n * float(TARGET) / r))
+            m = int(math.ceil(n * (float(TARGET) / r)))  # librosa: ratio first
             y = y[:m] if len(y) >= m else np.concatenate([y, np.zeros(m - len(y), np.float32)])
             assert y.dtype == np.float32
             out[f"r{r}_n{n}"] = y

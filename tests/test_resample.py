@@ -130,3 +130,24 @@ def test_load_then_encode(tmp_path):
     y, sr = ingest.load(p, sr=24000, device="cuda:0")
     assert sr == 24000 and len(y) == 72000
     assert bits_equal(y, librosa_polyphase_ref(pcm.astype(np.float32) / 32768.0, 16000, 24000))
+
+
+@pytest.mark.gpu
+def test_resample_kernel_window_variants_vs_scipy():
+    """Down-sampling ratios whose per-pass input window needs 1, 2, 4 prefetch registers per thread or the
+    load-then-compute path (96 kHz -> 24 kHz: > 1024 samples), against scipy live."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from scipy.signal import resample_poly
+    rng = np.random.default_rng(12)
+    for orig in (8000, 48000, 72000, 96000, 22050):
+        g = math.gcd(orig, 24000)
+        xs = [rng.normal(0, 0.2, n).astype(np.float32) for n in (orig * 3 + 17, 5, orig // 3)]
+        outs = ingest.resample(xs, orig, 24000, device="cuda:0")
+        for x, o in zip(xs, outs):
+            want = resample_poly(x, 24000 // g, orig // g)
+            # librosa: n_samples = int(np.ceil(n * ratio)) with ratio = float(target) / orig, rounded first --
+            # 7350 samples at 22.05 kHz give ceil(8000.000000000001) = 8001, one zero past resample_poly's 8000
+            m = int(math.ceil(len(x) * (24000.0 / orig)))
+            want = want[:m] if len(want) >= m else np.concatenate([want, np.zeros(m - len(want), np.float32)])
+            assert bits_equal(o.cpu().numpy(), want), (orig, len(x))
