@@ -214,6 +214,10 @@ struct mimi_engine {
     // PREC_F16X3: stage 0 on the fp16-plane fused kernel (MIMI_HIP_RES0_H16=0 falls back to the fp32-MFMA one)
     bool res0_h16_on = true;
     bool res1_h16_on = true;  // MIMI_HIP_RES1_H16=0: stage 1 on the fp32-MFMA fused kernel
+    // PREC_F16X3: stage 0 (fused block + down conv) runs over chunks of s0_chunk utterances so the chunk's
+    // y planes (61 MB per 10 s utterance) are re-read from the 256 MiB Infinity Cache instead of HBM
+    // (MIMI_HIP_S0_CHUNK; 0 = whole batch)
+    int s0_chunk = 0;
 
     std::unordered_map<std::string, std::vector<float>> host_w;
     std::unordered_map<std::string, std::vector<int64_t>> expected;  // name -> shape
@@ -458,6 +462,7 @@ extern "C" int mimi_create(const mimi_config* cfg, int device, mimi_engine** out
     if (const char* rs = std::getenv("MIMI_HIP_RES128_SPLIT")) e->res128_split = std::atoi(rs) != 0;
     if (const char* r0 = std::getenv("MIMI_HIP_RES0_H16")) e->res0_h16_on = std::atoi(r0) != 0;
     if (const char* r1 = std::getenv("MIMI_HIP_RES1_H16")) e->res1_h16_on = std::atoi(r1) != 0;
+    if (const char* sc = std::getenv("MIMI_HIP_S0_CHUNK")) e->s0_chunk = std::atoi(sc);
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipEventCreateWithFlags(&e->ws_free, hipEventDisableTiming));
     HIP_TRY(hipMalloc(&e->amax_dev, ((size_t)kMaxActSlots * AMAX_SLOT_WORDS + kMaxActSlots) * sizeof(unsigned)));
@@ -1244,7 +1249,61 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     int C = c.num_filters;
     char nm[64];
     Act yact, xact, xeact, hact;  // the tensors currently held by y, x (last down conv), xe, h
-    for (int si = 0; si < c.num_ratios; ++si) {
+    int si0 = 0;
+    {
+        // stage 0 in utterance chunks (fp16 fused block + its down conv per chunk, same activation slots)
+        const int64_t T = p.T[0], T1 = p.T[1];
+        const int bc0 = e->s0_chunk;
+        if (bc0 > 0 && bc0 < B && h16 && ns && e->res0_h16 && e->res0_h16_on && !e->taps && c.num_ratios > 1 &&
+            1 < e->unfuse_from && (unsigned long long)B * (unsigned long long)((T + 31) / 32) < (1ull << 32)) {
+            yact = new_act();
+            const Act aa = new_act(), xa = new_act(), ha = new_act();
+            const double H = C / c.compress;
+            for (int b0 = 0; b0 < B; b0 += bc0) {
+                const int bc = std::min(bc0, B - b0);
+                ResArgs ra{};
+                ra.x = w.x;
+                ra.audio = audio + (long long)b0 * T;
+                ra.w0 = e->conv0.w;
+                ra.b0 = e->conv0.b;
+                ra.w3frag = e->res3[0].wfrag;
+                ra.w1frag = e->res1[0].wfrag;
+                ra.T = T;
+                ra.batch = bc;
+                ra.w3 = e->res3[0].w;
+                ra.b3 = e->res3[0].b;
+                ra.w1 = e->res1[0].w;
+                ra.b1 = e->res1[0].b;
+                ra.y = w.y;
+                ra.yp = w.y;
+                ra.y_pstride = (long long)bc * T * C;
+                ra.yns = ns;
+                ra.yscale = yact.scale;
+                ra.yamax = yact.amax;
+                ra.wh16 = e->res0_h16;
+                ra.ascale = aa.scale;
+                ra.xscale = xa.scale;
+                ra.hscale = ha.scale;
+                ra.unscale0 = 1.0f / (aa.scale * e->res0_wsc[0]);
+                ra.unscale1 = 1.0f / (xa.scale * e->res0_wsc[1]);
+                ra.unscale2 = 1.0f / (ha.scale * e->res0_wsc[2]);
+                ra.aamax = aa.amax;
+                ra.xamax = xa.amax;
+                ra.hamax = ha.amax;
+                LAUNCH_TRY(launch_resblock(C, ra, s, &kname), "resblock");
+                const double fl = 2.0 * bc * T * (3.0 * C * H + H * C) + 2.0 * bc * T * C * c.kernel_size;
+                rec.mark("res_s0", fl, (double)bc * T * 4 * (1 + C), kname);
+                GemmArgs ad = conv_args(e->down[0], w.y, T, w.x + (long long)b0 * T1 * 2 * C, T1, bc);
+                planes_in(ad, w.y, (long long)bc * T * C);
+                use_h(ad, e->down[0].wh, e->down[0].wscale, yact);
+                LAUNCH_TRY(launch_gemm(ROLE_DOWN, ad, s, &kname, prec), "down");
+                rec.mark("down_s0", gemm_flops(ad), gemm_bytes(ad, false), kname);
+            }
+            C *= 2;
+            si0 = 1;
+        }
+    }
+    for (int si = si0; si < c.num_ratios; ++si) {
         const int64_t T = p.T[si];
         const bool unf = ns && si > 0 && si >= e->unfuse_from;
         if (!unf) {
