@@ -38,15 +38,19 @@ __device__ __forceinline__ long long pass_w0(long long m0, long long pre_remove,
 // WPT > 0: the next pass's window (<= WPT * 256 samples) is loaded into registers while this pass computes, then
 // stored into the other half of a double-buffered LDS window (one barrier per pass, HBM latency hidden);
 // WPT == 0: load-then-compute (windows over 1024 samples: extreme ratios only)
-template <int WPT>
+// UPC > 0: the up-sampling factor as a compile-time constant (1: 48/72/96 -> 24 kHz, 3: 8/16 -> 24 kHz), so the
+// unrolled tap loop's LDS addresses are immediate offsets from two bases (2 ds_read + mul + add per tap); 0:
+// any factor, read at run time
+template <int WPT, int UPC>
 __global__ __launch_bounds__(RS_BLOCK) void resample_poly_kernel(const float* __restrict__ x,
                                                                  const long long* __restrict__ in_off,
                                                                  const long long* __restrict__ in_len,
                                                                  float* __restrict__ y,
                                                                  const long long* __restrict__ out_off,
                                                                  const long long* __restrict__ out_len,
-                                                                 const float* __restrict__ h, int lh, int up,
+                                                                 const float* __restrict__ h, int lh, int up_rt,
                                                                  int down, long long pre_remove) {
+    const int up = UPC > 0 ? UPC : up_rt;
     extern __shared__ float lds[];
     const int W = (int)resample_window(lh, up, down);
     float* hs = lds;           // the filter, lh taps
@@ -104,11 +108,12 @@ __global__ __launch_bounds__(RS_BLOCK) void resample_poly_kernel(const float* __
             const long long jhi = min(q0 + pr / up, n_in - 1);
             const long long jlo = max(q0 + (pr - (lh - 1) + kc * up + up - 1) / up - kc, 0LL);
             float acc = 0.0f;
-            int k = pr - (int)(jlo - q0) * up;  // filter index of the first term (< lh)
+            const int k = pr - (int)(jlo - q0) * up;  // filter index of the first term (< lh)
             const float* xp = xs + (int)(jlo - w0);
+            const float* hp = hs + k;
             const int cnt = (int)(jhi - jlo + 1);
-#pragma unroll 4
-            for (int t = 0; t < cnt; ++t) acc = __fadd_rn(acc, __fmul_rn(xp[t], hs[k - t * up]));
+#pragma unroll 8
+            for (int t = 0; t < cnt; ++t) acc = __fadd_rn(acc, __fmul_rn(xp[t], hp[-t * up]));
             yc[m] = acc;
         }
         if (WPT > 0) {
@@ -141,15 +146,24 @@ hipError_t launch_resample_poly(const float* x, const long long* in_off, const l
     const long long cap = (4096 + nclips - 1) / nclips;
     if (bx > cap) bx = cap;
     const dim3 grid((unsigned)bx, (unsigned)nclips);
-#define RS_LAUNCH(N)                                                                                            \
-    hipLaunchKernelGGL(resample_poly_kernel<N>, grid, dim3(RS_BLOCK), (size_t)lds_bytes, s, x, in_off, in_len, y, \
-                       out_off, out_len, h, lh, up, down, pre_remove)
-    switch (wpt) {
-        case 1: RS_LAUNCH(1); break;
-        case 2: RS_LAUNCH(2); break;
-        case 4: RS_LAUNCH(4); break;
-        default: RS_LAUNCH(0); break;
+#define RS_LAUNCH(N, U)                                                                                      \
+    hipLaunchKernelGGL((resample_poly_kernel<N, U>), grid, dim3(RS_BLOCK), (size_t)lds_bytes, s, x, in_off, in_len, \
+                       y, out_off, out_len, h, lh, up, down, pre_remove)
+#define RS_LAUNCH_W(U)              \
+    switch (wpt) {                  \
+        case 1: RS_LAUNCH(1, U); break; \
+        case 2: RS_LAUNCH(2, U); break; \
+        case 4: RS_LAUNCH(4, U); break; \
+        default: RS_LAUNCH(0, U); break; \
     }
+    if (up == 3) {
+        RS_LAUNCH_W(3);
+    } else if (up == 1) {
+        RS_LAUNCH_W(1);
+    } else {
+        RS_LAUNCH_W(0);
+    }
+#undef RS_LAUNCH_W
 #undef RS_LAUNCH
     return hipGetLastError();
 }

@@ -44,8 +44,10 @@ def main():
     algo = 4 * (a.clips * n + nout)
     from scipy.signal import resample_poly
     xs = x[:n].cpu().numpy()
+    import math
+    g = math.gcd(a.rate, 24000)
     t0 = time.perf_counter()
-    resample_poly(xs, 24000 // 8000, a.rate // 8000) if a.rate == 16000 else None
+    resample_poly(xs, 24000 // g, a.rate // g)
     cpu_s = time.perf_counter() - t0
     print(json.dumps({"kernel": "resample_poly_kernel", "clips": a.clips, "clip_seconds": a.seconds,
                       "rate": a.rate, "ms_per_call": round(ms, 4),
