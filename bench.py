@@ -28,6 +28,7 @@ for _p in (os.path.join(ROOT, "tokenize-audio_amd"), ROOT):
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 MFMA/vector peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec
 BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak
+F16X3_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 3  # fp32-accurate products as 3 fp16 products
 
 
 def mfma_peak_for(kernel: str):
@@ -93,6 +94,51 @@ def cpu_baseline(seconds_budget: float, threads: int, clip_s: float):
     return {"value": round(done * clip_s / el, 3), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
             "sample": f"{done} x {clip_s:g} s clips, batch 1, K=8, oracle/mimi_ref.py (torch {torch.__version__} CPU, "
                       f"{threads} threads, {cpu_model})"}
+
+
+def pmc_lookup(pmc_kernels, name):
+    """PMC summary entry of a kernel symbol: the summary keys drop rocprof's 'void ' prefix and, for
+    non-template kernels, the parameter list that the engine's names keep."""
+    if name in pmc_kernels:
+        return pmc_kernels[name]
+    bare = name[5:] if name.startswith("void ") else name
+    if "(" in bare and not bare.endswith(">"):
+        bare = bare[:bare.index("(")]
+    return pmc_kernels.get(bare, {})
+
+
+def north_star_groups(prof, steps, pmc_path):
+    """BASELINE.json's reporting asks: HBM GB/s and TFLOP/s of the SEANet conv stack, MFMA utilisation of the
+    transformer.  Device ms and algorithmic FLOPs from the engine's events; HBM bytes = the PMC passes'
+    FETCH_SIZE x 2 + WRITE_SIZE per launch of each kernel symbol (profiles/pmc_summary.json; a symbol shared
+    by several stages carries its average) x that stage's launches."""
+    pmc = {}
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f).get("kernels", {})
+    groups = {
+        "conv_stack": [s for s in prof if s.startswith(("res", "down_s", "final"))],
+        "transformer": [s for s in prof if s in ("layernorm", "qkv", "attention", "o_proj", "fc1", "fc2")],
+        "quantizer": [s for s in prof if s in ("downsample", "input_proj", "rvq")],
+    }
+    out = {}
+    for g, stages in groups.items():
+        if not stages:
+            continue
+        ms = sum(prof[s]["ms"] for s in stages) / steps
+        fl = sum(prof[s]["flops"] for s in stages) / steps
+        hbm = [pmc_lookup(pmc, prof[s]["kernel"]).get("traffic_bytes") for s in stages]
+        d = {"stages": stages, "ms_per_step": round(ms, 3), "tflops": round(fl / (ms / 1e3) / 1e12, 1),
+             "frac_f16x3_peak": round(fl / (ms / 1e3) / 1e12 / F16X3_PEAK_TFLOPS, 4)}
+        missing = [prof[s]["kernel"] for s, b in zip(stages, hbm) if b is None]
+        if missing:
+            d["hbm_unmeasured_kernels"] = sorted(set(missing))
+        else:
+            by = sum(b * prof[s]["launches"] / steps for b, s in zip(hbm, stages))
+            d.update({"hbm_bytes_per_step": round(by), "hbm_GBps": round(by / (ms / 1e3) / 1e9, 1),
+                      "frac_hbm_peak": round(by / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)})
+        out[g] = d
+    return out
 
 
 def main():
@@ -217,7 +263,7 @@ def main():
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            k = pmc.get("kernels", {}).get(dom_name, {})
+            k = pmc_lookup(pmc.get("kernels", {}), dom_name)
             if "traffic_bytes" in k:
                 traffic = round(k["traffic_bytes"])
                 traffic_src = {"source": f"profiles/{pmc['tag']}_pmc_summary.json", "unit": "bytes per launch",
@@ -233,6 +279,7 @@ def main():
                                   "tflops": round(tot_fl / (tot_ms / 1000) / 1e12, 2),
                                   "frac_fp32_peak": round(tot_fl / (tot_ms / 1000) / 1e12 / FP32_PEAK_TFLOPS, 4)}
         result["stages_ms_per_step"] = {s: round(v["ms"] / args.steps, 3) for s, v in prof.items()}
+        result["north_star"] = north_star_groups(prof, args.steps, pmc_path)
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.cpu_threads, args.seconds)
     if rank == 0:
