@@ -122,3 +122,24 @@ def test_import_without_gpu_has_no_fallback():
         pytest.skip("GPU present")
     with pytest.raises(Exception):
         model.MimiHipModel(synthetic.make_state_dict(seed=0, num_quantizers=2), device="cuda")
+
+
+def test_bench_north_star_groups(tmp_path):
+    """bench.py's north-star breakdown: stage grouping, PMC lookup by bare symbol, HBM rate arithmetic."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    pmc = {"tag": "t", "kernels": {"mimi::resblock0_h16_kernel": {"traffic_bytes": 2.0e9},
+                                   "mimi::gemm_planes_kernel<1, 2>": {"traffic_bytes": 1.0e9}}}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps(pmc))
+    prof = {"res_s0": {"ms": 7.0, "flops": 1.4e12, "kernel": "mimi::resblock0_h16_kernel(mimi::ResArgs)",
+                       "launches": 10},
+            "down_s0": {"ms": 10.0, "flops": 2.5e12, "kernel": "void mimi::gemm_planes_kernel<1, 2>", "launches": 10},
+            "qkv": {"ms": 5.0, "flops": 1.0e12, "kernel": "unknown", "launches": 80}}
+    g = bench.north_star_groups(prof, 10, str(p))
+    cs = g["conv_stack"]
+    assert cs["stages"] == ["res_s0", "down_s0"] and cs["ms_per_step"] == 1.7
+    assert cs["hbm_bytes_per_step"] == 3_000_000_000 and abs(cs["hbm_GBps"] - 3e9 / 1.7e-3 / 1e9) < 0.1
+    assert g["transformer"]["hbm_unmeasured_kernels"] == ["unknown"]
+    assert "quantizer" not in g
