@@ -7,5 +7,5 @@ i=0
 for cfg in "$@"; do
   i=$((i+1))
   env $cfg timeout -k 10 300 python bench.py --cpu-baseline-seconds 0 > gpurun_out/ab_$i.log 2>&1 || { echo "run $i ($cfg) failed"; exit 1; }
-  echo "run $i ($cfg): $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_$i.log)"
+  echo "run $i ($cfg): $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_$i.log | head -1)"
 done
