@@ -120,16 +120,27 @@ def test_resample_kernel_full_size_vs_scipy():
 
 
 @pytest.mark.gpu
-def test_load_then_encode(tmp_path):
-    """WAV at 16 kHz -> GPU resample -> the same samples librosa's polyphase mode gives (restated)."""
+def test_load_then_encode(tmp_path, state_dict):
+    """WAV at 16 kHz -> GPU resample -> the same samples librosa's polyphase mode gives (restated) -> the
+    drop-in MimiEncoder on the HIP engine -> the oracle's codes for those samples."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    pcm = np.random.default_rng(5).integers(-20000, 20000, 16000 * 3, dtype=np.int16)
+    from mimi_hip.encoder import MimiEncoder
+    from mimi_hip.model import MimiHipModel
+    from oracle import mimi_ref
+    t = np.arange(16000) / 16000.0
+    pcm = (8000 * np.sin(2 * np.pi * 180 * t) * (0.6 + 0.4 * np.sin(2 * np.pi * 3 * t))
+           + np.random.default_rng(5).normal(0, 300, t.size)).astype(np.int16)
     p = str(tmp_path / "a.wav")
     _write_wav(p, pcm, 16000, 2)
     y, sr = ingest.load(p, sr=24000, device="cuda:0")
-    assert sr == 24000 and len(y) == 72000
-    assert bits_equal(y, librosa_polyphase_ref(pcm.astype(np.float32) / 32768.0, 16000, 24000))
+    want = librosa_polyphase_ref(pcm.astype(np.float32) / 32768.0, 16000, 24000)
+    assert sr == 24000 and len(y) == 24000 and bits_equal(y, want)
+    enc = MimiEncoder(device="cuda:0", model=MimiHipModel(state_dict, device="cuda:0"))
+    codes = enc.encode_audio_chunk(y, 24000)
+    ref = mimi_ref.encode(torch.from_numpy(want)[None, None], state_dict, 32)[0].numpy()
+    assert codes.shape == ref.shape == (32, 13)
+    assert (codes == ref).mean() > 0.99, (codes == ref).mean()
 
 
 @pytest.mark.gpu
