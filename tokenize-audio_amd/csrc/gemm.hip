@@ -161,8 +161,20 @@ static bool pair_ok(const GemmArgs& a) {
 // fp16 down convs: 256x128 tiles, tap-pair stages (2 x 67.6 KiB), A's LDS-DMA halved, issued by 4 loader
 // waves beside the 8 compute waves: -4..-15 % against the 3-stage ring without loaders
 // (profiles/r1j_gemm_bench_pair.log, r1j_gemm_bench_ld.log)
+// Small grids (a batch of 1-4 utterances): when the default tile leaves fewer than kSmallGrid workgroups, the
+// fp16 GEMMs switch to 64-row tiles of the SAME kernel family -- same MFMA shape (16x16x32), K step, K order,
+// tap pairing and epilogue -- so every output element is produced by the identical instruction sequence and an
+// utterance's codes do not depend on the batch it is encoded in (test_full_size_batch_properties compares B = 1
+// against B = 32 bitwise).
+constexpr long long kSmallGrid = 128;
+static long long tiles(const GemmArgs& a, int bm, int bn) {
+    return (long long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn) * a.batch;
+}
+
 template <int EPI, int OUTP, int TAG>
 static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
+    if (pair_ok(a) && tiles(a, 256, 128) < kSmallGrid)
+        return run_planes<64, 64, 2, 2, 2, 2, EPI, OUTP, TAG, 0, 32, 16, FL_PAIR, true>(a, s);
     if (pair_ok(a)) return run_planes<256, 128, 4, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR, true>(a, s);
     return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP, TAG, 0, 32, 16, 0, true>(a, s);
 }
@@ -171,6 +183,33 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
     const int prec = g_prec;
     if (prec != PREC_BF16X6 && prec != PREC_BF16X3 && prec != PREC_F16X3) return hipErrorInvalidValue;
     if (prec == PREC_F16X3) {
+        switch (role) {
+            case ROLE_FINAL:
+                if (tiles(a, 128, 128) < kSmallGrid)
+                    return run_planes<64, 64, 2, 2, 2, 4, EPI_BIAS_OUT, 0, 4, 0, 32, 16, 0, true>(a, s);
+                break;
+            case ROLE_QKV:  // (RoPE pairs need 4 column tiles per wave: 64 x 128)
+                if (tiles(a, 128, 128) < kSmallGrid)
+                    return run_planes<64, 128, 2, 2, 2, 4, EPI_ROPE, 0, 5, 0, 32, 16, 0, true>(a, s);
+                break;
+            case ROLE_OPROJ:
+                if (tiles(a, 128, 128) < kSmallGrid)
+                    return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 0, 6, 0, 32, 16, 0, true>(a, s);
+                break;
+            case ROLE_FC1:
+                if (tiles(a, 256, 256) < kSmallGrid)
+                    return run_planes<64, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 0, 32, 16, 0, true>(a, s);
+                break;
+            case ROLE_FC2:
+                if (tiles(a, 128, 128) < kSmallGrid)
+                    return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 0, 8, 0, 32, 16, 0, true>(a, s);
+                break;
+            case ROLE_RES3P:
+                if (tiles(a, 256, 128) < kSmallGrid)
+                    return run_planes<64, 64, 2, 2, 2, 3, EPI_BIAS_ELU, 2, 12, 0, 32, 16, 0, true>(a, s);
+                break;
+            default: break;
+        }
         switch (role) {
             case ROLE_DOWN: return run_planes_down_h16<EPI_BIAS, 0, 2>(a, s);
             case ROLE_DOWN_ELU: return run_planes_down_h16<EPI_BIAS_ELU, 2, 3>(a, s);
@@ -213,7 +252,10 @@ static hipError_t dispatch(int role, const GemmArgs& a, hipStream_t s) {
         case ROLE_OPROJ: return run_prec<false, PAD_ZERO, EPI_SCALE_RES, 6>(a, s, g_prec);
         case ROLE_FC1: return run_prec<false, PAD_ZERO, EPI_GELU, 7>(a, s, g_prec);
         case ROLE_FC2: return run_prec<false, PAD_ZERO, EPI_SCALE_RES, 8>(a, s, g_prec);
-        case ROLE_DOWNSAMPLE: return run_prec<false, PAD_REPLICATE, EPI_NONE, 9>(a, s, g_prec);
+        case ROLE_DOWNSAMPLE:  // small grids: 64x64 tiles, same 32x32 MFMA sequence per output (see kSmallGrid)
+            if ((g_prec == PREC_BF16X6 || g_prec == PREC_F16X3) && tiles(a, 128, 128) < kSmallGrid)
+                return run_split<64, 64, 1, 2, 3, false, PAD_REPLICATE, EPI_NONE, 9>(a, s);
+            return run_prec<false, PAD_REPLICATE, EPI_NONE, 9>(a, s, g_prec);
         case ROLE_INPROJ: return run_auto<false, PAD_ZERO, EPI_NONE, 10>(a, s);
         default: return hipErrorInvalidValue;
     }

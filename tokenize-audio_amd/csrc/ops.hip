@@ -791,9 +791,12 @@ __device__ __forceinline__ int rvq_merge(const RvqWork& w, int L, long long f, i
     return (ix < 0 || ix >= ncodes) ? 0 : ix;
 }
 
-template <int D>
+// FT: frames per workgroup -- RVQ_FT, or 32 for small batches (more workgroups; the work layout stays padded
+// to RVQ_FT, and each (frame, code) distance is the same fmaf chain either way)
+template <int D, int FT>
 __global__ __launch_bounds__(512) void rvq_level_kernel(RvqArgs p, int L) {
-    constexpr int FT = RVQ_FT, LDH = D / 2 + 4;
+    constexpr int LDH = D / 2 + 4;
+    static_assert(FT % 32 == 0 && RVQ_FT % FT == 0, "frame tile");
     constexpr int NSL = 2048 / RVQ_CS;
     __shared__ __attribute__((aligned(16))) float img[2][FT][LDH];  // -2 r, split by k parity
     __shared__ float xn[FT];
@@ -938,9 +941,15 @@ __global__ __launch_bounds__(256) void rvq_final_kernel(RvqArgs p, int L) {
 hipError_t launch_rvq(const RvqArgs& a, hipStream_t s) {
     if (a.D != 256 || a.ncodes != 2048 || !a.work) return hipErrorInvalidValue;
     if (a.frames <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((a.frames + RVQ_FT - 1) / RVQ_FT), 2048 / RVQ_CS);
+    // small batches (fewer 64-frame workgroups than CUs, B < 16 x 10 s): 32-frame tiles
+    const bool small = (a.frames + RVQ_FT - 1) / RVQ_FT * (2048 / RVQ_CS) < 256;
+    const int ft = small ? 32 : RVQ_FT;
+    const dim3 grid((unsigned)((a.frames + ft - 1) / ft), 2048 / RVQ_CS);
     for (int L = 0; L < a.levels; ++L) {
-        hipLaunchKernelGGL((rvq_level_kernel<256>), grid, dim3(512), 0, s, a, L);
+        if (small)
+            hipLaunchKernelGGL((rvq_level_kernel<256, 32>), grid, dim3(512), 0, s, a, L);
+        else
+            hipLaunchKernelGGL((rvq_level_kernel<256, RVQ_FT>), grid, dim3(512), 0, s, a, L);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
