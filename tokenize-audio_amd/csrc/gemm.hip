@@ -174,7 +174,7 @@ static long long tiles(const GemmArgs& a, int bm, int bn) {
 template <int EPI, int OUTP, int TAG>
 static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
     if (pair_ok(a) && tiles(a, 256, 128) < kSmallGrid)
-        return run_planes<64, 64, 2, 2, 2, 2, EPI, OUTP, TAG, 0, 32, 16, FL_PAIR, true>(a, s);
+        return run_planes<64, 64, 2, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR, true>(a, s);
     if (pair_ok(a)) return run_planes<256, 128, 4, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR, true>(a, s);
     return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP, TAG, 0, 32, 16, 0, true>(a, s);
 }
@@ -186,27 +186,27 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         switch (role) {
             case ROLE_FINAL:
                 if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 4, EPI_BIAS_OUT, 0, 4, 0, 32, 16, 0, true>(a, s);
+                    return run_planes<64, 64, 2, 2, 2, 4, EPI_BIAS_OUT, 0, 4, 4, 32, 16, 0, true>(a, s);
                 break;
             case ROLE_QKV:  // (RoPE pairs need 4 column tiles per wave: 64 x 128)
                 if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 128, 2, 2, 2, 4, EPI_ROPE, 0, 5, 0, 32, 16, 0, true>(a, s);
+                    return run_planes<64, 128, 2, 2, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, 0, true>(a, s);
                 break;
             case ROLE_OPROJ:
                 if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 0, 6, 0, 32, 16, 0, true>(a, s);
+                    return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 0, 6, 4, 32, 16, 0, true>(a, s);
                 break;
             case ROLE_FC1:
                 if (tiles(a, 256, 256) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 0, 32, 16, 0, true>(a, s);
+                    return run_planes<64, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, 0, true>(a, s);
                 break;
             case ROLE_FC2:
                 if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 0, 8, 0, 32, 16, 0, true>(a, s);
+                    return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 0, 8, 4, 32, 16, 0, true>(a, s);
                 break;
             case ROLE_RES3P:
                 if (tiles(a, 256, 128) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 3, EPI_BIAS_ELU, 2, 12, 0, 32, 16, 0, true>(a, s);
+                    return run_planes<64, 64, 2, 2, 2, 3, EPI_BIAS_ELU, 2, 12, 4, 32, 16, 0, true>(a, s);
                 break;
             default: break;
         }
