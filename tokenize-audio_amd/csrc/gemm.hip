@@ -231,8 +231,9 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         case ROLE_DOWN_XE: return run_planes_big<EPI_BIAS, 3 | 8, 2 | 8, 11>(a, s, prec);
         case ROLE_RES3P: return run_planes_big<EPI_BIAS_ELU, 3, 2, 12>(a, s, prec);
         case ROLE_RES1P:  // K = C/2 = 128 / 256: short K, output-heavy -> 74 KiB tiles, two workgroups per CU
-            if (prec == PREC_F16X3)
-                return run_planes<128, 64, 2, 2, 2, 3, EPI_BIAS_RES_ELU, 2, 13, 0, 32, 16, 0, true>(a, s);
+            if (prec == PREC_F16X3)  // fp16: a 2-stage ring (48 KiB, three workgroups per CU): -10..-14 % vs 3
+                                     // stages, 4 loader waves or 64x64 tiles (profiles/r1l_ab_small_kernels.txt)
+                return run_planes<128, 64, 2, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13, 0, 32, 16, 0, true>(a, s);
             if (prec == PREC_BF16X6) return run_planes<128, 64, 2, 2, 3, 2, EPI_BIAS_RES_ELU, 3, 13>(a, s);
             return run_planes<128, 64, 2, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13>(a, s);
         default: return hipErrorInvalidValue;
