@@ -205,7 +205,7 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
                     return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 0, 8, 4, 32, 16, 0, true>(a, s);
                 break;
             case ROLE_RES3P:
-                if (tiles(a, 256, 128) < kSmallGrid)
+                if (tiles(a, 128, 128) < kSmallGrid)
                     return run_planes<64, 64, 2, 2, 2, 3, EPI_BIAS_ELU, 2, 12, 4, 32, 16, 0, true>(a, s);
                 break;
             default: break;
@@ -221,7 +221,9 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         case ROLE_DOWN: return run_planes_big<EPI_BIAS, 0, 0, 2>(a, s, prec);
         case ROLE_DOWN_ELU: return run_planes_big_ld<EPI_BIAS_ELU, 3, 2, 3>(a, s, prec);  // planes out: final conv
         case ROLE_FINAL: return run_planes_small_ld<EPI_BIAS_OUT, 4>(a, s, prec);
-        case ROLE_QKV: return run_planes_small<EPI_ROPE, 5>(a, s, prec);  // (256x256: -11 % alone, 0 in the engine)
+        case ROLE_QKV:  // fp16: a 2-stage ring, -10 % vs 4 stages (profiles/r1l_ab_small_kernels.txt)
+            if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 2, EPI_ROPE, 0, 5, 0, 32, 16, 0, true>(a, s);
+            return run_planes_small<EPI_ROPE, 5>(a, s, prec);  // (256x256: -11 % alone, 0 in the engine)
         case ROLE_OPROJ: return run_planes_small_ld<EPI_SCALE_RES, 6>(a, s, prec);
         case ROLE_FC1:  // planes out: fc2; fp16: 256x256 tiles (epilogue in 2 column passes), -8..-11 %
                         // (profiles/r1j_gemm_bench_256.log)
@@ -229,7 +231,9 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
             return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);
         case ROLE_FC2: return run_planes_small_ld<EPI_SCALE_RES, 8>(a, s, prec);
         case ROLE_DOWN_XE: return run_planes_big<EPI_BIAS, 3 | 8, 2 | 8, 11>(a, s, prec);
-        case ROLE_RES3P: return run_planes_big<EPI_BIAS_ELU, 3, 2, 12>(a, s, prec);
+        case ROLE_RES3P:  // fp16: 128x128 on a 2-stage ring (two workgroups per CU), -4 % vs 256x128 x 3
+            if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 2, EPI_BIAS_ELU, 2, 12, 0, 32, 16, 0, true>(a, s);
+            return run_planes_big<EPI_BIAS_ELU, 3, 2, 12>(a, s, prec);
         case ROLE_RES1P:  // K = C/2 = 128 / 256: short K, output-heavy -> 74 KiB tiles, two workgroups per CU
             if (prec == PREC_F16X3)  // fp16: a 2-stage ring (48 KiB, three workgroups per CU): -10..-14 % vs 3
                                      // stages, 4 loader waves or 64x64 tiles (profiles/r1l_ab_small_kernels.txt)
