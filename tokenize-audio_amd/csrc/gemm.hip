@@ -110,7 +110,8 @@ static hipError_t run_planes_small(const GemmArgs& a, hipStream_t s, int prec) {
 }
 template <int EPI, int TAG>
 static hipError_t run_planes_small_ld(const GemmArgs& a, hipStream_t s, int prec) {
-    if (prec == PREC_F16X3) return run_planes<128, 128, 2, 2, 2, 4, EPI, 0, TAG, 4, 32, 16, 0, true>(a, s);
+    // fp16: 3 stages (o_proj / fc2 -2 %, final conv equal vs 4; profiles/r1l_ab_small_kernels.txt)
+    if (prec == PREC_F16X3) return run_planes<128, 128, 2, 2, 2, 3, EPI, 0, TAG, 4, 32, 16, 0, true>(a, s);
     if (prec == PREC_BF16X6) return run_planes<128, 128, 2, 2, 3, 3, EPI, 0, TAG, 4>(a, s);
     return run_planes<128, 128, 2, 2, 2, 3, EPI, 0, TAG, 4>(a, s);
 }
