@@ -198,7 +198,7 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
                     return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 0, 6, 4, 32, 16, 0, true>(a, s);
                 break;
             case ROLE_FC1:
-                if (tiles(a, 256, 256) < kSmallGrid)
+                if (tiles(a, 128, 128) < kSmallGrid)
                     return run_planes<64, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, 0, true>(a, s);
                 break;
             case ROLE_FC2:
@@ -226,9 +226,10 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
             if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 2, EPI_ROPE, 0, 5, 0, 32, 16, 0, true>(a, s);
             return run_planes_small<EPI_ROPE, 5>(a, s, prec);  // (256x256: -11 % alone, 0 in the engine)
         case ROLE_OPROJ: return run_planes_small_ld<EPI_SCALE_RES, 6>(a, s, prec);
-        case ROLE_FC1:  // planes out: fc2; fp16: 256x256 tiles (epilogue in 2 column passes), -8..-11 %
-                        // (profiles/r1j_gemm_bench_256.log)
-            if (prec == PREC_F16X3) return run_planes<256, 256, 4, 2, 2, 2, EPI_GELU, 2, 7, 0, 32, 16, 0, true>(a, s);
+        case ROLE_FC1:  // planes out: fc2; fp16: 128x128 on a 2-stage ring (two workgroups per CU): -4 % vs
+                        // 256x256 x 2 stages, which beat 256x128 x 3 by 8-11 % (profiles/r1j_gemm_bench_256.log,
+                        // r1l_ab_small_kernels.txt)
+            if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 2, EPI_GELU, 2, 7, 0, 32, 16, 0, true>(a, s);
             return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);
         case ROLE_FC2: return run_planes_small_ld<EPI_SCALE_RES, 8>(a, s, prec);
         case ROLE_DOWN_XE: return run_planes_big<EPI_BIAS, 3 | 8, 2 | 8, 11>(a, s, prec);
