@@ -1,22 +1,37 @@
 """Throughput of the Mimi encode hot path on MI355X: audio-seconds encoded per wall-second (K = 8, 24 kHz).
 
-    python bench.py [--gpus N --steps K --warmup W --batch B --seconds S]
+    python bench.py [--gpus N --steps K --warmup W --batch B --seconds S --workload batch|yodas2|mls]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Workload (BASELINE.json configs[1]): one step = one ``mimi_encode`` of a batch of B = 32 synthetic 10 s /
-24 kHz clips (speech-like, seeded) already resident in HBM, K = 8 codebooks, weights = the seeded synthetic
-kyutai/mimi-shaped checkpoint (random init; throughput does not depend on values).  Multi-GPU: one process
-per GPU, each encodes its own batches (utterance round-robin, no data-path collective: SURVEY.md §8e);
-per-GPU work is fixed as N grows ("weak").  The timed region is bracketed by barrier + synchronize; the
-max over ranks is reported.  Rank 0 prints ONE JSON line.
+``--gpus N`` without torchrun's environment launches N ranks itself (``torch.distributed.run`` as a child
+process, started before anything touches the GPU) and exits with its status; under torchrun, WORLD_SIZE must
+equal ``--gpus``.
 
-roofline: per-kernel device time from HIP events recorded by the engine on its launch stream during the
-timed steps, aggregated per kernel symbol; the dominant kernel's algorithmic FLOPs / its time vs the MFMA
-peak of the arithmetic it runs on (see ``mfma_peak_for``).  cpu_baseline: the oracle (torch CPU restatement of MimiModel.encode) on a bounded sample.
+Workloads (one "step" each; per-GPU work is fixed as N grows: weak scaling):
+
+* ``batch`` (default, BASELINE.json configs[1], LibriTTS-R-style): one ``mimi_encode`` of B = 32 synthetic
+  10 s / 24 kHz clips already resident in HBM (``--batch 64`` = configs[2], Emilia).
+* ``yodas2`` (configs[3]): one ``MimiEncoder.encode_audio_batch`` of B mixed-length clips U[1.5, 20] s from
+  host memory -- feature extraction (pad to longest), host->device, encode, codes back to host, trim -- the
+  reference YODAS2 caller's batch path (``yodas2-mimi/process_shard.py:494-525``).  Clips are this rank's
+  round-robin share (``mimi_hip.sharding``).  value counts unpadded audio seconds.
+* ``mls`` (configs[4], encode part): B utterances U[10, 20] s, each through ``MimiEncoder.encode_audio_chunk``
+  (batch 1, as ``mls-en-mimi-pretrain/process_shard.py:302-307``), host->device and back included.
+
+Weights: the seeded synthetic kyutai/mimi-shaped checkpoint (random init; throughput does not depend on
+values).  The timed region is bracketed by barrier + synchronize; the max over ranks is reported.  Rank 0
+prints ONE JSON line.
+
+roofline: per-kernel device time from HIP events recorded by the engine on its launch stream during the timed
+steps, aggregated per kernel symbol; the dominant kernel's algorithmic FLOPs / its time vs the MFMA peak of the
+arithmetic it runs on (see ``mfma_peak_for``).  cpu_baseline: the oracle (torch CPU restatement of
+MimiModel.encode) on a bounded sample of the same workload.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,14 +44,20 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 MFMA/vector peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec
 BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak
 F16X3_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 3  # fp32-accurate products as 3 fp16 products
+DTYPE_LABEL = {
+    "f16x3": "f16x3 (fp32-emulating: 2 fp16 planes per operand, 3 products, fp32 accumulate; RVQ distances fp32)",
+    "bf16x6": "bf16x6 (fp32-emulating: 3 bf16 planes, 6 products, fp32 accumulate; RVQ distances fp32)",
+    "bf16x3": "bf16x3 (2 bf16 planes, 3 products, fp32 accumulate; RVQ distances fp32)",
+    "f32": "f32 (fp32 MFMA throughout)",
+}
 
 
 def mfma_peak_for(kernel: str):
     """Peak that bounds a GEMM kernel, in fp32-equivalent TFLOP/s of the algorithmic (fp32) FLOPs it does.
 
-    fp32 kernels run on v_mfma_f32_32x32x2_f32: 157.3 TF.  The split-bf16 kernels compute the same fp32 GEMM
-    as P bf16 products per fp32 multiply-add (NS = 3 planes -> 6 products, NS = 2 -> 3) on the dense bf16
-    MFMA, so their ceiling is 2.5 PF / P (416.7 TF for bf16x6, 833.3 TF for bf16x3)."""
+    fp32 kernels run on v_mfma_f32_32x32x2_f32: 157.3 TF.  The split kernels compute the same fp32 GEMM as P
+    16-bit products per fp32 multiply-add (NS = 3 bf16 planes -> 6 products, NS = 2 -> 3) on the dense
+    bf16/fp16 MFMA, so their ceiling is 2.5 PF / P (416.7 TF for bf16x6, 833.3 TF for f16x3 / bf16x3)."""
     if "gemm_bf16x_kernel<" in kernel or "gemm_planes_kernel<" in kernel:
         targs = [t.strip() for t in kernel.split("<", 1)[1].rstrip(">").split(",")]
         ns = int(targs[4])
@@ -54,46 +75,76 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=("batch", "yodas2", "mls"), default="batch")
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--seconds", type=float, default=10.0, help="clip length of the 'batch' workload")
     ap.add_argument("--num-quantizers", type=int, default=8)
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0,
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0,
                     help="wall budget of the CPU-baseline sample (0 disables)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0: this process's CPU affinity, capped by OMP_NUM_THREADS)")
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage events")
+    ap.add_argument("--no-f32-mode", action="store_true", help="skip the fp32-MFMA comparison run")
     ap.add_argument("--precision", default=None, help="GEMM precision mode (default: the engine's)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
 
-def cpu_baseline(seconds_budget: float, threads: int, clip_s: float):
-    """The oracle on the host cores: whole 10 s clips, batch 1 (config 1 of BASELINE.json), until the budget
-    is spent.  Returns the same metric (audio-s / wall-s)."""
+def self_launch(args) -> int:
+    """--gpus N > 1 outside torchrun: run torch.distributed.run as a child (this process never touched the
+    GPU) and return its exit status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_threads(requested: int) -> int:
+    if requested > 0:
+        return requested
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def cpu_baseline(seconds_budget: float, threads: int, clip_s: float, batch: int):
+    """The oracle on the host cores, same metric: whole clips at batch 1 (config 1 of BASELINE.json) and at the
+    GPU workload's batch, each on about half the budget.  ``value`` is the rate at the GPU's batch size."""
     import torch
 
     from mimi_hip import synthetic
     from oracle import mimi_ref
-    threads = max(1, min(threads, os.cpu_count() or 1))
     torch.set_num_threads(threads)
     sd = synthetic.make_state_dict(seed=0, num_quantizers=8)
     sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
     n = int(clip_s * 24000)
-    clip = torch.from_numpy(synthetic.speech_like(n, 0, 0))[None, None]
-    mimi_ref.encode(clip, sdt, 8)  # warm
-    done, t0 = 0, time.perf_counter()
-    while True:
-        mimi_ref.encode(clip, sdt, 8)
-        done += 1
-        el = time.perf_counter() - t0
-        if el >= seconds_budget or done >= 200:
-            break
+    rates = {}
+    for b in sorted({1, batch}):
+        clips = torch.from_numpy(synthetic.clip_batch(b, n, seed=0))[:, None]
+        mimi_ref.encode(clips[:1], sdt, 8)  # warm
+        done, t0 = 0, time.perf_counter()
+        while True:
+            mimi_ref.encode(clips, sdt, 8)
+            done += 1
+            el = time.perf_counter() - t0
+            if el >= seconds_budget / 2 or done >= 200:
+                break
+        rates[b] = (done * b * clip_s / el, done)
     try:
         cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:
         cpu_model = "unknown"
-    return {"value": round(done * clip_s / el, 3), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
-            "sample": f"{done} x {clip_s:g} s clips, batch 1, K=8, oracle/mimi_ref.py (torch {torch.__version__} CPU, "
-                      f"{threads} threads, {cpu_model})"}
+    sample = "; ".join(f"batch {b}: {d} encode(s) of {b} x {clip_s:g} s = {r:.1f} audio-s/s"
+                       for b, (r, d) in rates.items())
+    return {"value": round(rates[batch][0], 3), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
+            "sample": f"{sample}; K=8, oracle/mimi_ref.py (torch {torch.__version__} CPU, {threads} threads of "
+                      f"{len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else '?'} in this "
+                      f"process's affinity, {cpu_model})",
+            "batch1_value": round(rates[1][0], 3)}
 
 
 def pmc_lookup(pmc_kernels, name):
@@ -141,14 +192,127 @@ def north_star_groups(prof, steps, pmc_path):
     return out
 
 
+def roofline_from_profile(prof, steps):
+    per_kernel = {}
+    for stage, st in prof.items():
+        k = per_kernel.setdefault(st["kernel"], {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "launches": 0,
+                                                  "stages": []})
+        k["ms"] += st["ms"]
+        k["flops"] += st["flops"]
+        k["bytes"] += st["bytes"]
+        k["launches"] += st["launches"]
+        k["stages"].append(stage)
+    dom_name, dom = max(per_kernel.items(), key=lambda kv: kv[1]["ms"])
+    t_launch = dom["ms"] / 1000.0 / dom["launches"]
+    gemm_like = dom["flops"] > 0
+    if gemm_like:
+        achieved = dom["flops"] / dom["launches"] / t_launch / 1e12
+        peak, peak_note = mfma_peak_for(dom_name)
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "peak_basis": peak_note}
+    else:
+        achieved = dom["bytes"] / dom["launches"] / t_launch / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4)}
+    traffic, traffic_src = None, None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        k = pmc_lookup(pmc.get("kernels", {}), dom_name)
+        if "traffic_bytes" in k:
+            traffic = round(k["traffic_bytes"])
+            traffic_src = {"source": f"profiles/{pmc['tag']}_pmc_summary.json", "unit": "bytes per launch",
+                           "fetch_bytes": round(k["fetch_bytes"]), "write_bytes": round(k["write_bytes"])}
+    roof.update({"traffic": traffic, "traffic_detail": traffic_src, "kernel": dom_name, "stages": dom["stages"],
+                 "avg_launch_ms": round(1000 * t_launch, 4), "launches": dom["launches"],
+                 "algorithmic_per_launch": dom["flops"] / dom["launches"] if gemm_like
+                 else dom["bytes"] / dom["launches"]})
+    tot_ms = sum(v["ms"] for v in per_kernel.values())
+    tot_fl = sum(v["flops"] for v in per_kernel.values())
+    whole = {"device_ms_per_step": round(tot_ms / steps, 3),
+             "tflops_fp32_equivalent": round(tot_fl / (tot_ms / 1000) / 1e12, 2),
+             "frac_f16x3_peak": round(tot_fl / (tot_ms / 1000) / 1e12 / F16X3_PEAK_TFLOPS, 4)}
+    return roof, whole, pmc_path
+
+
+class Workload:
+    """One step of the selected workload on this rank; ``audio_seconds`` = unpadded audio per step."""
+
+    def __init__(self, args, model, dev, world, rank):
+        import numpy as np
+        import torch
+
+        from mimi_hip import synthetic
+        from mimi_hip.config import encoded_length
+        from mimi_hip.encoder import MimiEncoder
+        from mimi_hip.sharding import make_batches, shard_indices
+        self.kind = args.workload
+        K = args.num_quantizers
+        B = args.batch
+        if self.kind == "batch":
+            L = int(round(args.seconds * 24000))
+            # this rank's utterances: a distinct seeded slice of the shard (round-robin i -> rank i % N)
+            self.audio = torch.from_numpy(synthetic.clip_batch(B, L, seed=1000 + rank)).to(dev)
+            self.codes = torch.empty((B, K, encoded_length(L)), dtype=torch.int32, device=dev)
+            self.audio_seconds = B * args.seconds
+            self.host_audio = self.audio.cpu().pin_memory()
+            self.steps_clips = None
+
+            def step():
+                model.encode_int32(self.audio, K, out=self.codes)
+            self.step = step
+            self.desc = (f"LibriTTS-R-style batch encode (configs[{1 if B <= 32 else 2}]): batch={B} x "
+                         f"{args.seconds:g} s @ 24 kHz resident in HBM, K={K} codebooks, 1 encode per step per GPU")
+            return
+        enc = MimiEncoder(device=dev, model=model, num_quantizers=K)
+        lo, hi = (1.5, 20.0) if self.kind == "yodas2" else (10.0, 20.0)
+        n_steps = args.warmup + args.steps
+        # the whole shard's utterance list; this rank takes i % world == rank (sharding.py), in batches of B
+        n_total = world * B * n_steps
+        lengths = synthetic.random_lengths(n_total, lo, hi, seed=77)
+        mine = shard_indices(n_total, world, rank)
+        batches = make_batches(mine, B)
+        self.clips = [[synthetic.speech_like(lengths[i], 77, i) for i in b] for b in batches[:n_steps]]
+        self.step_seconds = [sum(len(a) for a in c) / 24000.0 for c in self.clips]
+        self.i = 0
+
+        if self.kind == "yodas2":
+            def step():
+                enc.encode_audio_batch(self.clips[self.i], 24000)
+                self.i += 1
+            self.desc = (f"YODAS2-style shard (configs[3]): batches of {B} mixed-length clips U[{lo:g}, {hi:g}] s "
+                         f"from host memory through MimiEncoder.encode_audio_batch (pad to longest, H2D, encode, "
+                         f"D2H, trim), K={K}, utterance round-robin over {world} GPU(s)")
+        else:
+            def step():
+                for a in self.clips[self.i]:
+                    enc.encode_audio_chunk(a, 24000)
+                self.i += 1
+            self.desc = (f"MLS-style stream (configs[4], encode part): {B} utterances U[{lo:g}, {hi:g}] s per step, "
+                         f"each through MimiEncoder.encode_audio_chunk (batch 1, H2D + D2H included), K={K}, "
+                         f"utterance round-robin over {world} GPU(s)")
+        self.step = step
+        self._np = np
+
+    def timed_seconds(self, first, count):
+        if self.kind == "batch":
+            return self.audio_seconds * count
+        return sum(self.step_seconds[first:first + count])
+
+
 def main():
     args = parse()
-    import numpy as np
-    import torch
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(self_launch(args))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -159,63 +323,47 @@ def main():
     torch.cuda.set_device(dev)
 
     from mimi_hip import synthetic
-    from mimi_hip.config import encoded_length
     from mimi_hip.model import MimiHipModel
 
     K = args.num_quantizers
-    B = args.batch
-    L = int(round(args.seconds * 24000))
     model = MimiHipModel(synthetic.make_state_dict(seed=0, num_quantizers=K), device=dev)
     if args.precision:
         model.set_precision(args.precision)
-    # this rank's utterances: a distinct seeded slice of the shard (round-robin i -> rank i % N)
-    audio = torch.from_numpy(synthetic.clip_batch(B, L, seed=1000 + rank)).to(dev)
-    codes = torch.empty((B, K, encoded_length(L)), dtype=torch.int32, device=dev)
-
-    def step():
-        model.encode_int32(audio, K, out=codes)
+    wl = Workload(args, model, dev, world, rank)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     for _ in range(args.warmup):
-        step()
+        wl.step()
     torch.cuda.synchronize()
-    if not args.no_profile:
+    profile = not args.no_profile and wl.kind == "batch"
+    if profile:
         model.profile_reset()
         model.set_profiling(True)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        wl.step()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
+    audio_s = wl.timed_seconds(args.warmup, args.steps)
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        t = torch.tensor([elapsed, audio_s], dtype=torch.float64, device=dev)
+        tmax = t[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed, audio_s = float(tmax.item()), float(t[1].item())
     prof = {}
-    if not args.no_profile:
+    if profile:
         model.set_profiling(False)
         prof = model.profile_read()
 
-    # PCIe-inclusive rate (host f32 in -> device codes -> host): reported beside, never as `value`
-    host_audio = audio.cpu().pin_memory()
-    torch.cuda.synchronize()
-    tp0 = time.perf_counter()
-    for _ in range(max(1, min(args.steps, 3))):
-        a = host_audio.to(dev, non_blocking=True)
-        c = model.encode_int32(a, K)
-        c.cpu()
-    torch.cuda.synchronize()
-    pcie_rate = max(1, min(args.steps, 3)) * B * args.seconds / (time.perf_counter() - tp0)
-
-    total_audio_s = world * B * args.seconds * args.steps
-    value = total_audio_s / elapsed
+    value = audio_s / elapsed
     result = {
         "metric": "audio-sec encoded/sec (Mimi 8-codebook, 24 kHz)",
         "value": round(value, 2),
@@ -227,61 +375,46 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": DTYPE_LABEL.get(model.precision, model.precision),
         "data": "synthetic (seeded speech-like 24 kHz clips; seeded random-init kyutai/mimi-shaped weights)",
-        "config": {"workload": f"LibriTTS-R-style batch encode: batch={B} x {args.seconds:g} s @ 24 kHz, "
-                               f"K={K} codebooks, 1 encode per step per GPU",
-                   "global_batch": world * B, "clip_seconds": args.seconds, "num_quantizers": K,
-                   "parallelism": f"utterance round-robin x{world} (no collective)",
+        "config": {"workload": wl.desc, "global_batch": world * args.batch,
+                   "clip_seconds": args.seconds if wl.kind == "batch" else "mixed",
+                   "num_quantizers": K, "parallelism": f"utterance round-robin x{world} (no collective)",
                    "gemm_precision": model.precision},
-        "pcie_inclusive_value": round(pcie_rate * world, 2),
     }
+    if wl.kind == "batch":
+        # PCIe-inclusive rate (host f32 in -> device codes -> host): reported beside, never as `value`
+        n = max(1, min(args.steps, 3))
+        torch.cuda.synchronize()
+        tp0 = time.perf_counter()
+        for _ in range(n):
+            a = wl.host_audio.to(dev, non_blocking=True)
+            model.encode_int32(a, K).cpu()
+        torch.cuda.synchronize()
+        result["pcie_inclusive_value"] = round(world * n * wl.audio_seconds / (time.perf_counter() - tp0), 2)
+        if not args.no_f32_mode and model.precision != "f32":
+            # the same workload on true fp32 MFMA arithmetic, for comparison with the split-precision number
+            prev = model.precision
+            model.set_precision("f32")
+            wl.step()
+            torch.cuda.synchronize()
+            n32 = max(1, min(args.steps, 5))
+            tf0 = time.perf_counter()
+            for _ in range(n32):
+                wl.step()
+            torch.cuda.synchronize()
+            result["f32_mode_value"] = round(world * n32 * wl.audio_seconds / (time.perf_counter() - tf0), 2)
+            model.set_precision(prev)
     if prof:
-        per_kernel = {}
-        for stage, st in prof.items():
-            k = per_kernel.setdefault(st["kernel"], {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "launches": 0,
-                                                      "stages": []})
-            k["ms"] += st["ms"]
-            k["flops"] += st["flops"]
-            k["bytes"] += st["bytes"]
-            k["launches"] += st["launches"]
-            k["stages"].append(stage)
-        dom_name, dom = max(per_kernel.items(), key=lambda kv: kv[1]["ms"])
-        t_launch = dom["ms"] / 1000.0 / dom["launches"]
-        gemm_like = dom["flops"] > 0
-        if gemm_like:
-            achieved = dom["flops"] / dom["launches"] / t_launch / 1e12
-            peak, peak_note = mfma_peak_for(dom_name)
-            roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 4), "peak_basis": peak_note}
-        else:
-            achieved = dom["bytes"] / dom["launches"] / t_launch / 1e9
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4)}
-        traffic, traffic_src = None, None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-        if os.path.exists(pmc_path):
-            with open(pmc_path) as f:
-                pmc = json.load(f)
-            k = pmc_lookup(pmc.get("kernels", {}), dom_name)
-            if "traffic_bytes" in k:
-                traffic = round(k["traffic_bytes"])
-                traffic_src = {"source": f"profiles/{pmc['tag']}_pmc_summary.json", "unit": "bytes per launch",
-                               "fetch_bytes": round(k["fetch_bytes"]), "write_bytes": round(k["write_bytes"])}
-        roof.update({"traffic": traffic, "traffic_detail": traffic_src, "kernel": dom_name, "stages": dom["stages"],
-                     "avg_launch_ms": round(1000 * t_launch, 4), "launches": dom["launches"],
-                     "algorithmic_per_launch": dom["flops"] / dom["launches"] if gemm_like
-                     else dom["bytes"] / dom["launches"]})
+        roof, whole, pmc_path = roofline_from_profile(prof, args.steps)
         result["roofline"] = roof
-        tot_ms = sum(v["ms"] for v in per_kernel.values())
-        tot_fl = sum(v["flops"] for v in per_kernel.values())
-        result["whole_encode"] = {"device_ms_per_step": round(tot_ms / args.steps, 3),
-                                  "tflops": round(tot_fl / (tot_ms / 1000) / 1e12, 2),
-                                  "frac_fp32_peak": round(tot_fl / (tot_ms / 1000) / 1e12 / FP32_PEAK_TFLOPS, 4)}
+        result["whole_encode"] = whole
         result["stages_ms_per_step"] = {s: round(v["ms"] / args.steps, 3) for s, v in prof.items()}
         result["north_star"] = north_star_groups(prof, args.steps, pmc_path)
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.cpu_threads, args.seconds)
+        cb_batch = args.batch if wl.kind == "batch" else 1
+        result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, cpu_threads(args.cpu_threads),
+                                              args.seconds if wl.kind == "batch" else 15.0, cb_batch)
     if rank == 0:
         line = json.dumps(result)
         print(line, flush=True)

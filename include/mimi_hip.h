@@ -110,18 +110,21 @@ int mimi_rvq_encode(mimi_engine* e, const float* dev_embedding, int64_t frames, 
  * Arithmetic of the conv / linear GEMMs (the residual VQ distances are always exact fp32):
  *   MIMI_PRECISION_F32     v_mfma_f32_32x32x2_f32 (fp32 MFMA)
  *   MIMI_PRECISION_BF16X6  fp32 emulated on the bf16 matrix cores: both operands split into 3 bf16 planes,
- *                          6 plane products accumulated in fp32 (default; ~fp32 accuracy, 2.7x MFMA rate)
+ *                          6 plane products accumulated in fp32 (~fp32 accuracy, 2.7x MFMA rate)
  *   MIMI_PRECISION_BF16X3  2 planes, 3 products (~1e-5 relative, 5.3x MFMA rate)
- *   MIMI_PRECISION_F16X3   fp32 emulated on the fp16 matrix cores: both operands split into 2 fp16 planes
- *                          (22-bit significand) with power-of-two scales, 3 products; the engine checks every
- *                          activation's range after the encode and re-runs it with corrected scales when a
- *                          tensor left fp16's window (so mimi_encode synchronises its stream in this mode)
+ *   MIMI_PRECISION_F16X3   (default) fp32 emulated on the fp16 matrix cores: both operands split into 2 fp16
+ *                          planes (22-bit significand) at power-of-two scales, 3 products.  Activation scales
+ *                          are fixed per tensor at mimi_finalize from a calibration encode (never from the
+ *                          caller's audio: an item's codes depend on its own samples and the padded length
+ *                          only).  mimi_encode reads the activations' maxima back after the encode (it
+ *                          synchronises its stream in this mode); on an overflow of a fixed scale each item is
+ *                          re-encoded alone, and in bf16x6 if it overflows alone.
  */
 enum { MIMI_PRECISION_F32 = 0, MIMI_PRECISION_BF16X6 = 1, MIMI_PRECISION_BF16X3 = 2, MIMI_PRECISION_F16X3 = 3 };
 /* default: MIMI_PRECISION_F16X3 */
 int mimi_set_precision(mimi_engine* e, int32_t mode);
 int mimi_get_precision(const mimi_engine* e);
-/* MIMI_PRECISION_F16X3: encodes re-run so far because an activation left fp16's window (diagnostic). */
+/* MIMI_PRECISION_F16X3: encodes that took the overflow fallback so far (diagnostic). */
 int64_t mimi_f16_reruns(const mimi_engine* e);
 
 /* Frames produced for `length` samples with the default config (reference float32 length math). */

@@ -83,3 +83,36 @@ def test_gloo_world2_matches_single_process_per_rank_batches():
         for b in sharding.make_batches(sharding.shard_indices(len(audio), 2, r), 2):
             exp.update(zip(b, fake.encode_audio_batch([audio[i] for i in b], 24000)))
     assert got == [exp[i].tolist() for i in range(len(audio))]
+
+
+@pytest.mark.gpu
+def test_sharded_real_engines_match_single(tmp_path):
+    """Two ranks, each with its own HIP engine (both on cuda:0 here), gloo group, DistributedMimiEncoder over the
+    real MimiEncoder: the merged codes equal one process encoding the same per-rank batches."""
+    import subprocess
+    import sys
+
+    import torch
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no HIP device")
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = tmp_path / "merged.npz"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", f"--master-port={_free_port()}", os.path.join(here, "shard_worker.py"), str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import shard_worker
+    from mimi_hip import synthetic
+    from mimi_hip.encoder import MimiEncoder
+    from mimi_hip.model import MimiHipModel
+    audio = shard_worker.clips()
+    model = MimiHipModel(synthetic.make_state_dict(seed=0), device="cuda:0")
+    enc = MimiEncoder(device="cuda:0", model=model)
+    exp = {}
+    for rank in range(2):
+        for b in sharding.make_batches(sharding.shard_indices(len(audio), 2, rank), shard_worker.BATCH):
+            exp.update(zip(b, enc.encode_audio_batch([audio[i] for i in b], 24000)))
+    model.close()
+    with np.load(out, allow_pickle=False) as z:
+        for i in range(len(audio)):
+            assert np.array_equal(z[f"c{i}"], exp[i]), i

@@ -204,20 +204,9 @@ struct mimi_engine {
     bool finalized = false;
     int levels_available = 0;
     int precision = PREC_F16X3;
-    // planes path: residual blocks of stages >= unfuse_from run as two plane GEMMs (k3 -> h planes, k1 + skip)
-    // instead of the fused fp32-MFMA kernel (MIMI_HIP_UNFUSE_FROM overrides; >= num_ratios disables)
-    int unfuse_from = 2;
-    // planes path: split-bf16 persistent fused block for C = 128 (MIMI_HIP_RES128_SPLIT=1).  Off by default: it
-    // is VALU/phase-bound at one workgroup per CU and measured 1.81 ms vs 1.69 ms for the fp32-MFMA fused
-    // kernel at B = 32 x 10 s (profiles/r1_ab_res128.txt)
-    bool res128_split = false;
-    // PREC_F16X3: stage 0 on the fp16-plane fused kernel (MIMI_HIP_RES0_H16=0 falls back to the fp32-MFMA one)
-    bool res0_h16_on = true;
-    bool res1_h16_on = true;  // MIMI_HIP_RES1_H16=0: stage 1 on the fp32-MFMA fused kernel
-    // PREC_F16X3: stage 0 (fused block + down conv) runs over chunks of s0_chunk utterances so the chunk's
-    // y planes (61 MB per 10 s utterance) are re-read from the 256 MiB Infinity Cache instead of HBM
-    // (MIMI_HIP_S0_CHUNK; 0 = whole batch)
-    int s0_chunk = 0;
+    // planes path: residual blocks of stages >= kUnfuseFrom run as two plane GEMMs (k3 -> h planes, k1 + skip);
+    // stages 0 and 1 run the fused fp16 blocks (resblock.hip)
+    static constexpr int kUnfuseFrom = 2;
 
     std::unordered_map<std::string, std::vector<float>> host_w;
     std::unordered_map<std::string, std::vector<int64_t>> expected;  // name -> shape
@@ -248,13 +237,20 @@ struct mimi_engine {
 
     hipEvent_t ws_free = nullptr;  // recorded at the end of every encode: the next one (any stream) waits on it
 
-    // PREC_F16X3 activation scales: plane-format tensor i of an encode (in launch order) is stored as fp16
-    // planes of x * act_scale[i]; its producer max-reduces |x| into amax_dev[i] (see f16_rescale)
+    // PREC_F16X3 activation scales (see "activation scales" above calibrate_scales): plane-format tensor `name`
+    // is stored as fp16 planes of x * act_scale[slot_of[name]], a power of two fixed at mimi_finalize from a
+    // calibration encode -- never from the caller's audio, so codes are a pure function of each item's input.
+    // Its producer max-reduces |x| into amax_dev[slot] for the overflow check.
+    std::map<std::string, int> slot_of;
     std::vector<float> act_scale;
+    bool calibrating = false;
+    bool uncalibrated_slot = false;  // an encode named a tensor the calibration did not see
     unsigned* amax_dev = nullptr;   // [kMaxActSlots][AMAX_SLOT_WORDS] sub-slots, then [kMaxActSlots] reduced
     unsigned* amax_red = nullptr;
     unsigned* amax_host = nullptr;  // pinned
-    int f16_reruns = 0;             // encodes re-run with corrected scales (diagnostic)
+    int32_t* item_codes = nullptr;  // one item's codes (per-item overflow fallback)
+    size_t item_codes_cap = 0;
+    int f16_reruns = 0;             // encodes that took the overflow fallback (diagnostic)
     bool profiling = false;
     std::vector<ProfEvent> pending;  // recorded since last read; first event of each encode named ""
     std::vector<hipEvent_t> event_pool;
@@ -272,9 +268,11 @@ struct mimi_engine {
 
 static int dev_alloc(mimi_engine* e, void** p, size_t bytes) {
     hipError_t err = hipMalloc(p, bytes);
-    if (err != hipSuccess)
+    if (err != hipSuccess) {
+        (void)hipGetLastError();
         return set_err(err == hipErrorOutOfMemory ? MIMI_ERR_OUT_OF_MEMORY : MIMI_ERR_HIP, "hipMalloc(%zu): %s",
                        bytes, hipGetErrorString(err));
+    }
     e->allocations.push_back(*p);
     return MIMI_OK;
 }
@@ -458,11 +456,6 @@ extern "C" int mimi_create(const mimi_config* cfg, int device, mimi_engine** out
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return set_err(MIMI_ERR_INVALID_ARGUMENT, "device %d of %d", device, ndev);
     e->device = device;
-    if (const char* uf = std::getenv("MIMI_HIP_UNFUSE_FROM")) e->unfuse_from = std::atoi(uf);
-    if (const char* rs = std::getenv("MIMI_HIP_RES128_SPLIT")) e->res128_split = std::atoi(rs) != 0;
-    if (const char* r0 = std::getenv("MIMI_HIP_RES0_H16")) e->res0_h16_on = std::atoi(r0) != 0;
-    if (const char* r1 = std::getenv("MIMI_HIP_RES1_H16")) e->res1_h16_on = std::atoi(r1) != 0;
-    if (const char* sc = std::getenv("MIMI_HIP_S0_CHUNK")) e->s0_chunk = std::atoi(sc);
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipEventCreateWithFlags(&e->ws_free, hipEventDisableTiming));
     HIP_TRY(hipMalloc(&e->amax_dev, ((size_t)kMaxActSlots * AMAX_SLOT_WORDS + kMaxActSlots) * sizeof(unsigned)));
@@ -820,6 +813,8 @@ static float torch_sqsum_host(const float* r, int D) {
     return tot;
 }
 
+static int calibrate_scales(mimi_engine* e);
+
 extern "C" int mimi_finalize(mimi_engine* e) {
     if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
     std::lock_guard<std::mutex> lk(e->mu);
@@ -931,6 +926,7 @@ extern "C" int mimi_finalize(mimi_engine* e) {
         return rc;
     e->levels_available = L;
     e->host_w.clear();
+    if ((rc = calibrate_scales(e))) return rc;
     e->finalized = true;
     return MIMI_OK;
 }
@@ -974,7 +970,7 @@ static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspa
         // x at stage 0 only holds the conv0 tap (the stage-0 block recomputes conv0 from the audio)
         if (s > 0 || e->taps) xmax = std::max(xmax, (size_t)p.T[s] * C);
         ymax = std::max(ymax, (size_t)p.T[s] * C);
-        if (ns && s >= e->unfuse_from && s > 0) xemax = std::max(xemax, (size_t)p.T[s] * C);
+        if (ns && s >= mimi_engine::kUnfuseFrom && s > 0) xemax = std::max(xemax, (size_t)p.T[s] * C);
         C *= 2;
     }
     xmax = std::max(xmax, act((size_t)p.T[c.num_ratios] * C));  // last down conv's (planes) output
@@ -1017,6 +1013,7 @@ static int ensure_ws(mimi_engine* e, size_t bytes, hipStream_t s) {
     }
     hipError_t err = hipMalloc(&e->ws, bytes);
     if (err != hipSuccess) {
+        (void)hipGetLastError();  // clear it: the launch checks (hipGetLastError) must not see this failure
         e->ws = nullptr;
         return set_err(err == hipErrorOutOfMemory ? MIMI_ERR_OUT_OF_MEMORY : MIMI_ERR_HIP,
                        "workspace hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(err));
@@ -1190,9 +1187,9 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     return MIMI_OK;
 }
 
-// One pass of the whole encode at precision prec (f16 mode: *nslots = the plane-format tensors written).
+// One pass of the whole encode at precision prec.
 static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s,
-                       int prec, int* nslots) {
+                       int prec) {
     const mimi_config& c = e->cfg;
     const StagePlan p = plan_lengths(c, L);
     Workspace w{};
@@ -1207,17 +1204,26 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         float scale = 0.0f;  // > 0: fp16 planes of x * scale
         unsigned* amax = nullptr;
     };
-    int nslot = 0;
-    auto new_act = [&]() {
+    // the activation-scale slot of plane tensor `name` (fixed names, so a tensor keeps its scale whatever the
+    // batch, length or code path); new names only while calibrating
+    auto new_act = [&](const std::string& name) {
         Act a;
-        if (!h16 || nslot >= kMaxActSlots) return a;
-        if ((int)e->act_scale.size() <= nslot) e->act_scale.resize(nslot + 1, 1.0f);
-        a.scale = e->act_scale[nslot];
-        a.amax = e->amax_dev + (size_t)nslot * AMAX_SLOT_WORDS;
-        ++nslot;
+        if (!h16) return a;
+        auto it = e->slot_of.find(name);
+        int slot;
+        if (it != e->slot_of.end()) {
+            slot = it->second;
+        } else {
+            if (!e->calibrating) e->uncalibrated_slot = true;
+            if ((int)e->slot_of.size() >= kMaxActSlots) return a;
+            slot = (int)e->slot_of.size();
+            e->slot_of[name] = slot;
+            e->act_scale.resize(slot + 1, 1.0f);
+        }
+        a.scale = e->act_scale[slot];
+        a.amax = e->amax_dev + (size_t)slot * AMAX_SLOT_WORDS;
         return a;
     };
-    if (h16 && nslots) *nslots = 0;
     // fp16 weight planes + 1 / (activation scale x weight scale) for a GEMM reading plane tensor `in`
     auto use_h = [&](GemmArgs& a, const void* wh, float wscale, const Act& in) {
         if (!h16) return;
@@ -1249,63 +1255,14 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     int C = c.num_filters;
     char nm[64];
     Act yact, xact, xeact, hact;  // the tensors currently held by y, x (last down conv), xe, h
-    int si0 = 0;
-    {
-        // stage 0 in utterance chunks (fp16 fused block + its down conv per chunk, same activation slots)
-        const int64_t T = p.T[0], T1 = p.T[1];
-        const int bc0 = e->s0_chunk;
-        if (bc0 > 0 && bc0 < B && h16 && ns && e->res0_h16 && e->res0_h16_on && !e->taps && c.num_ratios > 1 &&
-            1 < e->unfuse_from && (unsigned long long)B * (unsigned long long)((T + 31) / 32) < (1ull << 32)) {
-            yact = new_act();
-            const Act aa = new_act(), xa = new_act(), ha = new_act();
-            const double H = C / c.compress;
-            for (int b0 = 0; b0 < B; b0 += bc0) {
-                const int bc = std::min(bc0, B - b0);
-                ResArgs ra{};
-                ra.x = w.x;
-                ra.audio = audio + (long long)b0 * T;
-                ra.w0 = e->conv0.w;
-                ra.b0 = e->conv0.b;
-                ra.w3frag = e->res3[0].wfrag;
-                ra.w1frag = e->res1[0].wfrag;
-                ra.T = T;
-                ra.batch = bc;
-                ra.w3 = e->res3[0].w;
-                ra.b3 = e->res3[0].b;
-                ra.w1 = e->res1[0].w;
-                ra.b1 = e->res1[0].b;
-                ra.y = w.y;
-                ra.yp = w.y;
-                ra.y_pstride = (long long)bc * T * C;
-                ra.yns = ns;
-                ra.yscale = yact.scale;
-                ra.yamax = yact.amax;
-                ra.wh16 = e->res0_h16;
-                ra.ascale = aa.scale;
-                ra.xscale = xa.scale;
-                ra.hscale = ha.scale;
-                ra.unscale0 = 1.0f / (aa.scale * e->res0_wsc[0]);
-                ra.unscale1 = 1.0f / (xa.scale * e->res0_wsc[1]);
-                ra.unscale2 = 1.0f / (ha.scale * e->res0_wsc[2]);
-                ra.aamax = aa.amax;
-                ra.xamax = xa.amax;
-                ra.hamax = ha.amax;
-                LAUNCH_TRY(launch_resblock(C, ra, s, &kname), "resblock");
-                const double fl = 2.0 * bc * T * (3.0 * C * H + H * C) + 2.0 * bc * T * C * c.kernel_size;
-                rec.mark("res_s0", fl, (double)bc * T * 4 * (1 + C), kname);
-                GemmArgs ad = conv_args(e->down[0], w.y, T, w.x + (long long)b0 * T1 * 2 * C, T1, bc);
-                planes_in(ad, w.y, (long long)bc * T * C);
-                use_h(ad, e->down[0].wh, e->down[0].wscale, yact);
-                LAUNCH_TRY(launch_gemm(ROLE_DOWN, ad, s, &kname, prec), "down");
-                rec.mark("down_s0", gemm_flops(ad), gemm_bytes(ad, false), kname);
-            }
-            C *= 2;
-            si0 = 1;
-        }
-    }
-    for (int si = si0; si < c.num_ratios; ++si) {
+    const auto nmf = [](const char* fmt, int i) {
+        char b[48];
+        snprintf(b, sizeof b, fmt, i);
+        return std::string(b);
+    };
+    for (int si = 0; si < c.num_ratios; ++si) {
         const int64_t T = p.T[si];
-        const bool unf = ns && si > 0 && si >= e->unfuse_from;
+        const bool unf = ns && si > 0 && si >= mimi_engine::kUnfuseFrom;
         if (!unf) {
             ResArgs ra{};
             ra.x = w.x;
@@ -1326,13 +1283,17 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             ra.yp = w.y;
             ra.y_pstride = (long long)B * T * C;
             ra.yns = ns;
-            yact = new_act();
+            yact = new_act(nmf("y%d", si));
             ra.yscale = yact.scale;
             ra.yamax = yact.amax;
-            if (si == 0 && h16 && e->res0_h16 && e->res0_h16_on &&
-                (unsigned long long)B * (unsigned long long)((T + 31) / 32) < (1ull << 32)) {
+            if (h16 && (si > 1 || (si == 0 && !e->res0_h16) || (si == 1 && !(C == 128 && e->res1_h16))))
+                return set_err(MIMI_ERR_UNSUPPORTED, "f16x3: no fp16 fused block for stage %d", si);
+            if (h16 && (unsigned long long)B * (unsigned long long)((T + 31) / 32) >= (1ull << 32))
+                return set_err(MIMI_ERR_UNSUPPORTED, "f16x3: %d x %lld steps exceed the block index range", B,
+                               (long long)T);
+            if (si == 0 && h16) {
                 // fp16-plane stage-0 block: audio, ELU(x0) and ELU(h) are split in-kernel, each at its own scale
-                const Act aa = new_act(), xa = new_act(), ha = new_act();
+                const Act aa = new_act("s0.audio"), xa = new_act("s0.x"), ha = new_act("s0.h");
                 ra.wh16 = e->res0_h16;
                 ra.ascale = aa.scale;
                 ra.xscale = xa.scale;
@@ -1341,14 +1302,12 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                 ra.unscale1 = 1.0f / (xa.scale * e->res0_wsc[1]);
                 ra.unscale2 = 1.0f / (ha.scale * e->res0_wsc[2]);
                 ra.aamax = aa.amax;
-                if (const char* d = std::getenv("MIMI_HIP_DBG")) ra.dbg = std::atoi(d);
                 ra.xamax = xa.amax;
                 ra.hamax = ha.amax;
             }
-            if (si == 1 && C == 128 && h16 && e->res1_h16 && e->res1_h16_on &&
-                (unsigned long long)B * (unsigned long long)((T + 31) / 32) < (1ull << 32)) {
+            if (si == 1 && h16) {
                 // fp16-plane stage-1 block: ELU(x) and ELU(h) split in-kernel at their own scales
-                const Act xa = new_act(), ha = new_act();
+                const Act xa = new_act("s1.x"), ha = new_act("s1.h");
                 ra.wh16 = e->res1_h16;
                 ra.xscale = xa.scale;
                 ra.hscale = ha.scale;
@@ -1356,10 +1315,6 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                 ra.unscale2 = 1.0f / (ha.scale * e->res1_wsc[1]);
                 ra.xamax = xa.amax;
                 ra.hamax = ha.amax;
-            }
-            if (ns && !h16 && C == 128 && e->res128_split) {  // split-bf16 fused block (resblock.hip)
-                ra.w3s = e->res3[si].wsplit;
-                ra.w1s = e->res1[si].wsplit;
             }
             LAUNCH_TRY(launch_resblock(C, ra, s, &kname), "resblock");
             snprintf(nm, sizeof nm, "res_s%d", si);
@@ -1376,7 +1331,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             use_h(a3, e->res3[si].wh, e->res3[si].wscale, xeact);
             a3.Cp = w.h;
             a3.c_pstride = (long long)B * T * Hh;
-            hact = new_act();
+            hact = new_act(nmf("h%d", si));
             out_act(a3, hact);
             LAUNCH_TRY(launch_gemm(ROLE_RES3P, a3, s, &kname, prec), "res3");
             snprintf(nm, sizeof nm, "res3_s%d", si);
@@ -1387,7 +1342,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             a1.R = w.x;
             a1.Cp = w.y;
             a1.c_pstride = (long long)B * T * C;
-            yact = new_act();
+            yact = new_act(nmf("y%d", si));
             out_act(a1, yact);
             LAUNCH_TRY(launch_gemm(ROLE_RES1P, a1, s, &kname, prec), "res1");
             snprintf(nm, sizeof nm, "res1_s%d", si);
@@ -1396,7 +1351,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         snprintf(nm, sizeof nm, "res%d_elu", si);
         if ((rc = save_tap_planes(e, nm, w.y, ns, B, T, C, s, yact.scale))) return rc;
         const bool last = si == c.num_ratios - 1;
-        const bool next_unf = ns && !last && si + 1 >= e->unfuse_from;
+        const bool next_unf = ns && !last && si + 1 >= mimi_engine::kUnfuseFrom;
         GemmArgs ad = conv_args(e->down[si], w.y, T, w.x, p.T[si + 1], B);
         int role = last ? ROLE_DOWN_ELU : ROLE_DOWN;
         if (ns) {
@@ -1406,13 +1361,13 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                 ad.Cp = w.x;
                 ad.c_pstride = (long long)B * p.T[si + 1] * 2 * C;
                 ad.C = nullptr;
-                xact = new_act();
+                xact = new_act("x_last");
                 out_act(ad, xact);
             } else if (next_unf) {  // fp32 x (the skip) + ELU(x) planes (the next k3 conv's input)
                 ad.Cp = w.xe;
                 ad.c_pstride = (long long)B * p.T[si + 1] * 2 * C;
                 role = ROLE_DOWN_XE;
-                xeact = new_act();
+                xeact = new_act(nmf("xe%d", si + 1));
                 out_act(ad, xeact);
             }
         }
@@ -1442,7 +1397,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     for (int l = 0; l < c.num_hidden_layers; ++l) {
         const DevXfmr& x = e->xf[l];
         const long long nact = rows * Hd;
-        const Act t1a = new_act();
+        const Act t1a = new_act(nmf("xf%d.ln1", l));
         LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1a.scale,
                                     t1a.amax),
                    "ln1");
@@ -1459,7 +1414,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         use_h(aq, x.wqkv_h, x.wqkv_hs, t1a);
         LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, prec), "qkv");
         rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
-        const Act atta = new_act();
+        const Act atta = new_act(nmf("xf%d.att", l));
         LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh), s,
                                     w.att, nact, ns, atta.scale, atta.amax),
                    "attention");
@@ -1474,7 +1429,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         use_h(ao, x.wo_h, x.wo_hs, atta);
         LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
         rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
-        const Act t1b = new_act();
+        const Act t1b = new_act(nmf("xf%d.ln2", l));
         LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1b.scale,
                                     t1b.amax),
                    "ln2");
@@ -1488,7 +1443,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             a1.Cp = w.ff;  // only fc2 reads it: planes out
             a1.c_pstride = rows * c.intermediate_size;
             a1.C = nullptr;
-            ffa = new_act();
+            ffa = new_act(nmf("xf%d.ff", l));
             out_act(a1, ffa);
         }
         LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, prec), "fc1");
@@ -1518,46 +1473,151 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     if ((rc = save_tap(e, "proj", w.proj, B, T2, 2 * Dq, s))) return rc;
     if ((rc = run_rvq(e, w.proj, (int64_t)B * T2, K, codes, (int)T2, w.rvq, s, rec))) return rc;
     HIP_TRY(hipEventRecord(e->ws_free, s));
-    if (h16 && nslots) *nslots = nslot;
     return MIMI_OK;
 }
 
 // Activation scales (PREC_F16X3).  A plane tensor with max|x| = a stored at scale s keeps every element's full
-// 22-bit significand down to 2^-3 / s (h1 = fp16(x s - h0) normal) and an absolute error <= 2^-25 / s below,
-// i.e. <= 2^-22 a for all of it, as long as a s >= 2^-3; a s < 2^15 keeps x s (and h0) finite.  A tensor that
-// left [2^-3, 2^15) is re-centred at a s in [2^6, 2^7) and the encode re-run (the scales persist, so a shard of
-// similar audio re-runs only its first batch, if at all).  Non-finite or zero maxima are left alone (an
-// upstream overflow in this pass, or a NaN input the reference would propagate too).
-static bool f16_rescale(mimi_engine* e, int nslots) {
-    bool again = false;
-    for (int i = 0; i < nslots; ++i) {
-        float a;
-        std::memcpy(&a, &e->amax_host[i], 4);
-        if (!(a > 0.0f) || !std::isfinite(a)) continue;
-        const float as = a * e->act_scale[i];
-        if (as >= 32768.0f || as < 0.125f) {
-            e->act_scale[i] = std::ldexp(1.0f, 6 - std::ilogb(a));
-            again = true;
-        }
+// 22-bit significand down to 2^-3 / s (h1 = fp16(x s - h0) normal) and an absolute error <= 2^-25 / s below;
+// a s < 2^15 keeps x s (and h0) finite.  The scales are FIXED per tensor name: mimi_finalize runs a calibration
+// encode on three full-scale 10 s signals (calibrate_scales) and puts every tensor's calibration maximum at
+// a s in [2^7, 2^8).  They never follow the caller's audio, so an item's codes are a pure function of its own
+// samples and the padded length -- not of its batch-mates or of what the engine encoded before (the reference
+// is a pure function of the batch too, TF/modeling_mimi.py:1297-1386).  A tensor 2^7 x louder than the
+// calibration's loudest would overflow: every encode reads the per-tensor maxima back, and on an overflow each
+// item is re-encoded alone (at the same padded length) and, if it overflows alone, in the scale-free bf16x6
+// arithmetic -- so the fallback too depends on the item alone.  Quieter tensors need no action: their
+// absolute error stays <= 2^-25 / s = 2^-32..2^-33 of the calibration maximum.
+constexpr float kF16Overflow = 32768.0f;  // a s >= 2^15: x s may round to an fp16 infinity
+
+// folds and reads back the per-slot maxima of the last pass (synchronises s)
+static int read_amax(mimi_engine* e, hipStream_t s, int* n) {
+    const int ns = (int)e->slot_of.size();
+    *n = ns;
+    if (ns == 0) return MIMI_OK;
+    LAUNCH_TRY(launch_amax_reduce(e->amax_dev, ns, e->amax_red, s), "amax_reduce");
+    HIP_TRY(hipMemcpyAsync(e->amax_host, e->amax_red, ns * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return MIMI_OK;
+}
+
+static float slot_amax(const mimi_engine* e, int i) {
+    float a;
+    std::memcpy(&a, &e->amax_host[i], 4);
+    return a;
+}
+
+// one f16x3 pass and its overflow check.  Non-finite maxima are not overflows of the scale: they come from a
+// non-finite input, which the reference propagates too.
+static int f16_pass(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s,
+                    bool* overflow) {
+    *overflow = false;
+    HIP_TRY(hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), s));
+    int rc = encode_pass(e, audio, B, L, K, codes, s, PREC_F16X3);
+    if (rc) return rc;
+    if (e->uncalibrated_slot) return set_err(MIMI_ERR_STATE, "f16x3: an activation has no calibrated scale");
+    int n = 0;
+    if ((rc = read_amax(e, s, &n))) return rc;
+    for (int i = 0; i < n; ++i) {
+        const float a = slot_amax(e, i);
+        if (std::isfinite(a) && a * e->act_scale[i] >= kF16Overflow) *overflow = true;
     }
-    return again;
+    return MIMI_OK;
+}
+
+static int calibrate_scales(mimi_engine* e) {
+    const int B = 3;
+    const int64_t L = 240000;
+    std::vector<float> h((size_t)B * L);
+    uint64_t st = 0x243F6A8885A308D3ull;  // splitmix64
+    auto uni = [&]() {
+        uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+    };
+    const double fs = 24000.0, pi = 3.14159265358979323846;
+    float pk = 0.0f;
+    for (int64_t i = 0; i < L; ++i) {
+        const double t = i / fs;
+        h[i] = (float)(2.0 * uni() - 1.0);  // white noise, U[-1, 1]
+        // harmonic mix of a gliding 90..250 Hz fundamental under a 4 Hz syllable envelope
+        const double f0 = 170.0 + 80.0 * std::sin(2 * pi * 0.3 * t);
+        double v = 0.0;
+        for (int k = 1; k <= 12; ++k) v += std::sin(2 * pi * f0 * k * t + 0.7 * k) / k;
+        v *= 0.55 + 0.45 * std::sin(2 * pi * 4.0 * t);
+        h[L + i] = (float)v;
+        pk = std::max(pk, std::fabs(h[L + i]));
+        // logarithmic sine sweep 50 Hz -> 11 kHz over the clip, amplitude 1
+        const double T = L / fs, k = std::log(11000.0 / 50.0);
+        h[2 * L + i] = (float)std::sin(2 * pi * 50.0 * T / k * (std::exp(t / T * k) - 1.0));
+    }
+    for (int64_t i = 0; i < L; ++i) h[L + i] /= pk;
+    const int K = e->cfg.num_semantic_quantizers;
+    const int64_t T2 = plan_lengths(e->cfg, L).frames12;
+    float* d_audio = nullptr;
+    int32_t* d_codes = nullptr;
+    hipStream_t s = nullptr;
+    int rc = MIMI_OK;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    if (hipMalloc(&d_audio, h.size() * 4) != hipSuccess || hipMalloc(&d_codes, (size_t)B * K * T2 * 4) != hipSuccess) {
+        rc = set_err(MIMI_ERR_OUT_OF_MEMORY, "calibration buffers");
+    } else if (hipMemcpy(d_audio, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        rc = set_err(MIMI_ERR_HIP, "calibration upload");
+    }
+    e->calibrating = true;
+    for (int it = 0; rc == MIMI_OK && it < 8; ++it) {
+        if (hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), s) != hipSuccess) {
+            rc = set_err(MIMI_ERR_HIP, "calibration memset");
+            break;
+        }
+        int n = 0;
+        if ((rc = encode_pass(e, d_audio, B, L, K, d_codes, s, PREC_F16X3)) || (rc = read_amax(e, s, &n))) break;
+        bool changed = false;
+        for (int i = 0; i < n; ++i) {
+            const float a = slot_amax(e, i);
+            if (!(a > 0.0f) || !std::isfinite(a)) continue;
+            const float as = a * e->act_scale[i];
+            if (as < 64.0f || as >= 512.0f) {  // hysteresis band around the [2^7, 2^8) target
+                e->act_scale[i] = std::ldexp(1.0f, 7 - std::ilogb(a));
+                changed = true;
+            }
+        }
+        if (!changed) break;
+    }
+    e->calibrating = false;
+    (void)hipStreamSynchronize(s);
+    if (d_audio) (void)hipFree(d_audio);
+    if (d_codes) (void)hipFree(d_codes);
+    (void)hipStreamDestroy(s);
+    return rc;
 }
 
 static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s) {
-    int prec = e->precision;
-    for (int attempt = 0;; ++attempt) {
-        const bool h16 = prec == PREC_F16X3;
-        if (h16) HIP_TRY(hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), s));
-        int nslots = 0;
-        int rc = encode_pass(e, audio, B, L, K, codes, s, prec, &nslots);
-        if (rc || !h16 || nslots == 0) return rc;
-        LAUNCH_TRY(launch_amax_reduce(e->amax_dev, nslots, e->amax_red, s), "amax_reduce");
-        HIP_TRY(hipMemcpyAsync(e->amax_host, e->amax_red, nslots * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    const int prec = e->precision;
+    const StagePlan p = plan_lengths(e->cfg, L);
+    if (prec != PREC_F16X3 || act_planes(e, p, prec) != 2) return encode_pass(e, audio, B, L, K, codes, s, prec);
+    bool ovf = false;
+    int rc = f16_pass(e, audio, B, L, K, codes, s, &ovf);
+    if (rc || !ovf) return rc;
+    ++e->f16_reruns;
+    if (B == 1) return encode_pass(e, audio, 1, L, K, codes, s, PREC_BF16X6);
+    const size_t per = (size_t)K * p.frames12;
+    if (e->item_codes_cap < per) {
         HIP_TRY(hipStreamSynchronize(s));
-        if (!f16_rescale(e, nslots)) return MIMI_OK;
-        ++e->f16_reruns;
-        if (attempt >= 2) prec = PREC_BF16X6;  // scales still moving: finish this call in bf16x6
+        if (e->item_codes) HIP_TRY(hipFree(e->item_codes));
+        e->item_codes = nullptr;
+        e->item_codes_cap = 0;
+        HIP_TRY(hipMalloc(&e->item_codes, per * sizeof(int32_t)));
+        e->item_codes_cap = per;
     }
+    for (int b = 0; b < B; ++b) {
+        const float* ab = audio + (int64_t)b * L;
+        if ((rc = f16_pass(e, ab, 1, L, K, e->item_codes, s, &ovf))) return rc;
+        if (ovf && (rc = encode_pass(e, ab, 1, L, K, e->item_codes, s, PREC_BF16X6))) return rc;
+        HIP_TRY(hipMemcpyAsync(codes + b * per, e->item_codes, per * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    }
+    return MIMI_OK;
 }
 
 extern "C" int mimi_encode(mimi_engine* e, const float* audio, int32_t batch, int64_t length, int32_t K,
@@ -1581,6 +1641,7 @@ extern "C" int mimi_encode(mimi_engine* e, const float* audio, int32_t batch, in
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the HIP null stream, as in every HIP API
+    (void)hipGetLastError();  // a failure left by an unrelated earlier call must not fail this encode's launches
     return encode_locked(e, audio, batch, length, K, codes, s);
 }
 
@@ -1628,6 +1689,7 @@ extern "C" void mimi_destroy(mimi_engine* e) {
     if (e->ws_free) (void)hipEventDestroy(e->ws_free);
     if (e->amax_dev) (void)hipFree(e->amax_dev);
     if (e->amax_host) (void)hipHostFree(e->amax_host);
+    if (e->item_codes) (void)hipFree(e->item_codes);
     delete e;
 }
 

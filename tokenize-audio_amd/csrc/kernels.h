@@ -198,8 +198,6 @@ struct ResArgs {
     unsigned* yamax;
     const float* w3frag;  // optional: W3 / W1 in MFMA-fragment order [ntile][kquad][64 lanes][4] (stage 0)
     const float* w1frag;
-    const void* w3s;      // optional: W3 / W1 as 3 bf16 planes [3][N][K] (split-bf16 fused block, C = 128)
-    const void* w1s;
     // PREC_F16X3 fused block (stage 0: resblock0_h16_kernel): weights as 2 scaled fp16 planes in 32x32x16-MFMA
     // A-fragment order (layout in resblock.hip, built by engine.cpp make_res_h16).  The block's inputs and
     // internal operands are split in-kernel at power-of-two scales chosen by the engine; each one's max|v| is
@@ -208,7 +206,6 @@ struct ResArgs {
     float ascale, xscale, hscale;     // audio (conv0 input), ELU(x) (conv3 input), ELU(h) (conv1 input)
     float unscale0, unscale1, unscale2;
     unsigned *aamax, *xamax, *hamax;
-    int dbg;  // experiment flags (MIMI_HIP_DBG), 0 in production
 };
 hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** kname);
 

@@ -487,258 +487,6 @@ __global__ __launch_bounds__(256) void resblock0_wave_kernel(ResArgs p) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// C = 128 block on the split-bf16 matrix cores (planes path): fp32-level accuracy at ~2.7x the fp32-MFMA
-// rate.  Persistent: one workgroup per CU (143 KiB LDS) walks 128-row blocks; the NEXT block's x rows are
-// prefetched into registers while the current block computes, so the HBM phases hide under the MFMAs.
-// Per block, 4 waves:
-//   A  x (registers) -> ELU -> 3 bf16 planes: the slab [3][130][128] (rows m0-2 .. m0+127) in LDS
-//   B  h[128][64] = slab (*) W3 (K = 384 in 12 chunks of 32; W3 planes streamed by LDS-DMA through a
-//      3-deep ring with counted vmcnt and one barrier per chunk); each wave 32 rows x 64 cols
-//   C  h -> ELU(h + b3) -> planes over the dead slab; W1 planes [3][128][64] LDS-DMA'd beside it
-//   D  y[128][128] = h . W1^T (K = 64), each wave 64 x 64
-//   E  acc + b1 staged fp32, read back in the thread -> float4 map of A: y = ELU(x + (acc + b1)) with x
-//      still in registers, written as 3 bf16x4 planes (or fp32)
-// Swizzles: 64-B W3 rows at chunk c ^ ((row >> 2) & 3), 128-B W1 rows at c ^ ((row >> 1) & 7) (DMA source
-// side), padded 272-B slab rows / 144-B h rows: every ds_read_b128 quarter-wave hits 16 distinct 16-B slots.
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void resblock128_split_kernel(ResArgs p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    constexpr int C = 128, H = 64, BM = 128, NS = 3;
-    constexpr int RS = C + 8;             // slab row stride (bf16): 272 B
-    constexpr int SLABP = (BM + 2) * RS;  // per plane
-    constexpr int W3P = 64 * 32;          // W3 chunk plane image [64 n][32 k]
-    constexpr int W3STG = NS * W3P;
-    constexpr int RSH = H + 8;            // h row stride (bf16): 144 B
-    constexpr int HP = BM * RSH;
-    constexpr int W1P = C * H;            // W1 plane image [128 n][64 k], 128-B rows
-    constexpr int SLAB_ALL = NS * SLABP;
-    constexpr int NST = 3;                // W3 ring depth: chunk kc+1 in flight while kc is consumed
-    constexpr int LDE = 68;               // epilogue staging row stride (fp32)
-    __shared__ __attribute__((aligned(16))) __bf16 lds[SLAB_ALL + NST * W3STG];
-    static_assert(NS * HP + NS * W1P <= SLAB_ALL + NST * W3STG, "h + W1 fit the slab + ring");
-    static_assert(4 * 64 * LDE * 2 <= SLAB_ALL + NST * W3STG, "epilogue staging fits");
-    __bf16* slab = lds;
-    __bf16* ring = lds + SLAB_ALL;
-    __bf16* hpl = lds;            // after B
-    __bf16* w1l = lds + NS * HP;  // after B
-    float* stg = reinterpret_cast<float*>(lds);  // after D: [4 waves][64][LDE]
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int hsel = lane >> 5, l31 = lane & 31;
-    const long long T = p.T;
-    const long long nbt = (T + BM - 1) / BM;         // blocks per item
-    const long long nblk = nbt * p.batch;
-    const __bf16* __restrict__ w3s = reinterpret_cast<const __bf16*>(p.w3s);  // [3][64][384]
-    const __bf16* __restrict__ w1s = reinterpret_cast<const __bf16*>(p.w1s);  // [3][128][64]
-    const int wm = wave >> 1, wn = wave & 1;
-
-    // thread -> float4 map of a block: q-th float4 = block row (tid + 256q) >> 5, channels ((tid & 31) * 4)
-    // (+ halo rows m0-2, m0-1 for threads < 64)
-    constexpr int NQ = BM * (C / 4) / 256;  // 16
-    f32x4 xc[NQ], xn[NQ], hc = {0.f, 0.f, 0.f, 0.f}, hn = {0.f, 0.f, 0.f, 0.f};
-    // exactly NQ + 1 loads per lane, unconditional (clamped address, select): the counted vmcnt waits below
-    // rely on the count
-    auto load_block = [&](long long blk, f32x4 (&xr)[NQ], f32x4& hr) {
-        const long long bb = blk / nbt, m0 = (blk % nbt) * BM;
-        const float* xb = p.x + bb * T * C;
-        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int idx = tid + q * 256;
-            const long long pos = m0 + (idx >> 5);
-            const f32x4 t = *reinterpret_cast<const f32x4*>(xb + (pos < T ? pos : T - 1) * C + (idx & 31) * 4);
-            xr[q] = pos < T ? t : z;
-        }
-        const long long hp = m0 - 2 + ((tid >> 5) & 1);
-        const f32x4 t = *reinterpret_cast<const f32x4*>(xb + (hp >= 0 ? hp : 0) * C + (tid & 31) * 4);
-        hr = (tid < 64 && hp >= 0) ? t : z;
-    };
-    // W3 chunk kc -> ring stage st: 12 pieces of 16 rows x 64 B; wave w takes each plane's rows 16w..16w+15
-    auto issue_w3 = [&](int kc, int st) {
-        const int row = wave * 16 + (lane >> 2);
-        const int c = (lane & 3) ^ ((row >> 2) & 3);
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            const __bf16* src = w3s + ((long long)q * 64 + row) * (3 * C) + kc * 32 + c * 8;
-            __bf16* dst = ring + st * W3STG + q * W3P + wave * 16 * 32;
-            __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-        }
-    };
-    auto put_slab = [&](int srow, int c, f32x4 v) {
-        bf16x4 hp[NS];
-        split_bf16x4<NS>(elu4(v), hp);
-#pragma unroll
-        for (int pl = 0; pl < NS; ++pl) *reinterpret_cast<bf16x4*>(slab + pl * SLABP + srow * RS + c) = hp[pl];
-    };
-
-    long long blk = blockIdx.x;
-    if (blk < nblk) load_block(blk, xn, hn);
-    for (; blk < nblk; blk += gridDim.x) {
-        const long long bb = blk / nbt, m0 = (blk % nbt) * BM;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) xc[q] = xn[q];
-        hc = hn;
-        __syncthreads();  // the previous block's epilogue reads of the LDS are done
-        issue_w3(0, 0);
-        issue_w3(1, 1);
-        // ---- A: slab (rows with position >= T hold ELU(0) = 0: never read by a stored row)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int idx = tid + q * 256;
-            put_slab((idx >> 5) + 2, (idx & 31) * 4, xc[q]);
-        }
-        if (tid < 64) put_slab(tid >> 5, (tid & 31) * 4, hc);
-
-        // ---- B: h = slab (*) W3, wave rows 32w .. 32w+31, all 64 columns
-        f32x16 acc1[1][2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc1[0][j][r] = 0.f;
-        constexpr int KC = 3 * C / 32;  // 12
-        for (int kc = 0; kc < KC; ++kc) {
-            // retire chunk kc (and everything older, e.g. the previous block's stores)
-            if (kc + 1 < KC) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS) : "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();  // chunk kc landed for every wave; slab complete (kc = 0); stage (kc+2)%3 free
-            if (kc + 2 < KC) issue_w3(kc + 2, (kc + 2) % NST);
-            const __bf16* wst = ring + (kc % NST) * W3STG;
-            const int kk3 = (kc * 32) / C, ci0 = (kc * 32) % C;  // tap, channel base of this chunk
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-                bf16x8 af[NS][1], bf[NS][2];
-#pragma unroll
-                for (int pl = 0; pl < NS; ++pl) {
-                    const int i = wave * 32 + l31;
-                    af[pl][0] = *reinterpret_cast<const bf16x8*>(slab + pl * SLABP + (i + kk3) * RS + ci0 + kk * 16 +
-                                                                 8 * hsel);
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const int n = j * 32 + l31;
-                        const int phys = ((kk * 2 + hsel) ^ ((n >> 2) & 3)) * 8;
-                        bf[pl][j] = *reinterpret_cast<const bf16x8*>(wst + pl * W3P + n * 32 + phys);
-                    }
-                }
-                mma_split<NS, 1, 2>(acc1, af, bf);
-            }
-        }
-        __syncthreads();  // slab and ring are dead
-
-        // ---- C: W1 planes by LDS-DMA (48 pieces of 8 rows x 128 B; wave w: pieces w, w+4, ...), h planes
-#pragma unroll
-        for (int q = 0; q < 12; ++q) {
-            const int j = wave + q * 4;
-            const int pl = j / 16, rb = j % 16;
-            const int row = rb * 8 + (lane >> 3);
-            const int c = (lane & 7) ^ ((row >> 1) & 7);
-            const __bf16* src = w1s + ((long long)pl * C + row) * H + c * 8;
-            __bf16* dst = w1l + pl * W1P + rb * 8 * H;
-            __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0,
-                                             0);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int n = j * 32 + l31;
-            const float bias = p.b3[n];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
-                float v = elu_f(acc1[0][j][r] + bias);
-#pragma unroll
-                for (int pl = 0; pl < NS; ++pl) {
-                    const __bf16 hv = (__bf16)v;
-                    hpl[pl * HP + row * RSH + n] = hv;
-                    v = v - (float)hv;
-                }
-            }
-        }
-        // next block's x: issued after the W1 pieces, in flight under C .. E and the next slab build
-        const bool more = blk + gridDim.x < nblk;
-        if (more) {
-            load_block(blk + gridDim.x, xn, hn);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ + 1) : "memory");  // W1 landed; x may fly
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-
-        // ---- D: y = h . W1^T, wave (wm, wn) = 64 x 64 block
-        f32x16 acc2[2][2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc2[i][j][r] = 0.f;
-#pragma unroll
-        for (int kk = 0; kk < H / 16; ++kk) {
-            bf16x8 af[NS][2], bf[NS][2];
-#pragma unroll
-            for (int pl = 0; pl < NS; ++pl) {
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const int row = wm * 64 + i * 32 + l31;
-                    af[pl][i] = *reinterpret_cast<const bf16x8*>(hpl + pl * HP + row * RSH + kk * 16 + 8 * hsel);
-                }
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int n = wn * 64 + j * 32 + l31;
-                    const int phys = ((kk * 2 + hsel) ^ ((n >> 1) & 7)) * 8;
-                    bf[pl][j] = *reinterpret_cast<const bf16x8*>(w1l + pl * W1P + n * H + phys);
-                }
-            }
-            mma_split<NS, 2, 2>(acc2, af, bf);
-        }
-        __syncthreads();  // h / W1 dead: the epilogue staging reuses the LDS
-
-        // ---- E: stage acc + b1 per wave tile, read back in the A map, y = ELU(x + v)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const float bias = p.b1[wn * 64 + j * 32 + l31];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int lrow = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
-                    stg[(wave * 64 + lrow) * LDE + j * 32 + l31] = acc2[i][j][r] + bias;
-                }
-            }
-        __syncthreads();
-        const long long ybase = bb * T * C;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int idx = tid + q * 256;
-            const int r = idx >> 5, c = (idx & 31) * 4;
-            const long long row = m0 + r;
-            if (row >= T) continue;
-            const int wv = (r >> 6) * 2 + (c >> 6);
-            const f32x4 a = *reinterpret_cast<const f32x4*>(stg + (wv * 64 + (r & 63)) * LDE + (c & 63));
-            float y[4] = {elu_f(xc[q].x + a.x), elu_f(xc[q].y + a.y), elu_f(xc[q].z + a.z), elu_f(xc[q].w + a.w)};
-            const long long o = ybase + row * C + c;
-            if (p.yns == 0) {
-                *reinterpret_cast<f32x4*>(p.y + o) = f32x4{y[0], y[1], y[2], y[3]};
-            } else {
-                __bf16* dst = reinterpret_cast<__bf16*>(p.yp) + o;
-                for (int pl = 0; pl < p.yns; ++pl) {
-                    bf16x4 hv;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        hv[e] = (__bf16)y[e];
-                        y[e] = y[e] - (float)hv[e];
-                    }
-                    *reinterpret_cast<bf16x4*>(dst + pl * p.y_pstride) = hv;
-                }
-            }
-        }
-    }
-#endif
-}
-
-// ------------------------------------------------------------------------------------------------
 // Stage 0 on the fp16 matrix cores (PREC_F16X3): conv0 (1 -> 64, k7) + residual block (64 -> 32 -> 64) + ELU,
 // persistent and wave-autonomous.  Every operand is 2 fp16 planes at a power-of-two scale (x s = h0 + h1,
 // 22-bit significand) and each GEMM takes the 3 significant plane products, on v_mfma_f32_32x32x16_f16.
@@ -1014,7 +762,7 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
             }
         if (t0 + j < T) mxy = fmaxf(mxy, tmy);  // steps past the end are not stored, not in max|y|
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (!(p.dbg & 1)) {
+        {
             const int sr = lane >> 3, sc = (lane & 7) * 8;
 #pragma unroll
             for (int pl = 0; pl < 2; ++pl)
@@ -1300,18 +1048,6 @@ hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** 
                 (void)hipGetDevice(&dev);
                 (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
                 hipLaunchKernelGGL(resblock128_h16_kernel, dim3((unsigned)ncu), dim3(64 * r1h::NW), 0, s, a);
-                return hipGetLastError();
-            }
-            if (a.w3s && a.w1s) {
-                static const char* nm = "mimi::resblock128_split_kernel(mimi::ResArgs)";
-                if (kname) *kname = nm;
-                // persistent: one workgroup per CU (143 KiB of LDS) walks the 128-row blocks
-                int dev = 0, ncu = 256;
-                (void)hipGetDevice(&dev);
-                (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-                const long long nblk = (a.T + 127) / 128 * a.batch;
-                const unsigned grid = (unsigned)std::min<long long>(nblk, ncu);
-                hipLaunchKernelGGL(resblock128_split_kernel, dim3(grid), dim3(256), 0, s, a);
                 return hipGetLastError();
             }
             return run_res<128, 64, true, false, 2, 2, 2, 2, 128>(a, s, kname);

@@ -53,6 +53,19 @@ class MimiHipError(RuntimeError):
         super().__init__(f"{STATUS_NAMES.get(status, status)}: {message}")
 
 
+def _oom_base():
+    try:
+        import torch
+        return torch.cuda.OutOfMemoryError
+    except Exception:  # torch-less use of the binding
+        return MemoryError
+
+
+class MimiHipOutOfMemoryError(MimiHipError, _oom_base()):
+    """MIMI_ERR_OUT_OF_MEMORY.  Also a ``torch.cuda.OutOfMemoryError``, so a caller's OOM guard written for the
+    reference's torch encode (e.g. the YODAS2 long-chunk split, yodas2-mimi/process_shard.py:434-493) sees it."""
+
+
 _lib = None
 _lock = threading.Lock()
 
@@ -109,7 +122,8 @@ def load(path: Optional[str] = None):
 def check(status: int) -> None:
     if status != MIMI_OK:
         msg = load().mimi_last_error()
-        raise MimiHipError(status, msg.decode() if msg else "")
+        cls = MimiHipOutOfMemoryError if status == 3 else MimiHipError
+        raise cls(status, msg.decode() if msg else "")
 
 
 def default_config() -> MimiConfigC:

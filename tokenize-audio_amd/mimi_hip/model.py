@@ -221,7 +221,7 @@ class MimiHipModel:
 
     # ---- instrumentation ------------------------------------------------------------------------
     def set_precision(self, mode: str):
-        """'f16x3' (default: fp32 emulated on the fp16 matrix cores, 2 scaled planes with a range check),
+        """'f16x3' (default: fp32 emulated on the fp16 matrix cores, 2 planes at calibrated fixed scales),
         'bf16x6' (3 bf16 planes), 'f32' (fp32 MFMA) or 'bf16x3' (2 bf16 planes, ~1e-5)."""
         _lib.check(self._lib.mimi_set_precision(self._h, _lib.PRECISIONS[mode]))
 
@@ -232,7 +232,7 @@ class MimiHipModel:
 
     @property
     def f16_reruns(self) -> int:
-        """Encodes re-run with corrected activation scales (f16x3 mode)."""
+        """Encodes that took the f16x3 overflow fallback (per-item re-encode, bf16x6 where an item overflows)."""
         return int(self._lib.mimi_f16_reruns(self._h))
 
     def set_profiling(self, enable: bool = True):

@@ -72,8 +72,12 @@ class DistributedMimiEncoder:
         self.batch_size = batch_size
         self.sample_rate = sample_rate
         if encoder is None:
+            import torch
+
             from .encoder import MimiEncoder
             local = int(os.environ.get("LOCAL_RANK", "0"))
+            # the current device must be this rank's GPU: an nccl process group stages gather_object there
+            torch.cuda.set_device(local)
             encoder = MimiEncoder(model_id, device=f"cuda:{local}", num_quantizers=num_quantizers)
         self.encoder = encoder
 
