@@ -99,6 +99,18 @@ int mimi_encode(mimi_engine* e, const float* dev_audio, int32_t batch, int64_t l
                 int32_t num_quantizers, int32_t* dev_codes, void* stream);
 
 /*
+ * mimi_encode in two halves, for callers that overlap host work (ingest, H2D of the next batch, writing
+ * codes) with the encode: mimi_encode_async enqueues the encode on `stream` and returns a ticket without
+ * waiting; mimi_encode_wait(ticket) waits for it on the host and, in f16x3, applies the overflow check (and the
+ * per-item fallback when a fixed activation scale overflowed) before returning.  dev_codes is valid once the
+ * wait returns; dev_audio and dev_codes must stay allocated until then.  At most 16 encodes per engine may be
+ * in flight; each ticket is waited exactly once.  mimi_encode = mimi_encode_async + mimi_encode_wait.
+ */
+int mimi_encode_async(mimi_engine* e, const float* dev_audio, int32_t batch, int64_t length, int32_t num_quantizers,
+                      int32_t* dev_codes, void* stream, int64_t* ticket);
+int mimi_encode_wait(mimi_engine* e, int64_t ticket);
+
+/*
  * The quantizer alone: dev_embedding is the pre-quantizer embedding, device f32 [frames][hidden_size]
  * (frame-major, i.e. the reference's [B, 512, T] transposed to [B*T, 512]).  dev_codes: int32
  * [num_quantizers][frames].

@@ -421,3 +421,22 @@ def test_segmenter_on_engine(engine):
             same += int((c[:, :-1] == buck[cid][:, :-1]).sum())
             total += c[:, :-1].size
     assert total > 0 and same / total > 0.99, same / total
+
+
+def test_async_encode_tickets(engine, state_dict):
+    """mimi_encode_async / mimi_encode_wait: several encodes in flight give the synchronous codes; a ticket is
+    waited once; the f16x3 overflow fallback still applies when it is only checked at the wait."""
+    from mimi_hip import _lib
+    xs = [torch.from_numpy(synthetic.clip_batch(2, 24000 * (1 + i), seed=40 + i)).cuda() for i in range(5)]
+    ref = [engine.encode_int32(x, 8).cpu() for x in xs]
+    tickets = [engine.encode_async(x, 8) for x in xs]
+    got = [t.wait().cpu() for t in reversed(tickets)][::-1]  # waited out of order
+    assert all(torch.equal(a, b) for a, b in zip(got, ref))
+    with pytest.raises(_lib.MimiHipError):
+        _lib.check(engine._lib.mimi_encode_wait(engine._h, tickets[0]._ticket or 123456789))
+    loud = torch.from_numpy(synthetic.speech_like(48000, 5, 1) * np.float32(3e4))[None].cuda()
+    before = engine.f16_reruns
+    t = engine.encode_async(loud, 8)
+    c_async = t.wait().cpu()
+    assert engine.f16_reruns == before + 1
+    assert torch.equal(c_async, engine.encode_int32(loud, 8).cpu())

@@ -105,7 +105,7 @@ def test_wrapper_batch_semantics_match_reference(golden, state_dict):
     for i, o in enumerate(outs):
         ref = arrays[f"batch_item{i}"]
         assert o.shape == ref.shape and o.dtype == np.int64
-        assert (o == ref).mean() >= 0.99
+        assert np.array_equal(o, ref), i  # the oracle is the reference's arithmetic on this CPU
     single = enc.encode_audio_batch([audio[2]], 24000)
     assert single[0].shape == arrays["batch_single"].shape
     assert enc.encode_audio_batch([], 24000) == []

@@ -249,6 +249,22 @@ struct mimi_engine {
     unsigned* amax_red = nullptr;
     unsigned* amax_host = nullptr;  // pinned
     int32_t* item_codes = nullptr;  // one item's codes (per-item overflow fallback)
+    // encodes enqueued by mimi_encode_async and not yet waited (see encode_async_locked)
+    struct Pending {
+        int64_t id = 0;  // ticket; 0 = free
+        hipEvent_t done = nullptr;
+        unsigned* amax = nullptr;  // pinned [kMaxActSlots]: this encode's per-tensor maxima (f16x3)
+        int nslots = 0;
+        bool h16 = false;
+        const float* audio = nullptr;
+        int B = 0, K = 0;
+        int64_t L = 0;
+        int32_t* codes = nullptr;
+        hipStream_t s = nullptr;
+    };
+    static constexpr int kMaxPending = 16;
+    Pending pend[kMaxPending];
+    int64_t next_ticket = 1;
     size_t item_codes_cap = 0;
     int f16_reruns = 0;             // encodes that took the overflow fallback (diagnostic)
     bool profiling = false;
@@ -1511,6 +1527,7 @@ static float slot_amax(const mimi_engine* e, int i) {
 static int f16_pass(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s,
                     bool* overflow) {
     *overflow = false;
+    HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));  // encodes enqueued on other streams use amax_dev too
     HIP_TRY(hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), s));
     int rc = encode_pass(e, audio, B, L, K, codes, s, PREC_F16X3);
     if (rc) return rc;
@@ -1593,15 +1610,18 @@ static int calibrate_scales(mimi_engine* e) {
     return rc;
 }
 
-static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s) {
-    const int prec = e->precision;
-    const StagePlan p = plan_lengths(e->cfg, L);
-    if (prec != PREC_F16X3 || act_planes(e, p, prec) != 2) return encode_pass(e, audio, B, L, K, codes, s, prec);
-    bool ovf = false;
-    int rc = f16_pass(e, audio, B, L, K, codes, s, &ovf);
-    if (rc || !ovf) return rc;
+// Per-item overflow fallback of one f16x3 encode (see "activation scales"): every item re-encoded alone at the
+// same padded length, in bf16x6 where it overflows alone.  Synchronises s.
+static int overflow_fallback(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes,
+                             hipStream_t s) {
     ++e->f16_reruns;
-    if (B == 1) return encode_pass(e, audio, 1, L, K, codes, s, PREC_BF16X6);
+    const StagePlan p = plan_lengths(e->cfg, L);
+    int rc;
+    if (B == 1) {
+        if ((rc = encode_pass(e, audio, 1, L, K, codes, s, PREC_BF16X6))) return rc;
+        HIP_TRY(hipStreamSynchronize(s));
+        return MIMI_OK;
+    }
     const size_t per = (size_t)K * p.frames12;
     if (e->item_codes_cap < per) {
         HIP_TRY(hipStreamSynchronize(s));
@@ -1611,38 +1631,129 @@ static int encode_locked(mimi_engine* e, const float* audio, int B, int64_t L, i
         HIP_TRY(hipMalloc(&e->item_codes, per * sizeof(int32_t)));
         e->item_codes_cap = per;
     }
+    bool ovf = false;
     for (int b = 0; b < B; ++b) {
         const float* ab = audio + (int64_t)b * L;
         if ((rc = f16_pass(e, ab, 1, L, K, e->item_codes, s, &ovf))) return rc;
         if (ovf && (rc = encode_pass(e, ab, 1, L, K, e->item_codes, s, PREC_BF16X6))) return rc;
         HIP_TRY(hipMemcpyAsync(codes + b * per, e->item_codes, per * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     }
+    HIP_TRY(hipStreamSynchronize(s));
     return MIMI_OK;
+}
+
+// Enqueues one encode on s and returns its ticket without waiting.  In f16x3 the per-tensor maxima are folded
+// and copied to this ticket's pinned slot behind the encode; mimi_encode_wait checks them.
+static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes,
+                               hipStream_t s, int64_t* ticket) {
+    mimi_engine::Pending* P = nullptr;
+    for (auto& q : e->pend)
+        if (q.id == 0) {
+            P = &q;
+            break;
+        }
+    if (!P)
+        return set_err(MIMI_ERR_STATE, "%d encodes in flight: call mimi_encode_wait first", mimi_engine::kMaxPending);
+    if (!P->done) HIP_TRY(hipEventCreateWithFlags(&P->done, hipEventDisableTiming));
+    if (!P->amax) HIP_TRY(hipHostMalloc(&P->amax, kMaxActSlots * sizeof(unsigned), hipHostMallocDefault));
+    const int prec = e->precision;
+    const bool h16 = prec == PREC_F16X3 && act_planes(e, plan_lengths(e->cfg, L), prec) == 2;
+    int rc;
+    int n = 0;
+    if (h16) {
+        HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));  // the maxima buffers are part of the workspace
+        HIP_TRY(hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), s));
+        if ((rc = encode_pass(e, audio, B, L, K, codes, s, PREC_F16X3))) return rc;
+        if (e->uncalibrated_slot) return set_err(MIMI_ERR_STATE, "f16x3: an activation has no calibrated scale");
+        n = (int)e->slot_of.size();
+        LAUNCH_TRY(launch_amax_reduce(e->amax_dev, n, e->amax_red, s), "amax_reduce");
+        HIP_TRY(hipMemcpyAsync(P->amax, e->amax_red, n * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipEventRecord(e->ws_free, s));
+    } else if ((rc = encode_pass(e, audio, B, L, K, codes, s, prec))) {
+        return rc;
+    }
+    HIP_TRY(hipEventRecord(P->done, s));
+    P->nslots = n;
+    P->h16 = h16;
+    P->audio = audio;
+    P->B = B;
+    P->L = L;
+    P->K = K;
+    P->codes = codes;
+    P->s = s;
+    P->id = e->next_ticket++;
+    *ticket = P->id;
+    return MIMI_OK;
+}
+
+static int encode_wait_locked(mimi_engine* e, int64_t ticket) {
+    mimi_engine::Pending* P = nullptr;
+    for (auto& q : e->pend)
+        if (ticket > 0 && q.id == ticket) P = &q;
+    if (!P) return set_err(MIMI_ERR_INVALID_ARGUMENT, "ticket %lld is not an encode in flight", (long long)ticket);
+    const mimi_engine::Pending q = *P;
+    P->id = 0;
+    HIP_TRY(hipEventSynchronize(q.done));
+    bool ovf = false;
+    for (int i = 0; q.h16 && i < q.nslots; ++i) {
+        float a;
+        std::memcpy(&a, &q.amax[i], 4);
+        if (std::isfinite(a) && a * e->act_scale[i] >= kF16Overflow) ovf = true;
+    }
+    return ovf ? overflow_fallback(e, q.audio, q.B, q.L, q.K, q.codes, q.s) : MIMI_OK;
+}
+
+static int check_encode_args(mimi_engine* e, const float* audio, int32_t batch, int64_t length, int32_t* K,
+                             int32_t* codes) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    if (!e->finalized) return set_err(MIMI_ERR_STATE, "mimi_finalize has not been called");
+    if (*K <= 0) *K = e->cfg.num_quantizers;
+    if (*K > e->cfg.num_quantizers)
+        return set_err(MIMI_ERR_INVALID_ARGUMENT,
+                       "The number of quantizers (i.e codebooks) asked should be lower than the total number of "
+                       "quantizers %d, but is currently %d.",
+                       e->cfg.num_quantizers, *K);
+    if (*K < e->cfg.num_semantic_quantizers)
+        return set_err(MIMI_ERR_INVALID_ARGUMENT, "num_quantizers %d below the semantic quantizers %d", *K,
+                       e->cfg.num_semantic_quantizers);
+    if (*K > e->levels_available)
+        return set_err(MIMI_ERR_WEIGHTS, "num_quantizers %d but the checkpoint has %d codebooks", *K, e->levels_available);
+    if (batch <= 0 || length <= 0 || !audio || !codes)
+        return set_err(MIMI_ERR_INVALID_ARGUMENT, "batch=%d length=%lld", batch, (long long)length);
+    if (length > (int64_t)1 << 31) return set_err(MIMI_ERR_INVALID_ARGUMENT, "length %lld too large", (long long)length);
+    return MIMI_OK;
+}
+
+extern "C" int mimi_encode_async(mimi_engine* e, const float* audio, int32_t batch, int64_t length, int32_t K,
+                                 int32_t* codes, void* stream, int64_t* ticket) {
+    int rc = check_encode_args(e, audio, batch, length, &K, codes);
+    if (rc) return rc;
+    if (!ticket) return set_err(MIMI_ERR_INVALID_ARGUMENT, "ticket is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    (void)hipGetLastError();  // a failure left by an unrelated earlier call must not fail this encode's launches
+    return encode_async_locked(e, audio, batch, length, K, codes, reinterpret_cast<hipStream_t>(stream), ticket);
+}
+
+extern "C" int mimi_encode_wait(mimi_engine* e, int64_t ticket) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    return encode_wait_locked(e, ticket);
 }
 
 extern "C" int mimi_encode(mimi_engine* e, const float* audio, int32_t batch, int64_t length, int32_t K,
                            int32_t* codes, void* stream) {
-    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
-    if (!e->finalized) return set_err(MIMI_ERR_STATE, "mimi_finalize has not been called");
-    if (K <= 0) K = e->cfg.num_quantizers;
-    if (K > e->cfg.num_quantizers)
-        return set_err(MIMI_ERR_INVALID_ARGUMENT,
-                       "The number of quantizers (i.e codebooks) asked should be lower than the total number of "
-                       "quantizers %d, but is currently %d.",
-                       e->cfg.num_quantizers, K);
-    if (K < e->cfg.num_semantic_quantizers)
-        return set_err(MIMI_ERR_INVALID_ARGUMENT, "num_quantizers %d below the semantic quantizers %d", K,
-                       e->cfg.num_semantic_quantizers);
-    if (K > e->levels_available)
-        return set_err(MIMI_ERR_WEIGHTS, "num_quantizers %d but the checkpoint has %d codebooks", K, e->levels_available);
-    if (batch <= 0 || length <= 0 || !audio || !codes)
-        return set_err(MIMI_ERR_INVALID_ARGUMENT, "batch=%d length=%lld", batch, (long long)length);
-    if (length > (int64_t)1 << 31) return set_err(MIMI_ERR_INVALID_ARGUMENT, "length %lld too large", (long long)length);
+    int rc = check_encode_args(e, audio, batch, length, &K, codes);
+    if (rc) return rc;
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the HIP null stream, as in every HIP API
     (void)hipGetLastError();  // a failure left by an unrelated earlier call must not fail this encode's launches
-    return encode_locked(e, audio, batch, length, K, codes, s);
+    int64_t ticket = 0;
+    // NULL stream = the HIP null stream, as in every HIP API
+    if ((rc = encode_async_locked(e, audio, batch, length, K, codes, reinterpret_cast<hipStream_t>(stream), &ticket)))
+        return rc;
+    return encode_wait_locked(e, ticket);
 }
 
 extern "C" int mimi_rvq_encode(mimi_engine* e, const float* emb, int64_t frames, int32_t K, int32_t* codes,
@@ -1690,6 +1801,10 @@ extern "C" void mimi_destroy(mimi_engine* e) {
     if (e->amax_dev) (void)hipFree(e->amax_dev);
     if (e->amax_host) (void)hipHostFree(e->amax_host);
     if (e->item_codes) (void)hipFree(e->item_codes);
+    for (auto& q : e->pend) {
+        if (q.done) (void)hipEventDestroy(q.done);
+        if (q.amax) (void)hipHostFree(q.amax);
+    }
     delete e;
 }
 

@@ -67,6 +67,8 @@ __device__ __forceinline__ int chunk_swz(int row) {
 //           and the B images of both taps, and the second K step reads the A image one row down.  A's
 //           LDS-DMA bytes halve (stage = 2 K steps; KOrder visits the chains' first taps only).
 enum : int { FL_READFIRST = 1, FL_PRIO = 2, FL_PAIR = 4 };
+// tuning diagnostics (tools/gemm_bench.hip only; results are garbage): no DMA refills after the prologue / no MFMAs
+enum : int { FL_DIAG_NODMA = 64, FL_DIAG_NOMMA = 128 };
 
 template <int BM, int BN, int WM, int WN, int NS, int STAGES, int EPI, int OUTP, int TAG, int LW = 0, int BK = 32,
           int MF = 32, int FL = 0, bool F16 = false>
@@ -260,7 +262,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         bf16x8 af[NS][TM], bf[NS][TN];
         if ((FL & FL_READFIRST) && compute) read_frags(As, Bs, 0, af, bf);
         // the stage consumed in step kt-1 is free: refill it with step kt + STAGES - 1
-        if (loader && kt + STAGES - 1 < KT) issue((kt + STAGES - 1) % STAGES);
+        if (!(FL & FL_DIAG_NODMA) && loader && kt + STAGES - 1 < KT) issue((kt + STAGES - 1) % STAGES);
         if (!compute) continue;
         if (FL & FL_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -268,7 +270,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
 #pragma unroll
             for (int ks = 0; ks < KSUB; ++ks) {
                 if (!(FL & FL_READFIRST) || ks > 0 || img > 0) read_frags(As, Bs, ks, af, bf, img);
-                mma_split<NS, TM, TN, F16>(acc, af, bf);
+                if (!(FL & FL_DIAG_NOMMA)) mma_split<NS, TM, TN, F16>(acc, af, bf);
             }
         if (FL & FL_PRIO) __builtin_amdgcn_s_setprio(0);
     }

@@ -10,6 +10,12 @@ in ``libritts-r-mimi/process_libritts_r.py:33-105``, ``yodas2-mimi/process_shard
   single item; otherwise pad-to-longest, ONE encode, trim item i to ``int(ceil(L_i / (sr / 12.5)))``
   frames                                                                                        ``:88-140``
 
+The inputs and outputs are the reference's; the data path is leaner.  The reference runs the feature
+extractor and moves ``input_values`` and the int64 ``padding_mask`` (8 B per sample) to the device, although
+the model ignores the mask (``TF/modeling_mimi.py:1244, :1247``).  Here the items are copied straight into a
+zeroed device batch (the same values as the extractor's right padding with 0.0, after its float32 cast), no
+mask is built or moved, and the int32 codes come back to the host before the int64 widening.
+
 A shard script switches by replacing its ``class MimiEncoder`` with ``from mimi_hip import MimiEncoder``.
 """
 from __future__ import annotations
@@ -43,14 +49,45 @@ class MimiEncoder:
         self.num_quantizers = num_quantizers
         logger.info("Mimi model loaded successfully")
 
+    def _check(self, arrays, sample_rate):
+        # the feature extractor's checks and float32 cast (ENC/feature_extraction_encodec.py:130-150)
+        if sample_rate is not None and sample_rate != self.feature_extractor.sampling_rate:
+            raise ValueError(
+                f"The model corresponding to this feature extractor: {self.feature_extractor} was trained using a "
+                f"sampling rate of {self.feature_extractor.sampling_rate}. Please make sure that the provided audio "
+                f"input was sampled with {self.feature_extractor.sampling_rate} and not {sample_rate}.")
+        out = []
+        for a in arrays:
+            a = np.asarray(a, dtype=np.float32)
+            if a.ndim != 1:
+                raise ValueError(f"Expected mono audio but example has {a.shape[-1]} channels")
+            out.append(a)
+        return out
+
+    def _encode_padded(self, arrays: List[np.ndarray]) -> np.ndarray:
+        """Right-pad with 0.0 to the longest on the device, one encode -> int32 [B, K, T] on the host."""
+        if not hasattr(self.model, "encode_async"):  # any other MimiModel.encode-compatible model: reference path
+            inputs = self.feature_extractor(raw_audio=arrays if len(arrays) > 1 else arrays[0],
+                                            sampling_rate=self.feature_extractor.sampling_rate, return_tensors="pt",
+                                            padding=True)
+            inputs = {k: v.to(self.device) for k, v in inputs.items()}
+            return self.model.encode(inputs["input_values"], inputs["padding_mask"],
+                                     num_quantizers=self.num_quantizers).audio_codes.cpu().numpy()
+        dev = self.model.device
+        lmax = max(a.shape[0] for a in arrays)
+        if lmax == 0:
+            raise ValueError("empty audio")
+        x = torch.zeros((len(arrays), lmax), dtype=torch.float32, device=dev)
+        for i, a in enumerate(arrays):
+            if a.shape[0]:
+                x[i, :a.shape[0]].copy_(torch.from_numpy(a))
+        K = self.num_quantizers or self.model.config.num_quantizers
+        return self.model.encode_async(x, K).wait().cpu().numpy()
+
     def encode_audio_chunk(self, audio_array: np.ndarray, sample_rate: int = 24000) -> np.ndarray:
         with torch.no_grad():
-            inputs = self.feature_extractor(raw_audio=audio_array, sampling_rate=sample_rate, return_tensors="pt")
-            inputs = {k: v.to(self.device) for k, v in inputs.items()}
-            encoder_outputs = self.model.encode(inputs["input_values"], inputs["padding_mask"],
-                                                num_quantizers=self.num_quantizers)
-            audio_codes = encoder_outputs.audio_codes
-            return audio_codes.cpu().numpy()[0]
+            (a,) = self._check([audio_array], sample_rate)
+            return self._encode_padded([a])[0].astype(np.int64)
 
     def encode_audio_batch(self, audio_arrays: List[np.ndarray], sample_rate: int = 24000) -> List[np.ndarray]:
         if len(audio_arrays) == 0:
@@ -58,17 +95,12 @@ class MimiEncoder:
         if len(audio_arrays) == 1:
             return [self.encode_audio_chunk(audio_arrays[0], sample_rate)]
         with torch.no_grad():
-            original_lengths = [len(audio) for audio in audio_arrays]
-            inputs = self.feature_extractor(raw_audio=audio_arrays, sampling_rate=sample_rate, return_tensors="pt",
-                                            padding=True)
-            inputs = {k: v.to(self.device) for k, v in inputs.items()}
-            encoder_outputs = self.model.encode(input_values=inputs["input_values"],
-                                                padding_mask=inputs["padding_mask"],
-                                                num_quantizers=self.num_quantizers)
-            audio_codes = encoder_outputs.audio_codes.cpu()
+            arrays = self._check(audio_arrays, sample_rate)
+            original_lengths = [len(audio) for audio in arrays]
+            audio_codes = self._encode_padded(arrays)
             frame_rate = sample_rate / 12.5
             results = []
             for i, orig_length in enumerate(original_lengths):
                 actual_frames = int(np.ceil(orig_length / frame_rate))
-                results.append(audio_codes[i, :, :actual_frames].numpy())
+                results.append(audio_codes[i, :, :actual_frames].astype(np.int64))
             return results

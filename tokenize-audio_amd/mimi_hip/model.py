@@ -78,6 +78,20 @@ def resolve_checkpoint(name_or_path: str) -> str:
         f"(+ config.json), set MIMI_HIP_CHECKPOINT, or use 'synthetic:<seed>' for the seeded test checkpoint")
 
 
+class EncodeTicket:
+    """An encode in flight (``MimiHipModel.encode_async``)."""
+
+    def __init__(self, model: "MimiHipModel", ticket: int, out: torch.Tensor, audio: torch.Tensor):
+        self._model, self._ticket, self.out, self._audio = model, ticket, out, audio
+
+    def wait(self) -> torch.Tensor:
+        if self._ticket:
+            t, self._ticket = self._ticket, 0
+            _lib.check(self._model._lib.mimi_encode_wait(self._model._h, t))
+            self._audio = None
+        return self.out
+
+
 class MimiHipModel:
     """Encode-only Mimi on MI355X."""
 
@@ -208,6 +222,21 @@ class MimiHipModel:
             _lib.check(self._lib.mimi_encode(self._h, ctypes.c_void_p(audio.data_ptr()), B, L, num_quantizers,
                                              ctypes.c_void_p(out.data_ptr()), self._stream()))
         return out
+
+    def encode_async(self, audio: torch.Tensor, num_quantizers: int, out: Optional[torch.Tensor] = None
+                     ) -> "EncodeTicket":
+        """Enqueue an encode of device f32 [B, L] on the current stream and return without waiting
+        (``mimi_encode_async``); ``ticket.wait()`` returns the int32 [B, K, T] codes once they are final (the
+        f16x3 overflow check runs there).  The ticket keeps ``audio`` alive until then."""
+        B, L = audio.shape
+        T = encoded_length(L, self.config)
+        if out is None:
+            out = torch.empty((B, num_quantizers, T), dtype=torch.int32, device=self.device)
+        t = ctypes.c_int64()
+        with self._lock:
+            _lib.check(self._lib.mimi_encode_async(self._h, ctypes.c_void_p(audio.data_ptr()), B, L, num_quantizers,
+                                                   ctypes.c_void_p(out.data_ptr()), self._stream(), ctypes.byref(t)))
+        return EncodeTicket(self, t.value, out, audio)
 
     def quantize(self, embedding: torch.Tensor, num_quantizers: int) -> torch.Tensor:
         """Quantizer alone on a pre-quantizer embedding [B, 512, T] -> int64 codes [B, K, T]."""

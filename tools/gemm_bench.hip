@@ -105,9 +105,12 @@ int main(int argc, char** argv) {
     Variant vars[] = {
         {"h2 256x128 8w mf16 s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
         {"h2 256x128 8w+4ld s2 pair", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR, true>, 64, 12, true},
-        {"h2 128x128 4w+4ld mf16 s4", launch_pl<128, 128, 2, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
-        {"h2 256x256 8w mf16 s2", launch_pl<256, 256, 4, 2, 2, 2, 0, 32, 16, 0, true>, 32, 12},
-        {"h2 256x256 8w bk16 s2 pair", launch_pl<256, 256, 4, 2, 2, 2, 0, 16, 32, FL_PAIR, true>, 32, 12, true},
+        {"DIAG nodma pair", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_DIAG_NODMA, true>, 64, 12, true},
+        {"DIAG nomma pair", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_DIAG_NOMMA, true>, 64, 12, true},
+        {"DIAG nodma+nomma pair", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_DIAG_NODMA | FL_DIAG_NOMMA, true>, 64, 12, true},
+        {"h2 256x128 8w+4ld s2 pair prio", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PRIO, true>, 64, 12, true},
+        {"h2 256x128 8w+4ld s2 pair rf", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_READFIRST, true>, 64, 12, true},
+        {"h2 256x128 8w+4ld s2 pair mf32", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 32, FL_PAIR, true>, 64, 12, true},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
@@ -115,7 +118,9 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
+    const char* only = argc > 2 ? argv[2] : nullptr;
     for (const Shape& sh : shapes) {
+        if (only && !strstr(only, sh.name)) continue;
         const long long K = (long long)sh.k * sh.cin;
         const size_t nA = (size_t)sh.batch * sh.tin * sh.cin, nW = (size_t)sh.N * K,
                      nC = (size_t)sh.batch * sh.tout * sh.N;
