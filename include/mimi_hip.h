@@ -158,6 +158,24 @@ int mimi_resample_poly(const float* dev_in, const int64_t* dev_in_off, const int
                        const float* dev_filter, int32_t filter_len, int32_t up, int32_t down, int64_t pre_remove,
                        void* stream);
 
+/*
+ * Codec-BPE training over code strings (replaces the BpeTrainer run of codec-bpe/bpe_trainer.py:147-156; driven
+ * by mimi_hip/bpe.py).  The corpus: words of symbol ids (0 .. n_initial_tokens-1 = special tokens, then the
+ * alphabet), concatenated in `symbols`, word w = symbols[word_offsets[w] .. word_offsets[w+1]), occurring
+ * word_counts[w] times; all host memory, copied.  max_token_length <= 0: unlimited; else a pair formed by a
+ * merge is counted only when its merged length is below it.  Then, per step: mimi_bpe_best gives the pair of
+ * highest count (ties: smallest (left, right); count 0 when none is left), the caller decides the new token's
+ * id (a new one, or the id of an existing token with the same spelling) and length, and mimi_bpe_merge applies
+ * it to every word.  Ids up to 131071.
+ */
+typedef struct mimi_bpe mimi_bpe;
+int mimi_bpe_create(int device, const int32_t* symbols, int64_t n_symbols, const int64_t* word_offsets,
+                    const int64_t* word_counts, int64_t n_words, int32_t n_initial_tokens, int32_t vocab_size,
+                    int32_t max_token_length, mimi_bpe** out);
+int mimi_bpe_best(mimi_bpe* h, int32_t* left, int32_t* right, int64_t* count);
+int mimi_bpe_merge(mimi_bpe* h, int32_t left, int32_t right, int32_t new_id, int32_t new_len);
+void mimi_bpe_destroy(mimi_bpe* h);
+
 /* Device bytes the workspace needs for (batch, length); the engine grows it on demand. */
 int64_t mimi_workspace_bytes(const mimi_engine* e, int32_t batch, int64_t length);
 

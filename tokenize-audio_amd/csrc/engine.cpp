@@ -57,6 +57,11 @@ static int set_err(int code, const char* fmt, ...) {
 
 extern "C" const char* mimi_last_error(void) { return g_last_error.c_str(); }
 
+int mimi::set_error_message(int code, const char* msg) {
+    g_last_error = msg;
+    return code;
+}
+
 // ------------------------------------------------------------------------------------------------
 // config / length math
 // ------------------------------------------------------------------------------------------------

@@ -6,6 +6,9 @@
 
 namespace mimi {
 
+// sets the thread-local mimi_last_error() text (engine.cpp); returns code
+int set_error_message(int code, const char* msg);
+
 // ELU(x) = x (x > 0), expm1(x) (x <= 0), branchless, as exp(x) - 1 on the exp unit (v_exp_f32 of x*log2(e)):
 // 4 VALU.  exp(x) - 1 cancels for small |x|, but the error stays ABSOLUTE ~1e-7 (an ulp of 1.0), the size of
 // the fp32 rounding of any O(1) activation, so the block outputs are unchanged at the 1e-6 level (the

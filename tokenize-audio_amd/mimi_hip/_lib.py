@@ -28,6 +28,7 @@ EXPORTED_SYMBOLS = (
     "mimi_encoded_length_cfg",
     "mimi_workspace_bytes", "mimi_destroy", "mimi_last_error", "mimi_set_profiling", "mimi_profile_read",
     "mimi_profile_reset", "mimi_set_taps", "mimi_get_tap", "mimi_resample_poly",
+    "mimi_bpe_create", "mimi_bpe_best", "mimi_bpe_merge", "mimi_bpe_destroy",
 )
 RESAMPLE_MAX_TAPS = 8192  # MIMI_RESAMPLE_MAX_TAPS
 
@@ -97,6 +98,11 @@ def _declare(lib):
         "mimi_profile_reset": (c.c_int, [vp]),
         "mimi_set_taps": (c.c_int, [vp, c.c_int]),
         "mimi_get_tap": (c.c_int, [vp, c.c_char_p, vp, c.c_int64, c.POINTER(c.c_int64), c.POINTER(c.c_int64)]),
+        "mimi_bpe_create": (c.c_int, [c.c_int, vp, c.c_int64, vp, vp, c.c_int64, c.c_int32, c.c_int32, c.c_int32,
+                                      c.POINTER(vp)]),
+        "mimi_bpe_best": (c.c_int, [vp, c.POINTER(c.c_int32), c.POINTER(c.c_int32), c.POINTER(c.c_int64)]),
+        "mimi_bpe_merge": (c.c_int, [vp, c.c_int32, c.c_int32, c.c_int32, c.c_int32]),
+        "mimi_bpe_destroy": (None, [vp]),
         "mimi_resample_poly": (c.c_int, [vp, vp, vp, c.c_int32, vp, vp, vp, c.c_int64, vp, c.c_int32, c.c_int32,
                                          c.c_int32, c.c_int64, vp]),
     }

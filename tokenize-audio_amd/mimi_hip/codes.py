@@ -19,8 +19,9 @@ NUM_CODEBOOKS: int = 8
 CODEBOOK_SIZE: int = 2048
 
 
-def codes_to_chars(codes: Union[List[List[int]], np.ndarray, torch.Tensor], codebook_size: int,
-                   copy_before_conversion: bool = True, unicode_offset: int = UNICODE_OFFSET) -> str:
+def codes_to_codepoints(codes: Union[List[List[int]], np.ndarray, torch.Tensor], codebook_size: int,
+                        copy_before_conversion: bool = True, unicode_offset: int = UNICODE_OFFSET) -> np.ndarray:
+    """The code points ``codes_to_chars`` turns into characters, flat, in string order."""
     if isinstance(codes, list):
         codes = np.array(codes)
         copy_before_conversion = False
@@ -34,7 +35,12 @@ def codes_to_chars(codes: Union[List[List[int]], np.ndarray, torch.Tensor], code
     # (in place when copy_before_conversion=False; same overflow behaviour for narrow dtypes)
     for i in range(codes.shape[0]):
         codes[i] += unicode_offset + i * codebook_size
-    flat = np.ascontiguousarray(codes.T.reshape(-1))
+    return np.ascontiguousarray(codes.T.reshape(-1))
+
+
+def codes_to_chars(codes: Union[List[List[int]], np.ndarray, torch.Tensor], codebook_size: int,
+                   copy_before_conversion: bool = True, unicode_offset: int = UNICODE_OFFSET) -> str:
+    flat = codes_to_codepoints(codes, codebook_size, copy_before_conversion, unicode_offset)
     if flat.size == 0:
         return ""
     if flat.dtype.kind not in "iu":
