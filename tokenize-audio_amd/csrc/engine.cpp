@@ -232,6 +232,9 @@ struct mimi_engine {
     float* cb_rows = nullptr;
     float* cb_frag = nullptr;
     float* cb_norm = nullptr;
+    void* cb_h16 = nullptr;       // fp16 planes for the approximate distances (ops.hip rvq_level_h16_kernel)
+    float* cb_unscale = nullptr;  // [level]
+    float* cb_emax = nullptr;     // [level]
 
     float* rope_cos = nullptr;
     float* rope_sin = nullptr;
@@ -945,6 +948,35 @@ extern "C" int mimi_finalize(mimi_engine* e) {
     }
     if ((rc = upload(e, &e->cb_rows, rows)) || (rc = upload(e, &e->cb_frag, frag)) || (rc = upload(e, &e->cb_norm, norms)))
         return rc;
+    {
+        // fp16 planes of embed * cs (cs: power of two putting max|embed| in [2^13, 2^14)) in 32x32x16 B-fragment
+        // order [level][code tile][k step][plane][lane (j, h)][8]: embed[32 ct + j][16 ks + 8 h + q]
+        std::vector<_Float16> h16((size_t)L * n * D * 2);
+        std::vector<float> unsc(L), emax(L);
+        for (int lv = 0; lv < L; ++lv) {
+            const float* R = rows.data() + (size_t)lv * n * D;
+            float amax = 0.0f, nmax = 0.0f;
+            for (size_t i = 0; i < (size_t)n * D; ++i) amax = std::max(amax, std::fabs(R[i]));
+            for (int j = 0; j < n; ++j) nmax = std::max(nmax, norms[(size_t)lv * n + j]);
+            const float cs = amax > 0.0f && std::isfinite(amax) ? std::ldexp(1.0f, 13 - std::ilogb(amax)) : 1.0f;
+            unsc[lv] = 1.0f / cs;
+            emax[lv] = std::sqrt(nmax) * (1.0f + 1e-6f);
+            _Float16* H = h16.data() + (size_t)lv * n * D * 2;
+            size_t o = 0;
+            for (int ct = 0; ct < n / 32; ++ct)
+                for (int ks = 0; ks < D / 16; ++ks)
+                    for (int pl = 0; pl < 2; ++pl)
+                        for (int lane = 0; lane < 64; ++lane)
+                            for (int q = 0; q < 8; ++q) {
+                                const float t = R[(size_t)(32 * ct + (lane & 31)) * D + 16 * ks + 8 * (lane >> 5) + q] * cs;
+                                const _Float16 hi = (_Float16)t;
+                                H[o++] = pl == 0 ? hi : (_Float16)(t - (float)hi);
+                            }
+        }
+        if ((rc = dev_alloc(e, &e->cb_h16, h16.size() * sizeof(_Float16)))) return rc;
+        HIP_TRY(hipMemcpy(e->cb_h16, h16.data(), h16.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+        if ((rc = upload(e, &e->cb_unscale, unsc)) || (rc = upload(e, &e->cb_emax, emax))) return rc;
+    }
     e->levels_available = L;
     e->host_w.clear();
     if ((rc = calibrate_scales(e))) return rc;
@@ -1200,11 +1232,14 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     r.cb_frag = e->cb_frag;
     r.cb_rows = e->cb_rows;
     r.cb_norm = e->cb_norm;
+    r.cb_h16 = e->cb_h16;
+    r.cb_unscale = e->cb_unscale;
+    r.cb_emax = e->cb_emax;
     r.codes = codes;
     r.frames_per_item = frames_per_item;
     LAUNCH_TRY(launch_rvq(r, s), "rvq");
     rec.mark("rvq", 2.0 * frames * r.D * r.ncodes * K, (double)frames * (2 * r.D) * 4 + (double)frames * K * 4,
-             "mimi::rvq_level_kernel<256>");
+             e->cb_h16 ? "mimi::rvq_level_h16_kernel<256>" : "mimi::rvq_level_kernel<256>");
     return MIMI_OK;
 }
 

@@ -14,6 +14,7 @@
 // MFMAs so their latency hides under 64 * (BM/WM/32) * (BN/WN/32) MFMA cycles per wave.
 // Fused prologue: ELU on A as it is written to LDS.  Fused epilogues: bias, ELU, residual add, GELU(erf),
 // layer scale + residual, RoPE (rotate-half pairs (d, d+32) live in the same lane of tiles tn, tn+1).
+#include <algorithm>
 #include <cstdio>
 
 
@@ -76,8 +77,20 @@ static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
     const long long nwg = (long long)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.batch;
     if (nwg > 0x7fffffffLL) return hipErrorInvalidValue;
     if (F16 && ((OUTP & 7) ? a.out_scale <= 0.0f : false)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL, F16>), dim3((unsigned)nwg),
-                       dim3((WM * WN + LW) * 64), 0, s, a);
+    auto kern = gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL, F16>;
+    long long grid = nwg;
+    if (FL & FL_PERSIST) {  // one workgroup per resident slot, a multiple of the 8 XCDs
+        static int slots = 0;
+        if (!slots) {
+            int dev = 0, ncu = 256, occ = 1;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, (WM * WN + LW) * 64, 0);
+            slots = std::max(8, ncu * std::max(1, occ) / 8 * 8);
+        }
+        grid = std::min<long long>(nwg, slots);
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3((WM * WN + LW) * 64), 0, s, a);
     return hipGetLastError();
 }
 
@@ -176,7 +189,7 @@ template <int EPI, int OUTP, int TAG>
 static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
     if (pair_ok(a) && tiles(a, 256, 128) < kSmallGrid)
         return run_planes<64, 64, 2, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR, true>(a, s);
-    if (pair_ok(a)) return run_planes<256, 128, 4, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR, true>(a, s);
+    if (pair_ok(a)) return run_planes<256, 128, 4, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR | FL_PERSIST, true>(a, s);
     return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP, TAG, 0, 32, 16, 0, true>(a, s);
 }
 

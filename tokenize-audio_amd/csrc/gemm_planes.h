@@ -66,7 +66,11 @@ __device__ __forceinline__ int chunk_swz(int row) {
 //           input line (A(m, (j+s)Cin + c) = A(m+1, j Cin + c)), so a stage holds ONE A image of BM + RPP rows
 //           and the B images of both taps, and the second K step reads the A image one row down.  A's
 //           LDS-DMA bytes halve (stage = 2 K steps; KOrder visits the chains' first taps only).
-enum : int { FL_READFIRST = 1, FL_PRIO = 2, FL_PAIR = 4 };
+//           FL_PERSIST -- a grid of (CUs x resident workgroups) loops over the tiles (tile = blockIdx.x + i *
+//           gridDim.x, the XCD map applied to the tile index): a tile's epilogue stores drain while the same
+//           workgroup already streams its next tile's first stages (the barrier between them waits for LDS
+//           only, never for the stores), and no workgroup launch / ring fill per tile.
+enum : int { FL_READFIRST = 1, FL_PRIO = 2, FL_PAIR = 4, FL_PERSIST = 8 };
 // tuning diagnostics (tools/gemm_bench.hip only; results are garbage): no DMA refills after the prologue / no MFMAs
 enum : int { FL_DIAG_NODMA = 64, FL_DIAG_NOMMA = 128 };
 
@@ -127,7 +131,10 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     const int wn = compute ? wave % WN : 0;
     const int M = p.M, N = p.N, K = p.K;
     const int MT = (M + BM - 1) / BM, NTn = (N + BN - 1) / BN;
-    const int logical = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntiles = MT * NTn * p.batch;
+    float omx = 0.0f;  // max|planes value| (fp16 planes: the engine's range check), over this workgroup's tiles
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int logical = xcd_remap(tile, ntiles);
     const int nt = logical % NTn;
     const int rest = logical / NTn;
     const int mt = rest % MT;
@@ -281,13 +288,12 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     // stores them as 2 x 16 B fp32 and / or one 16-B bf16x8 per plane -- instead of one scattered 4-B (2-B
     // per plane) store per value.
     __syncthreads();  // every wave is done with the ring
-    if (!compute) return;
+    if (compute) {
     float* stg = reinterpret_cast<float*>(lds) + wave * (RW * LDE);
     const float* __restrict__ Rb = p.R ? p.R + (long long)b * p.c_bstride : nullptr;
     const int rbase = m0 + wm * RW;
     const int cbase = n0 + wn * CW + (lane & (MF - 1));
     const float us = F16 ? p.unscale : 1.0f;  // 1 / (activation scale x weight scale): exact power of two
-    float omx = 0.0f;  // max|planes value| (fp16 planes: the engine's range check)
 #pragma unroll
     for (int jh = 0; jh < JH; ++jh) {
 #pragma unroll
@@ -376,7 +382,14 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     }
     asm volatile("" ::: "memory");  // this pass's staging reads precede the next pass's writes (same wave)
     }
-    if (F16 && ONS) amax_commit(p.out_amax, omx);
+    }  // compute waves
+    if (FL & FL_PERSIST) {
+        // the staging reads are done before the next tile's DMA lands in the ring; the stores keep draining
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+    }  // tiles
+    if (F16 && ONS && compute) amax_commit(p.out_amax, omx);
 #endif
 }
 

@@ -249,6 +249,12 @@ struct RvqArgs {
     const float* cb_frag;   // [level][ncodes/32][D/8][64 lanes][4]
     const float* cb_rows;   // [level][ncodes][D]
     const float* cb_norm;   // [level][ncodes]
+    // approximate-then-exact distances (rvq_level_h16_kernel): fp16 planes of embed * cb_scale[level] in
+    // 32x32x16 B-fragment order [level][ncodes/32][D/16][2 planes][64 lanes][8 halves], 1 / cb_scale and
+    // max_j |embed_j| per level; null -> the all-fp32-MFMA kernel
+    const void* cb_h16;
+    const float* cb_unscale;
+    const float* cb_emax;
     int32_t* codes;
     int frames_per_item;    // T (for [b][level][t] output); 0 -> [level][frame]
     void* work;             // rvq_work_bytes(frames): residual ping-pong + per-slice partial argmins

@@ -938,9 +938,237 @@ __global__ __launch_bounds__(256) void rvq_final_kernel(RvqArgs p, int L) {
     rvq_store_code(p, L, f, rvq_merge(w, L, f, NSL, p.ncodes));
 }
 
+// Approximate-then-exact form (default).  The distances above are exact only for the code that wins: per frame
+// and code slice, an approximate -2 r.e on the fp16 matrix cores (r and the codebook as 2 fp16 planes each, 3
+// products, v_mfma_f32_32x32x16_f16: 1/5 of the fp32-MFMA time) selects the codes whose approximate squared
+// distance lies within a window of the slice's approximate minimum, and only those are re-scored with the
+// reference's exact chain (the fmaf chain over k = 0..255, + |r|^2, + |e|^2, clamp, sqrt -- the same operations
+// as rvq_level_kernel, so the same bits).  The window is rigorous: both the fp32 chain and the fp16-plane sum
+// lie within gamma_256 * 2|r||e| + O(2^-21 |r||e|) of the true dot product, i.e. within 2^-14 |r| |e| of each
+// other; the window is 2 x 2^-12 (|r| + max|e|)^2 plus a slack for the final adds and the sqrt rounding, so
+// the slice's exact argmin (first index on ties) is always a candidate.  Typical: 1.0-1.1 candidates per frame
+// and slice (measured on the golden embeddings with a 4x narrower window).  If a workgroup's candidates
+// overflow the LDS list (degenerate codebooks, e.g. all-equal entries), it scores every code exactly.
+// Per level one launch of (frames / 32) x 8 slices: each level's work is spread over ~1000 workgroups (a
+// single launch chaining all levels per 32-frame workgroup measured 25 % slower: too few, too serial).
+constexpr int RVQ_H16_FT = 32;
+constexpr int RVQ_CAND = 2048;
+
+template <int D>
+__global__ __launch_bounds__(512, 2) void rvq_level_h16_kernel(RvqArgs p, int L) {
+    constexpr int FT = RVQ_H16_FT;
+    constexpr int LDH = D / 2 + 4;
+    constexpr int RLD = D + 8;  // fp16 plane rows: 528 B = 132 dwords (conflict-free b128 fragment reads)
+    constexpr int NSL = 2048 / RVQ_CS;
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    __shared__ __attribute__((aligned(16))) float img[2][FT][LDH];  // -2 r, split by k parity (exact chain)
+    __shared__ __attribute__((aligned(16))) _Float16 rpl[2][FT][RLD];  // fp16 planes of r * rs
+    __shared__ float xn[FT], rus[FT], win[FT], smin[FT];
+    __shared__ int prev[FT];
+    __shared__ float redd[8][FT];
+    __shared__ unsigned cand[RVQ_CAND];
+    __shared__ unsigned ncand;
+    __shared__ unsigned long long best[FT];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+    const long long f0 = (long long)blockIdx.x * FT;
+    const int slice = blockIdx.y;
+    const RvqWork w = rvq_work(p, NSL);
+
+    // ---- prologue (as rvq_level_kernel): finish level L-1, form r_L
+    if (L >= 1 && tid < FT) {
+        const long long f = f0 + tid;
+        int ix = 0;
+        if (f < p.frames) {
+            ix = rvq_merge(w, L - 1, f, NSL, p.ncodes);
+            if (slice == 0) rvq_store_code(p, L - 1, f, ix);
+        }
+        prev[tid] = ix;
+    }
+    if (tid < FT) best[tid] = ~0ull;
+    if (tid == 0) ncand = 0;
+    __syncthreads();
+    const bool fresh = (L == 0 || L == p.nsem);
+    const int coff = (L < p.nsem) ? 0 : D;
+    const float* rows_prev = p.cb_rows + (long long)(L - 1) * p.ncodes * D;
+    const float* rin = w.res((L + 1) & 1);
+    float* rout = w.res(L & 1);
+#pragma unroll 4
+    for (int idx = tid; idx < FT * D / 4; idx += 512) {
+        const int i = idx / (D / 4), k = (idx % (D / 4)) * 4;
+        const long long f = f0 + i;
+        f32x4 r = {0.f, 0.f, 0.f, 0.f};
+        if (f < p.frames) {
+            if (fresh) {
+                r = *reinterpret_cast<const f32x4*>(p.proj + f * (2 * D) + coff + k);
+            } else {
+                const f32x4 a = *reinterpret_cast<const f32x4*>(rin + f * D + k);
+                const f32x4 e = *reinterpret_cast<const f32x4*>(rows_prev + (long long)prev[i] * D + k);
+                r = a - e;
+            }
+            if (slice == 0) *reinterpret_cast<f32x4*>(rout + f * D + k) = r;
+        }
+        img[0][i][k >> 1] = -2.0f * r.x;
+        img[1][i][k >> 1] = -2.0f * r.y;
+        img[0][i][(k >> 1) + 1] = -2.0f * r.z;
+        img[1][i][(k >> 1) + 1] = -2.0f * r.w;
+    }
+    __syncthreads();
+    // |r|^2 in torch's order (rvq_level_kernel) and max|r| per frame (16 threads per frame)
+    {
+        const int fi = tid >> 4, l = tid & 15;
+        if (l < 8) {
+            float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+            for (int blk = 0; blk < D / 8; ++blk) {
+                const int k = blk * 8 + l;
+                const float v = img[k & 1][fi][k >> 1];
+                a[blk & 3] = a[blk & 3] + v * v;
+            }
+            const float part = ((a[0] + a[1]) + a[2]) + a[3];
+            float tot = __shfl(part, (lane & ~15));
+#pragma unroll
+            for (int q = 1; q < 8; ++q) tot = tot + __shfl(part, (lane & ~15) + q);
+            if (l == 0) xn[fi] = tot * 0.25f;
+        }
+        float mx = 0.0f;
+        for (int k = l; k < D; k += 16) mx = fmaxf(mx, fabsf(img[k & 1][fi][k >> 1]));
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        if (l == 0) {
+            mx *= 0.5f;  // max |r|
+            const float rs = mx > 0.0f && mx < INFINITY ? ldexpf(1.0f, 13 - ilogbf(mx)) : 1.0f;
+            rus[fi] = 1.0f / rs;
+            win[fi] = rs;  // (the scale, until the window replaces it below)
+        }
+    }
+    __syncthreads();
+    // fp16 planes of r * rs
+    for (int idx = tid; idx < FT * D / 2; idx += 512) {
+        const int i = idx / (D / 2), k = (idx % (D / 2)) * 2;
+        const float rs = -0.5f * win[i];
+        const float t0 = img[0][i][k >> 1] * rs, t1 = img[1][i][k >> 1] * rs;
+        const _Float16 a0 = (_Float16)t0, a1 = (_Float16)t1;
+        rpl[0][i][k] = a0;
+        rpl[0][i][k + 1] = a1;
+        rpl[1][i][k] = (_Float16)(t0 - (float)a0);
+        rpl[1][i][k + 1] = (_Float16)(t1 - (float)a1);
+    }
+    __syncthreads();
+
+    // ---- approximate r.e for FT frames x this wave's 32 codes; the wave's 32 KB of codebook planes stream from
+    // L2 with 4 k-steps in flight
+    const int code0 = slice * RVQ_CS + wave * 32;
+    const h8* bp = reinterpret_cast<const h8*>(p.cb_h16) +
+                   ((long long)L * (p.ncodes / 32) + code0 / 32) * (D / 16) * 2 * 64 + lane;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    constexpr int PF = 4;
+    h8 bq[PF][2];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+        bq[q][0] = bp[q * 128];
+        bq[q][1] = bp[q * 128 + 64];
+    }
+#pragma unroll PF
+    for (int ks = 0; ks < D / 16; ++ks) {
+        const int cur = ks % PF;
+        const h8 b0 = bq[cur][0], b1 = bq[cur][1];
+        if (ks + PF < D / 16) {
+            bq[cur][0] = bp[(ks + PF) * 128];
+            bq[cur][1] = bp[(ks + PF) * 128 + 64];
+        }
+        const h8 a0 = *reinterpret_cast<const h8*>(&rpl[0][lane & 31][ks * 16 + 8 * h]);
+        const h8 a1 = *reinterpret_cast<const h8*>(&rpl[1][lane & 31][ks * 16 + 8 * h]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
+    }
+    const int code = code0 + (lane & 31);
+    const float yn = p.cb_norm[(long long)L * p.ncodes + code];
+    const float cus = p.cb_unscale[L];
+    float ad[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        ad[r] = (-2.0f * (acc[r] * (rus[row] * cus)) + xn[row]) + yn;
+        float m = ad[r];
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+        if ((lane & 31) == 0) redd[wave][row] = m;
+    }
+    __syncthreads();
+    if (tid < FT) {
+        float m = redd[0][tid];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) m = fminf(m, redd[q][tid]);
+        smin[tid] = m;
+        const float emax = p.cb_emax[L];
+        const float rn = __builtin_sqrtf(fmaxf(xn[tid], 0.0f)) + emax;
+        win[tid] = ldexpf(rn * rn, -11) + ldexpf(fabsf(m), -20) + 1e-30f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        // NaN distances (a non-finite residual) are candidates too: the exact path decides
+        if (!(ad[r] > smin[row] + win[row]) && f0 + row < p.frames) {
+            const unsigned slot = atomicAdd(&ncand, 1u);
+            if (slot < RVQ_CAND) cand[slot] = ((unsigned)row << 16) | (unsigned)(code - slice * RVQ_CS);
+        }
+    }
+    __syncthreads();
+    // ---- exact re-scoring: the candidates, or (degenerate: the list overflowed) every code of the slice
+    const float* cbr = p.cb_rows + (long long)L * p.ncodes * D;
+    const unsigned nc = ncand;
+    const bool all = nc > RVQ_CAND;
+    const unsigned total = all ? FT * RVQ_CS : nc;
+    for (unsigned i = tid; i < total; i += 512) {
+        const int row = all ? (int)(i % FT) : (int)(cand[i] >> 16);
+        const int c = slice * RVQ_CS + (all ? (int)(i / FT) : (int)(cand[i] & 0xffff));
+        if (f0 + row >= p.frames) continue;
+        const f32x4* e = reinterpret_cast<const f32x4*>(cbr + (long long)c * D);
+        float a = 0.0f;
+        for (int k0 = 0; k0 < D / 4; k0 += 16) {  // 16 float4 of the code row in flight, then the in-order chain
+            f32x4 ev[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) ev[j] = e[k0 + j];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int k4 = k0 + j;
+                a = __builtin_fmaf(img[0][row][2 * k4], ev[j].x, a);
+                a = __builtin_fmaf(img[1][row][2 * k4], ev[j].y, a);
+                a = __builtin_fmaf(img[0][row][2 * k4 + 1], ev[j].z, a);
+                a = __builtin_fmaf(img[1][row][2 * k4 + 1], ev[j].w, a);
+            }
+        }
+        float d2 = a + xn[row];
+        d2 = d2 + p.cb_norm[(long long)L * p.ncodes + c];
+        const float d = __builtin_sqrtf(fmaxf(d2, 0.0f));
+        atomicMin(&best[row], ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)c);
+    }
+    __syncthreads();
+    if (tid < FT && f0 + tid < p.frames) {
+        const unsigned long long b = best[tid];
+        const long long f = f0 + tid;
+        w.pd(L & 1)[f * NSL + slice] = __uint_as_float((unsigned)(b >> 32));
+        w.pi(L & 1)[f * NSL + slice] = (int)(b & 0xffffffffu);
+    }
+}
+
 hipError_t launch_rvq(const RvqArgs& a, hipStream_t s) {
     if (a.D != 256 || a.ncodes != 2048 || !a.work) return hipErrorInvalidValue;
     if (a.frames <= 0) return hipSuccess;
+    if (a.cb_h16 && a.cb_unscale && a.cb_emax) {
+        const dim3 grid((unsigned)((a.frames + RVQ_H16_FT - 1) / RVQ_H16_FT), 2048 / RVQ_CS);
+        for (int L = 0; L < a.levels; ++L) {
+            hipLaunchKernelGGL((rvq_level_h16_kernel<256>), grid, dim3(512), 0, s, a, L);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(rvq_final_kernel, dim3((unsigned)((a.frames + 255) / 256)), dim3(256), 0, s, a, a.levels - 1);
+        return hipGetLastError();
+    }
     // small batches (fewer 64-frame workgroups than CUs, B < 16 x 10 s): 32-frame tiles
     const bool small = (a.frames + RVQ_FT - 1) / RVQ_FT * (2048 / RVQ_CS) < 256;
     const int ft = small ? 32 : RVQ_FT;

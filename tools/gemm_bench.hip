@@ -2,6 +2,7 @@
 //   hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I tokenize-audio_amd/csrc tools/gemm_bench.hip -o tools/bin/gemm_bench
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -47,7 +48,13 @@ void launch_bf(const GemmArgs& a, hipStream_t s) {
 template <int BM, int BN, int WM, int WN, int NS, int ST, int LW = 0, int BK = 32, int MF = 32, int FL = 0,
           bool F16 = false>
 void launch_pl(const GemmArgs& a, hipStream_t s) {
-    const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.batch;
+    int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.batch;
+    if (FL & FL_PERSIST) {
+        int occ = 1;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &occ, gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI_BIAS, 0, 0, LW, BK, MF, FL, F16>, (WM * WN + LW) * 64, 0);
+        nwg = std::min(nwg, 256 * std::max(1, occ));
+    }
     hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI_BIAS, 0, 0, LW, BK, MF, FL, F16>), dim3(nwg),
                        dim3((WM * WN + LW) * 64), 0, s, a);
 }
@@ -105,12 +112,12 @@ int main(int argc, char** argv) {
     Variant vars[] = {
         {"h2 256x128 8w mf16 s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
         {"h2 256x128 8w+4ld s2 pair", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR, true>, 64, 12, true},
-        {"DIAG nodma pair", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_DIAG_NODMA, true>, 64, 12, true},
-        {"DIAG nomma pair", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_DIAG_NOMMA, true>, 64, 12, true},
-        {"DIAG nodma+nomma pair", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_DIAG_NODMA | FL_DIAG_NOMMA, true>, 64, 12, true},
-        {"h2 256x128 8w+4ld s2 pair prio", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PRIO, true>, 64, 12, true},
-        {"h2 256x128 8w+4ld s2 pair rf", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_READFIRST, true>, 64, 12, true},
-        {"h2 256x128 8w+4ld s2 pair mf32", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 32, FL_PAIR, true>, 64, 12, true},
+        {"h2 256x128 8w+4ld s2 pair PERSIST", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"DIAG nomma+nodma PERSIST", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NODMA | FL_DIAG_NOMMA, true>, 64, 12, true},
+        {"h2 128x128 8w s2 (fc1/res3)", launch_pl<128, 128, 4, 2, 2, 2, 0, 32, 16, 0, true>, 32, 12},
+        {"h2 128x128 8w s2 PERSIST", launch_pl<128, 128, 4, 2, 2, 2, 0, 32, 16, FL_PERSIST, true>, 32, 12},
+        {"h2 128x128 4w+4ld s3 (o/fc2)", launch_pl<128, 128, 2, 2, 2, 3, 4, 32, 16, 0, true>, 32, 12},
+        {"h2 128x128 4w+4ld s3 PERSIST", launch_pl<128, 128, 2, 2, 2, 3, 4, 32, 16, FL_PERSIST, true>, 32, 12},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
