@@ -138,6 +138,11 @@ int mimi_set_precision(mimi_engine* e, int32_t mode);
 int mimi_get_precision(const mimi_engine* e);
 /* MIMI_PRECISION_F16X3: encodes that took the overflow fallback so far (diagnostic). */
 int64_t mimi_f16_reruns(const mimi_engine* e);
+/* hipGraph replay of MIMI_PRECISION_F16X3 encodes (default on): the second encode of a (batch, length, K) shape
+ * captures the whole pass into a graph, later ones replay it (same kernels and arguments: identical codes).
+ * Never used while profiling or taps are on.  enable = 0 drops the captured graphs.  Replays so far: */
+int mimi_set_graphs(mimi_engine* e, int32_t enable);
+int64_t mimi_graph_replays(const mimi_engine* e);
 
 /* Frames produced for `length` samples with the default config (reference float32 length math). */
 int64_t mimi_encoded_length(int64_t length);

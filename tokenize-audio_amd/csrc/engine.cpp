@@ -23,6 +23,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -280,6 +281,27 @@ struct mimi_engine {
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfStat> prof;
     std::vector<std::string> prof_order;
+
+    // hipGraph replay of the f16x3 encode (see graph_encode): one captured graph per (batch, length, K), the
+    // audio / codes pointers passed through io_dev
+    struct Graph {
+        int B = 0, K = 0;
+        int64_t L = 0;
+        int ws_gen = 0, rope_gen = 0;
+        hipGraph_t g = nullptr;
+        hipGraphExec_t x = nullptr;
+        uint64_t used = 0;
+    };
+    static constexpr int kMaxGraphs = 8;
+    std::vector<Graph> graphs;
+    std::map<std::tuple<int, int64_t, int>, int> graph_seen;  // eager encodes per shape (capture on the 2nd)
+    bool graphs_enabled = true;
+    bool capturing = false;
+    void** io_dev = nullptr;  // [audio, codes] of the replay
+    hipStream_t cap_stream = nullptr;
+    int ws_gen = 0, rope_gen = 0;
+    uint64_t graph_clock = 0;
+    int64_t graph_replays = 0;
 
     bool taps = false;
     struct Tap {
@@ -1072,6 +1094,7 @@ static int ensure_ws(mimi_engine* e, size_t bytes, hipStream_t s) {
                        "workspace hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(err));
     }
     e->ws_bytes = bytes;
+    ++e->ws_gen;  // captured graphs address the old workspace
     return MIMI_OK;
 }
 
@@ -1100,6 +1123,7 @@ static int ensure_rope(mimi_engine* e, int64_t T) {
     HIP_TRY(hipMemcpy(e->rope_cos, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->rope_sin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
     e->rope_T = Tn;
+    ++e->rope_gen;
     return MIMI_OK;
 }
 
@@ -1236,6 +1260,7 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     r.cb_unscale = e->cb_unscale;
     r.cb_emax = e->cb_emax;
     r.codes = codes;
+    r.codes_ref = e->capturing ? reinterpret_cast<int32_t* const*>(e->io_dev + 1) : nullptr;
     r.frames_per_item = frames_per_item;
     LAUNCH_TRY(launch_rvq(r, s), "rvq");
     rec.mark("rvq", 2.0 * frames * r.D * r.ncodes * K, (double)frames * (2 * r.D) * 4 + (double)frames * K * 4,
@@ -1292,7 +1317,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     };
     Recorder rec{e, s};
     const char* kname = "?";
-    HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));
+    if (!e->capturing) HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));  // (a replay waits outside the graph)
     rec.begin();
     auto gemm_flops = [](const GemmArgs& a) { return 2.0 * a.batch * (double)a.M * a.N * a.K; };
     auto gemm_bytes = [](const GemmArgs& a, bool res) {
@@ -1324,6 +1349,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             ra.x = w.x;
             if (si == 0) {
                 ra.audio = audio;
+                ra.audio_ref = e->capturing ? const_cast<const float* const*>(reinterpret_cast<float**>(e->io_dev)) : nullptr;
                 ra.w0 = e->conv0.w;
                 ra.b0 = e->conv0.b;
                 ra.w3frag = e->res3[0].wfrag;
@@ -1470,13 +1496,18 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         use_h(aq, x.wqkv_h, x.wqkv_hs, t1a);
         LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, prec), "qkv");
         rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
+        if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, B, T, 3 * H * Dh, s))) return rc;
         const Act atta = new_act(nmf("xf%d.att", l));
+        // fp16-plane attention in f16x3 mode (also for the no-plane long clips: the same arithmetic as their
+        // prefixes); true fp32 in f32 mode and the bf16 modes
+        const bool ah16 = prec == PREC_F16X3;
         LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh), s,
-                                    w.att, nact, ns, atta.scale, atta.amax),
+                                    w.att, nact, ns, atta.scale, atta.amax, ah16),
                    "attention");
         rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4,
-                 T <= 256 ? (atta.scale > 0.0f && ns == 2 ? "mimi::attention_t256_h16_kernel" : "mimi::attention_t256_kernel")
-                          : "mimi::attention_kernel");
+                 ah16 ? (T <= 256 ? "mimi::attention_t256_h16_kernel" : "mimi::attention_band_h16_kernel")
+                     : (T <= 256 ? "mimi::attention_t256_kernel" : "mimi::attention_kernel"));
+        if ((rc = save_tap_planes(e, nmf("att%d", l).c_str(), w.att, ns, B, T, H * Dh, s, atta.scale))) return rc;
         GemmArgs ao = linear_args(w.att, rows, H * Dh, x.wo, Hd, w.t0);
         ao.Wsplit = x.wo_s;
         ao.R = w.t0;
@@ -1485,6 +1516,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         use_h(ao, x.wo_h, x.wo_hs, atta);
         LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
         rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
+        if ((rc = save_tap(e, nmf("oproj%d", l).c_str(), w.t0, B, T, Hd, s))) return rc;
         const Act t1b = new_act(nmf("xf%d.ln2", l));
         LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1b.scale,
                                     t1b.amax),
@@ -1504,6 +1536,8 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         }
         LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, prec), "fc1");
         rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
+        if ((rc = save_tap_planes(e, nmf("ff%d", l).c_str(), w.ff, ns, B, T, c.intermediate_size, s, ffa.scale)))
+            return rc;
         GemmArgs a2 = linear_args(w.ff, rows, c.intermediate_size, x.w2, Hd, w.t0);
         a2.Wsplit = x.w2_s;
         a2.R = w.t0;
@@ -1528,7 +1562,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     rec.mark("input_proj", gemm_flops(ap), gemm_bytes(ap, false), kname);
     if ((rc = save_tap(e, "proj", w.proj, B, T2, 2 * Dq, s))) return rc;
     if ((rc = run_rvq(e, w.proj, (int64_t)B * T2, K, codes, (int)T2, w.rvq, s, rec))) return rc;
-    HIP_TRY(hipEventRecord(e->ws_free, s));
+    if (!e->capturing) HIP_TRY(hipEventRecord(e->ws_free, s));
     return MIMI_OK;
 }
 
@@ -1682,6 +1716,118 @@ static int overflow_fallback(mimi_engine* e, const float* audio, int B, int64_t 
     return MIMI_OK;
 }
 
+// ---- hipGraph replay (f16x3).  A small batch is launch-bound: ~80 kernels per encode, each a few
+// microseconds of GPU time.  The second encode of a (batch, length, K) shape captures the whole pass -- the
+// maxima reset, every kernel, the maxima fold -- into a graph on a private stream; later encodes of that shape
+// replay it on the caller's stream behind one set_io_kernel that writes this call's audio / codes pointers
+// into io_dev (the stage-0 block and the RVQ kernels read them from there; every other operand lives in the
+// engine: weights, workspace, rope tables).  A graph is dropped when the workspace or the rope tables it
+// addresses are reallocated.  The replay is the same kernels with the same arguments: bit-identical codes.
+static void destroy_graph(mimi_engine::Graph& g) {
+    if (g.x) (void)hipGraphExecDestroy(g.x);
+    if (g.g) (void)hipGraphDestroy(g.g);
+    g.x = nullptr;
+    g.g = nullptr;
+}
+
+static void drop_graphs(mimi_engine* e) {
+    for (auto& g : e->graphs) destroy_graph(g);
+    e->graphs.clear();
+}
+
+// Captures the f16x3 pass of (B, L, K) into a new graph.  On any failure the capture is abandoned and the
+// caller runs the eager pass (the error is cleared: a graph is an optimisation, never a requirement).
+static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int B, int64_t L, int K,
+                                          int32_t* codes) {
+    if (!e->io_dev && hipMalloc(&e->io_dev, 2 * sizeof(void*)) != hipSuccess) {
+        (void)hipGetLastError();
+        e->io_dev = nullptr;
+        return nullptr;
+    }
+    if (!e->cap_stream && hipStreamCreateWithFlags(&e->cap_stream, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        e->cap_stream = nullptr;
+        return nullptr;
+    }
+    hipStream_t cs = e->cap_stream;
+    if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    e->capturing = true;
+    int rc = MIMI_OK;
+    if (hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), cs) != hipSuccess)
+        rc = MIMI_ERR_HIP;
+    if (!rc) rc = encode_pass(e, audio, B, L, K, codes, cs, PREC_F16X3);
+    if (!rc && launch_amax_reduce(e->amax_dev, (int)e->slot_of.size(), e->amax_red, cs) != hipSuccess) rc = MIMI_ERR_HIP;
+    e->capturing = false;
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(cs, &g);
+    hipGraphExec_t x = nullptr;
+    if (rc || ec != hipSuccess || !g || e->uncalibrated_slot || hipGraphInstantiate(&x, g, nullptr, nullptr, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        if (g) (void)hipGraphDestroy(g);
+        return nullptr;
+    }
+    if ((int)e->graphs.size() >= mimi_engine::kMaxGraphs) {  // evict the least recently used
+        size_t lru = 0;
+        for (size_t i = 1; i < e->graphs.size(); ++i)
+            if (e->graphs[i].used < e->graphs[lru].used) lru = i;
+        destroy_graph(e->graphs[lru]);
+        e->graphs.erase(e->graphs.begin() + (long)lru);
+    }
+    mimi_engine::Graph ng;
+    ng.B = B;
+    ng.L = L;
+    ng.K = K;
+    ng.ws_gen = e->ws_gen;
+    ng.rope_gen = e->rope_gen;
+    ng.g = g;
+    ng.x = x;
+    e->graphs.push_back(ng);
+    return &e->graphs.back();
+}
+
+// Runs the f16x3 pass of (B, L, K) as a graph replay on s when it can (*replayed = true); otherwise leaves
+// everything to the eager path.
+static int graph_encode(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s,
+                        bool* replayed) {
+    *replayed = false;
+    if (!e->graphs_enabled || e->profiling || e->taps || e->calibrating) return MIMI_OK;
+    // sizes first: nothing may be allocated inside a capture, and a reallocation retires the graphs
+    const StagePlan p = plan_lengths(e->cfg, L);
+    int rc = ensure_ws(e, ws_layout(e, B, p, nullptr, PREC_F16X3), s);
+    if (rc) return rc;
+    if ((rc = ensure_rope(e, p.frames25))) return rc;
+    mimi_engine::Graph* gr = nullptr;
+    for (auto it = e->graphs.begin(); it != e->graphs.end();) {
+        if (it->ws_gen != e->ws_gen || it->rope_gen != e->rope_gen) {
+            destroy_graph(*it);
+            it = e->graphs.erase(it);
+            continue;
+        }
+        if (it->B == B && it->L == L && it->K == K) gr = &*it;
+        ++it;
+    }
+    if (!gr) {
+        const auto key = std::make_tuple(B, L, K);
+        if (e->graph_seen.size() > 256) e->graph_seen.clear();
+        if (++e->graph_seen[key] < 2) return MIMI_OK;  // a shape seen once runs eagerly
+        gr = capture_graph(e, audio, B, L, K, codes);
+        if (!gr) {
+            e->graphs_enabled = false;  // capture unsupported here: stay eager from now on
+            return MIMI_OK;
+        }
+    }
+    gr->used = ++e->graph_clock;
+    HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));
+    LAUNCH_TRY(launch_set_io(e->io_dev, audio, codes, s), "set_io");
+    HIP_TRY(hipGraphLaunch(gr->x, s));
+    ++e->graph_replays;
+    *replayed = true;
+    return MIMI_OK;
+}
+
 // Enqueues one encode on s and returns its ticket without waiting.  In f16x3 the per-tensor maxima are folded
 // and copied to this ticket's pinned slot behind the encode; mimi_encode_wait checks them.
 static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes,
@@ -1701,12 +1847,16 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
     int rc;
     int n = 0;
     if (h16) {
-        HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));  // the maxima buffers are part of the workspace
-        HIP_TRY(hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), s));
-        if ((rc = encode_pass(e, audio, B, L, K, codes, s, PREC_F16X3))) return rc;
-        if (e->uncalibrated_slot) return set_err(MIMI_ERR_STATE, "f16x3: an activation has no calibrated scale");
+        bool replayed = false;
+        if ((rc = graph_encode(e, audio, B, L, K, codes, s, &replayed))) return rc;
         n = (int)e->slot_of.size();
-        LAUNCH_TRY(launch_amax_reduce(e->amax_dev, n, e->amax_red, s), "amax_reduce");
+        if (!replayed) {
+            HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));  // the maxima buffers are part of the workspace
+            HIP_TRY(hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), s));
+            if ((rc = encode_pass(e, audio, B, L, K, codes, s, PREC_F16X3))) return rc;
+            if (e->uncalibrated_slot) return set_err(MIMI_ERR_STATE, "f16x3: an activation has no calibrated scale");
+            LAUNCH_TRY(launch_amax_reduce(e->amax_dev, n, e->amax_red, s), "amax_reduce");
+        }
         HIP_TRY(hipMemcpyAsync(P->amax, e->amax_red, n * sizeof(unsigned), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipEventRecord(e->ws_free, s));
     } else if ((rc = encode_pass(e, audio, B, L, K, codes, s, prec))) {
@@ -1845,6 +1995,9 @@ extern "C" void mimi_destroy(mimi_engine* e) {
         if (q.done) (void)hipEventDestroy(q.done);
         if (q.amax) (void)hipHostFree(q.amax);
     }
+    drop_graphs(e);
+    if (e->io_dev) (void)hipFree(e->io_dev);
+    if (e->cap_stream) (void)hipStreamDestroy(e->cap_stream);
     delete e;
 }
 
@@ -1859,6 +2012,20 @@ extern "C" int mimi_set_precision(mimi_engine* e, int32_t mode) {
     e->precision = mode;
     return MIMI_OK;
 }
+
+extern "C" int mimi_set_graphs(mimi_engine* e, int32_t enable) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    e->graphs_enabled = enable != 0;
+    if (!enable) {
+        drop_graphs(e);
+        e->graph_seen.clear();
+    }
+    return MIMI_OK;
+}
+
+extern "C" int64_t mimi_graph_replays(const mimi_engine* e) { return e ? e->graph_replays : -1; }
 
 extern "C" int mimi_get_precision(const mimi_engine* e) { return e ? e->precision : -1; }
 

@@ -101,6 +101,18 @@ __device__ __forceinline__ void amax_commit(unsigned* amax, float mx) {
     }
 }
 
+// A pointer a captured hipGraph reads at run time: the engine's io block, written by set_io_kernel in front of
+// every replay (a vector load that bypasses the scalar cache, made wave-uniform).  ref == null: direct.
+template <typename T>
+__device__ __forceinline__ T* io_pointer(T* const* ref, T* direct) {
+    if (!ref) return direct;
+    const unsigned long long v = *reinterpret_cast<const volatile unsigned long long*>(ref);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return reinterpret_cast<T*>(((unsigned long long)hi << 32) | lo);
+}
+// io[0] = audio, io[1] = codes (the pointers of one graph replay)
+hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStream_t s);
+
 // out[i] = max over the AMAX_SUB sub-slots of slot i (one wave per slot)
 hipError_t launch_amax_reduce(const unsigned* amax, int nslots, unsigned* out, hipStream_t s);
 
@@ -185,6 +197,7 @@ hipError_t launch_gemm(int role, const GemmArgs& a, hipStream_t s, const char** 
 struct ResArgs {
     const float* x;       // [B][T][C] raw input (unused when audio != null)
     const float* audio;   // stage 0 only: [B][T] waveform; x = conv0(audio) is recomputed in-kernel
+    const float* const* audio_ref;  // non-null (a captured hipGraph): the waveform pointer is read from here
     const float* w0;      // conv0 weight [64][7]
     const float* b0;      // conv0 bias [64]
     long long T;
@@ -227,10 +240,10 @@ hipError_t launch_layernorm(const float* x, const float* g, const float* b, floa
                             int yns = 0, float yscale = 0.0f, unsigned* yamax = nullptr);
 
 // Sliding-window causal attention on the fused qkv tensor [B][T][3*H*D] (q, k already rotated);
-// output [B][T][H*D].
+// output [B][T][H*D].  h16: the fp16-plane kernels (PREC_F16X3; T <= 256 needs fp16-plane output), else fp32.
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window,
-                            float scale, hipStream_t s, void* outp = nullptr, long long out_pstride = 0,
-                            int outns = 0, float oscale = 0.0f, unsigned* oamax = nullptr);
+                            float scale, hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
+                            unsigned* oamax, bool h16);
 
 // planes -> fp32 (x0 + x1 [+ x2], or (h0 + h1) / hscale for fp16 planes); used only to materialise per-stage
 // taps of plane-format activations.
@@ -256,6 +269,7 @@ struct RvqArgs {
     const float* cb_unscale;
     const float* cb_emax;
     int32_t* codes;
+    int32_t* const* codes_ref;  // non-null (a captured hipGraph): the codes pointer is read from here
     int frames_per_item;    // T (for [b][level][t] output); 0 -> [level][frame]
     void* work;             // rvq_work_bytes(frames): residual ping-pong + per-slice partial argmins
 };

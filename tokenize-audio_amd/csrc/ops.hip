@@ -441,6 +441,86 @@ __device__ __forceinline__ void split8_h(const float (&v)[8], float sc, f16x8& h
     }
 }
 
+// One 32-key chunk of the fp16-plane attention for the wave's 32 queries: S^T = K . Q^T and O^T += V^T . P^T as
+// 3 fp16 plane products each, fp32 online softmax (as attn_chunk).  Kc: the chunk's 32 K rows (plane stride KPL,
+// row stride KLD); Vc: column 0 of the chunk's keys in the V^T planes (plane stride VPL, row stride VLD, keys
+// permuted inside each 16 as the S^T accumulator holds them); us = 1 / (K scale x Q scale).
+template <int KLD, int KPL, int VLD, int VPL>
+__device__ __forceinline__ void attn_chunk_h16(f32x16 (&o)[2], float& m, float& l, const f16x8 (&qf)[4][2],
+                                               const _Float16* Kc, const _Float16* Vc, int c0, int qw, int qi,
+                                               int kend, int window, int hf, int col, float us,
+                                               float ofac = 1.0f, float pscale = 16384.0f) {
+    // S^T[key][query] = K . Q^T
+    f32x16 st;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        const int ko = col * KLD + 16 * ks + 8 * hf;
+        const f16x8 k0 = *reinterpret_cast<const f16x8*>(Kc + ko);
+        const f16x8 k1 = *reinterpret_cast<const f16x8*>(Kc + KPL + ko);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, qf[ks][0], st, 0, 0, 0);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, qf[ks][1], st, 0, 0, 0);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, qf[ks][0], st, 0, 0, 0);
+    }
+    // mask + online softmax for this lane's query (fp32, as attn_chunk)
+    float cmax = -INFINITY;
+    const bool full = c0 + 31 <= qw && c0 > qw + 31 - window && c0 + 31 <= kend;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        float v = st[r] * us;
+        if (!full) {
+            const int key = c0 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            const bool ok = key <= qi && key > qi - window && key <= kend;
+            v = ok ? v : -INFINITY;
+        }
+        st[r] = v;
+        cmax = fmaxf(cmax, v);
+    }
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
+    const float mnew = fmaxf(m, cmax);
+    const float corr = (m == -INFINITY) ? 0.f : __expf(m - mnew);
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float pv = (st[r] == -INFINITY) ? 0.f : __expf(st[r] - mnew);
+        st[r] = pv;
+        psum += pv;
+    }
+    psum += __shfl_xor(psum, 32);
+    l = l * corr + psum;
+    m = mnew;
+    const float oc = corr * ofac;  // ofac: a power of two (a change of the V scale), so o * oc rounds as o * corr
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] *= oc;
+    // O^T[d][query] += V^T . P^T: k-step ks = keys 16 ks .. +15 of the chunk, lane half hf element e =
+    // st[8 ks + e] (key (e & 3) + 8 (e >> 2) + 4 hf)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        float pe[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pe[e] = st[8 * ks + e];
+        f16x8 p0, p1;
+        split8_h(pe, pscale, p0, p1);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int vo = (32 * t + col) * VLD + 16 * ks + 8 * hf;
+            const f16x8 v0 = *reinterpret_cast<const f16x8*>(Vc + vo);
+            const f16x8 v1 = *reinterpret_cast<const f16x8*>(Vc + VPL + vo);
+            o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1, p0, o[t], 0, 0, 0);
+            o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0, p1, o[t], 0, 0, 0);
+            o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0, p0, o[t], 0, 0, 0);
+        }
+    }
+}
+// position of key r inside the V^T image: keys permuted inside each 16 as the S^T accumulator holds them
+__device__ __forceinline__ int vt_key_pos(int r) {
+    const int k = r & 15;
+    return (r & ~15) + 8 * ((k >> 2) & 1) + (k & 3) + 4 * ((k >> 3) & 1);
+}
+
 __global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __restrict__ qkv, int T, int H,
                                                                  int window, float scale, void* __restrict__ outp,
                                                                  long long pstride, float oscale,
@@ -533,8 +613,7 @@ __global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __
         }
         *reinterpret_cast<f16x4*>(Ks + r * KLD + c) = h0;
         *reinterpret_cast<f16x4*>(Ks + KPL + r * KLD + c) = h1;
-        const int k = r & 15;
-        const int pr = (r & ~15) + 8 * ((k >> 2) & 1) + (k & 3) + 4 * ((k >> 3) & 1);
+        const int pr = vt_key_pos(r);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const float t = vv[q][e] * sv;
@@ -556,69 +635,8 @@ __global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __
     if (qw < T) {
         const int kstart = max(0, qw - window + 1) & ~31;
         for (int c0 = kstart; c0 <= kend; c0 += 32) {
-            // S^T[key][query] = K . Q^T
-            f32x16 st;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) st[r] = 0.f;
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
-                const int ko = (c0 + col) * KLD + 16 * ks + 8 * hf;
-                const f16x8 k0 = *reinterpret_cast<const f16x8*>(Ks + ko);
-                const f16x8 k1 = *reinterpret_cast<const f16x8*>(Ks + KPL + ko);
-                st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, qf[ks][0], st, 0, 0, 0);
-                st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, qf[ks][1], st, 0, 0, 0);
-                st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, qf[ks][0], st, 0, 0, 0);
-            }
-            // mask + online softmax for this lane's query (fp32, as attn_chunk)
-            float cmax = -INFINITY;
-            const bool full = c0 + 31 <= qw && c0 > qw + 31 - window && c0 + 31 <= kend;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float v = st[r] * us;
-                if (!full) {
-                    const int key = c0 + (r & 3) + 8 * (r >> 2) + 4 * hf;
-                    const bool ok = key <= qi && key > qi - window && key <= kend;
-                    v = ok ? v : -INFINITY;
-                }
-                st[r] = v;
-                cmax = fmaxf(cmax, v);
-            }
-            cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
-            const float mnew = fmaxf(m, cmax);
-            const float corr = (m == -INFINITY) ? 0.f : __expf(m - mnew);
-            float psum = 0.f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float pv = (st[r] == -INFINITY) ? 0.f : __expf(st[r] - mnew);
-                st[r] = pv;
-                psum += pv;
-            }
-            psum += __shfl_xor(psum, 32);
-            l = l * corr + psum;
-            m = mnew;
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) o[t][r] *= corr;
-            // O^T[d][query] += V^T . P^T: k-step ks = keys 16 ks .. +15 of the chunk, lane half hf element e =
-            // st[8 ks + e] (key (e & 3) + 8 (e >> 2) + 4 hf)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                float pe[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) pe[e] = st[8 * ks + e];
-                f16x8 p0, p1;
-                split8_h(pe, 16384.0f, p0, p1);
-#pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    const int vo = (32 * t + col) * VLD + c0 + 16 * ks + 8 * hf;
-                    const f16x8 v0 = *reinterpret_cast<const f16x8*>(Vt + vo);
-                    const f16x8 v1 = *reinterpret_cast<const f16x8*>(Vt + VPL + vo);
-                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1, p0, o[t], 0, 0, 0);
-                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0, p1, o[t], 0, 0, 0);
-                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0, p0, o[t], 0, 0, 0);
-                }
-            }
+            attn_chunk_h16<KLD, KPL, VLD, VPL>(o, m, l, qf, Ks + c0 * KLD, Vt + c0, c0, qw, qi, kend, window, hf,
+                                               col, us);
         }
     }
     __syncthreads();  // K / V dead: the output staging reuses the LDS
@@ -641,13 +659,178 @@ __global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __
     amax_commit(oamax, mx);
 }
 
+// T > 256 (clips over 10.24 s) on the fp16 matrix cores: a workgroup = 128 queries of one (batch item, head), 4
+// waves x 32 queries.  The keys of its band [q0 - W + 1, q0 + 127] stream through LDS in 32-key chunks as fp16
+// planes of the K rows and of V^T (chunk c + 1's rows load into registers while chunk c is computed), with the
+// chunk math of attention_t256_h16_kernel (attn_chunk_h16).  Scales are powers of two: per chunk for K (each
+// chunk's S^T is formed from scratch, so it is unscaled by that chunk's 1 / (sK sQ)), per wave for Q; V's scale
+// follows the largest chunk seen so far: when a chunk needs a smaller scale the O^T accumulator is rescaled by the
+// ratio (exact: powers of two, folded into the online-softmax correction) and later smaller-valued chunks put the
+// ratio on P instead (P s <= 2^14).  Every scale depends on this item's own q/k/v only.
+__global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                                 int T, int H, int window, float scale,
+                                                                 void* __restrict__ outp, long long pstride, int outns,
+                                                                 float oscale, unsigned* __restrict__ oamax) {
+    constexpr int D = 64, KC = 32, LDO = D + 1;
+    constexpr int KLD = 72, KPL = KC * KLD;  // K planes: [32 keys][72 halves] (conflict-free b128 fragment reads)
+    constexpr int VLD = 40, VPL = D * VLD;   // V^T planes: [64 dims][40 halves]
+    constexpr int CH = 2 * KPL + 2 * VPL;    // halves of one chunk image
+    constexpr int OST = 4 * 32 * LDO * 2;    // halves of the output staging (fp32, 4 waves x 32 x 65)
+    __shared__ __attribute__((aligned(16))) _Float16 lds[CH > OST ? CH : OST];
+    __shared__ float red[2][4];
+    _Float16* Ks = lds;
+    _Float16* Vt = lds + 2 * KPL;
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hf = lane >> 5, col = lane & 31;
+    const long long ld = 3LL * H * D;
+    const float* base = qkv + (long long)b * T * ld;
+    const int q0 = blockIdx.x * 128;
+    const int qw = q0 + 32 * wave, qi = qw + col;
+    const int kstart = max(0, q0 - window + 1) & ~31;
+    const int kend = min(T - 1, q0 + 127);        // the workgroup's last key
+    const int kend_w = min(T - 1, qw + 31);       // this wave's
+    // Q planes (as attention_t256_h16_kernel)
+    float qv[4][8];
+    float mq = 0.0f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f}, c = {0.f, 0.f, 0.f, 0.f};
+        if (qi < T) {
+            const float* qr = base + (long long)qi * ld + h * D + 16 * ks + 8 * hf;
+            a = *reinterpret_cast<const f32x4*>(qr);
+            c = *reinterpret_cast<const f32x4*>(qr + 4);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            qv[ks][e] = a[e] * scale;
+            qv[ks][4 + e] = c[e] * scale;
+            mq = fmaxf(mq, fmaxf(fabsf(qv[ks][e]), fabsf(qv[ks][4 + e])));
+        }
+    }
+    const float sq = pow2_scale(wave_max(mq));
+    f16x8 qf[4][2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) split8_h(qv[ks], sq, qf[ks][0], qf[ks][1]);
+
+    // one chunk's K / V rows in registers: 2 + 2 float4 per thread (zeros past the band's last key)
+    f32x4 kr[2], vr[2];
+    auto fetch = [&](int c0) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int idx = tid + q * 256, r = idx >> 4, c = (idx & 15) * 4, j = c0 + r;
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            kr[q] = z;
+            vr[q] = z;
+            if (j <= kend) {
+                kr[q] = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + H * D + h * D + c);
+                vr[q] = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + 2 * H * D + h * D + c);
+            }
+        }
+    };
+    auto chunk_max = [&]() {
+        float a = 0.0f, v = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                a = fmaxf(a, fabsf(kr[q][e]));
+                v = fmaxf(v, fabsf(vr[q][e]));
+            }
+        a = wave_max(a);
+        v = wave_max(v);
+        if (lane == 0) {
+            red[0][wave] = a;
+            red[1][wave] = v;
+        }
+    };
+    f32x16 o[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    float svc = 0.0f;  // the V scale o is held at (0: no chunk yet)
+    fetch(kstart);
+    chunk_max();
+    for (int c0 = kstart; c0 <= kend; c0 += KC) {
+        // the previous chunk's fragment reads are done; red holds this chunk's maxima.  The explicit wait: hipcc
+        // emits no lgkmcnt(0) before this barrier on the loop's back edge, so another SIMD's wave could read red
+        // before this wave's write of it has landed (seen as run-to-run differences on real activations)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+        const float sk = pow2_scale(fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3])));
+        const float sv = pow2_scale(fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3])));
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int idx = tid + q * 256, r = idx >> 4, c = (idx & 15) * 4;
+            typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+            f16x4 h0, h1;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float t = kr[q][e] * sk;
+                h0[e] = (_Float16)t;
+                h1[e] = (_Float16)(t - (float)h0[e]);
+            }
+            *reinterpret_cast<f16x4*>(Ks + r * KLD + c) = h0;
+            *reinterpret_cast<f16x4*>(Ks + KPL + r * KLD + c) = h1;
+            const int pr = vt_key_pos(r);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float t = vr[q][e] * sv;
+                const _Float16 a0 = (_Float16)t;
+                Vt[(c + e) * VLD + pr] = a0;
+                Vt[VPL + (c + e) * VLD + pr] = (_Float16)(t - (float)a0);
+            }
+        }
+        __syncthreads();  // the chunk image is complete (and red is read)
+        const bool more = c0 + KC <= kend;
+        if (more) fetch(c0 + KC);
+        if (qw < T && c0 <= kend_w && c0 + KC - 1 > qw - window) {
+            float ofac = 1.0f;
+            if (svc == 0.0f || sv < svc) {
+                ofac = svc == 0.0f ? 1.0f : sv / svc;
+                svc = sv;
+            }
+            attn_chunk_h16<KLD, KPL, VLD, VPL>(o, m, l, qf, Ks, Vt, c0, qw, qi, kend_w, window, hf, col,
+                                               1.0f / (sk * sq), ofac, 16384.0f * (svc / sv));
+        }
+        if (more) chunk_max();
+    }
+    __syncthreads();  // the chunk image is dead: the output staging reuses the LDS
+    float* ow = reinterpret_cast<float*>(lds) + wave * 32 * LDO;
+    const float inv = (l > 0.f) ? 1.0f / (16384.0f * svc) / l : 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            ow[col * LDO + d] = o[t][r] * inv;
+        }
+    float mx = 0.0f;
+    for (int qq = 0; qq < 32; ++qq) {
+        const int q = qw + qq;
+        if (q < T)
+            store_act(out, outp, pstride, outns, ((long long)b * T + q) * (H * D) + h * D + lane,
+                      ow[qq * LDO + lane], oscale, &mx);
+    }
+    amax_commit(oamax, mx);
+}
+
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window, float scale,
                             hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
-                            unsigned* oamax) {
-    if (D != 64 || (outns != 0 && !outp) || (oscale > 0.0f && outns != 2)) return hipErrorInvalidValue;
-    if (T <= 256 && oscale > 0.0f && outns == 2) {  // fp16-plane output: the PREC_F16X3 engine
+                            unsigned* oamax, bool h16) {
+    if (D != 64 || (outns != 0 && !outp) || (outns == 0 && !out) || (oscale > 0.0f && outns != 2)) return hipErrorInvalidValue;
+    if (h16 && T <= 256) {  // fp16-plane output (the engine's plane path at these lengths)
+        if (!(oscale > 0.0f && outns == 2)) return hipErrorInvalidValue;
         hipLaunchKernelGGL(attention_t256_h16_kernel, dim3(H, batch), dim3(512), 0, s, qkv, T, H, window, scale, outp,
                            out_pstride, oscale, oamax);
+        return hipGetLastError();
+    }
+    if (h16) {  // T > 256: fp16-plane output, or fp32 for clips too long for the plane buffers
+        hipLaunchKernelGGL(attention_band_h16_kernel, dim3((T + 127) / 128, H, batch), dim3(256), 0, s, qkv, out, T, H,
+                           window, scale, outp, out_pstride, outns, oscale, oamax);
         return hipGetLastError();
     }
     if (T <= 256) {
@@ -658,6 +841,17 @@ hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int 
     dim3 grid((T + 127) / 128, H, batch);
     hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, qkv, out, T, H, window, scale, outp, out_pstride,
                        outns, oscale, oamax);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(64) void set_io_kernel(void** io, const float* audio, int32_t* codes) {
+    if (threadIdx.x == 0) {
+        io[0] = const_cast<float*>(audio);
+        io[1] = codes;
+    }
+}
+hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStream_t s) {
+    hipLaunchKernelGGL(set_io_kernel, dim3(1), dim3(64), 0, s, io, audio, codes);
     return hipGetLastError();
 }
 
@@ -769,11 +963,12 @@ __device__ __forceinline__ RvqWork rvq_work(const RvqArgs& p, int nsl) {
 }
 
 __device__ __forceinline__ void rvq_store_code(const RvqArgs& p, int level, long long f, int ix) {
+    int32_t* codes = io_pointer(p.codes_ref, p.codes);
     if (p.frames_per_item > 0) {
         const long long bb = f / p.frames_per_item, t = f % p.frames_per_item;
-        p.codes[(bb * p.levels + level) * p.frames_per_item + t] = ix;
+        codes[(bb * p.levels + level) * p.frames_per_item + t] = ix;
     } else {
-        p.codes[(long long)level * p.frames + f] = ix;
+        codes[(long long)level * p.frames + f] = ix;
     }
 }
 

@@ -597,6 +597,7 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
     float* aud = reinterpret_cast<float*>(slab + 2 * SPL);
 
     const long long T = p.T;
+    const float* __restrict__ audio = io_pointer(p.audio_ref, p.audio);
     const unsigned tpi = (unsigned)((T + 31) >> 5);  // tiles per item (host checks B x tpi < 2^32)
     const unsigned long long NT = (unsigned long long)tpi * p.batch;
     const unsigned long long W = (unsigned long long)gridDim.x * NW;
@@ -611,7 +612,7 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
     auto aload = [&](unsigned gg) {
         const unsigned bb = gg / tpi;
         const long long pos = (long long)(gg - bb * tpi) * 32 - 8 + lane;
-        return (lane < AUD && pos >= 0 && pos < T) ? p.audio[(long long)bb * T + pos] : 0.0f;
+        return (lane < AUD && pos >= 0 && pos < T) ? audio[(long long)bb * T + pos] : 0.0f;
     };
     // x0^T for the tile's 32 steps (lane column j = step t0 + j) from its audio window value av, + b0
     auto conv0 = [&](float av, f32x16 (&x0)[2]) {

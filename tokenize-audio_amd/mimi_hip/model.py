@@ -264,6 +264,14 @@ class MimiHipModel:
         """Encodes that took the f16x3 overflow fallback (per-item re-encode, bf16x6 where an item overflows)."""
         return int(self._lib.mimi_f16_reruns(self._h))
 
+    def set_graphs(self, enable: bool = True):
+        """hipGraph replay of repeated f16x3 encode shapes (default on; identical codes, fewer launches)."""
+        _lib.check(self._lib.mimi_set_graphs(self._h, int(enable)))
+
+    @property
+    def graph_replays(self) -> int:
+        return int(self._lib.mimi_graph_replays(self._h))
+
     def set_profiling(self, enable: bool = True):
         _lib.check(self._lib.mimi_set_profiling(self._h, int(enable)))
 
