@@ -187,6 +187,11 @@ static long long tiles(const GemmArgs& a, int bm, int bn) {
 
 template <int EPI, int OUTP, int TAG>
 static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
+    // small grids: long K (down_s3, K = 8192) retires 2 pair stages per barrier from a 4-deep ring (batch 1:
+    // 100 -> 83 us in the engine; the same grouping made the K <= 3072 transformer GEMMs slower there although
+    // faster in tools/gemm_bench.hip with warm caches, profiles/r2_gemm_bench_kg.log); shorter K: 2-stage ring
+    if (pair_ok(a) && tiles(a, 256, 128) < kSmallGrid && a.K >= 4096)
+        return run_planes<64, 64, 2, 2, 2, 4, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR | FL_KG2, true>(a, s);
     if (pair_ok(a) && tiles(a, 256, 128) < kSmallGrid)
         return run_planes<64, 64, 2, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR, true>(a, s);
     if (pair_ok(a)) return run_planes<256, 128, 4, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR | FL_PERSIST, true>(a, s);

@@ -30,6 +30,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
 }
 #endif
 
+// s_waitcnt vmcnt(later * PM) for a run-time later in [0, L] (the immediate must be a constant): retires the oldest
+// stage of a loading wave while `later` stages of PM pieces each stay in flight
+template <int PM, int L>
+__device__ __forceinline__ void wait_stages(int later) {
+    if constexpr (L == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        if (later >= L)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * PM) : "memory");
+        else
+            wait_stages<PM, L - 1>(later);
+    }
+}
+
 // (XCD-aware) linear workgroup index -> logical tile index; bijective for any count.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -60,17 +74,17 @@ __device__ __forceinline__ int chunk_swz(int row) {
 //   MF:     MFMA shape, 32 (v_mfma_f32_32x32x16_bf16) or 16 (v_mfma_f32_16x16x32_bf16, BK = 32).
 //   F16:    the planes are fp16 (2 planes, 3 products, PREC_F16X3) scaled by powers of two; the accumulator is
 //           multiplied by p.unscale before the epilogue; fp16 output planes hold out * p.out_scale.
-//   FL:     FL_READFIRST -- a K step's first fragment reads are issued before its DMA refill;
-//           FL_PRIO -- s_setprio(1) over the MFMA section;
+//   FL:     FL_PRIO -- s_setprio(1) over the MFMA section;
 //           FL_PAIR -- tap pairs of a k = 2s conv (the down convs): taps j and j+s of row m read the same
 //           input line (A(m, (j+s)Cin + c) = A(m+1, j Cin + c)), so a stage holds ONE A image of BM + RPP rows
 //           and the B images of both taps, and the second K step reads the A image one row down.  A's
 //           LDS-DMA bytes halve (stage = 2 K steps; KOrder visits the chains' first taps only).
+//           FL_KG2 / FL_KG4 -- 2 / 4 ring stages per barrier (below);
 //           FL_PERSIST -- a grid of (CUs x resident workgroups) loops over the tiles (tile = blockIdx.x + i *
 //           gridDim.x, the XCD map applied to the tile index): a tile's epilogue stores drain while the same
 //           workgroup already streams its next tile's first stages (the barrier between them waits for LDS
 //           only, never for the stores), and no workgroup launch / ring fill per tile.
-enum : int { FL_READFIRST = 1, FL_PRIO = 2, FL_PAIR = 4, FL_PERSIST = 8 };
+enum : int { FL_PRIO = 2, FL_PAIR = 4, FL_PERSIST = 8, FL_KG2 = 16, FL_KG4 = 32 };
 // tuning diagnostics (tools/gemm_bench.hip only; results are garbage): no DMA refills after the prologue / no MFMAs
 enum : int { FL_DIAG_NODMA = 64, FL_DIAG_NOMMA = 128 };
 
@@ -86,6 +100,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     constexpr int TN = BN / WN / MF;
     constexpr int KSUB = MF == 32 ? BK / 16 : BK / 32;  // MFMA k-steps per K step
     constexpr bool PAIR = (FL & FL_PAIR) != 0;
+    constexpr int KG = (FL & FL_KG4) ? 4 : (FL & FL_KG2) ? 2 : 1;  // ring stages per barrier
     constexpr int XR = PAIR ? RPP : 0;           // extra A image rows (PAIR: row BM, rounded to a piece)
     constexpr int NB = PAIR ? 2 : 1;             // B images (K steps) per stage
     constexpr int AR = BM + XR;                  // A image rows
@@ -100,8 +115,8 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     static_assert(MF == 32 || MF == 16, "MFMA shape");
     static_assert(TM >= 1 && TN >= 1 && KSUB >= 1, "tile");
     static_assert(NS * BM % RPP == 0 && NS * BN % RPP == 0, "whole pieces");
-    static_assert(STAGES >= 2 && STAGES <= 4, "stages");
-    static_assert(PMAX * (STAGES - 2) <= 63, "vmcnt range");
+    static_assert(STAGES >= 2 * KG && STAGES <= 8, "stages");
+    static_assert(PMAX * (STAGES - 2 * KG) <= 63, "vmcnt range");
     static_assert(EPI != EPI_ROPE || (MF == 32 ? TN % 2 == 0 : TN % 4 == 0), "rope pairs (d, d+32) in one lane");
     static_assert(!F16 || NS == 2, "fp16 planes: 2 planes, 3 products");
     // OUTP: 0 = fp32 C only; 2/3 = that many bf16 planes of the output (+ fp32 C when p.C is set);
@@ -239,46 +254,48 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         }
     };
 
+    // KG ring stages per barrier (FL_KG2 / FL_KG4): the loaders retire a group of KG stages at once and the
+    // compute waves run its KG K steps back to back (their fragment reads free to overlap the previous step's
+    // MFMAs); the ring keeps the next group(s) in flight, STAGES >= 2 KG
     if (loader) {
 #pragma unroll
-        for (int s = 0; s < STAGES - 1; ++s)
+        for (int s = 0; s < STAGES - KG; ++s)
             if (s < KT) issue(s);
     }
 
-    for (int kt = 0; kt < KT; ++kt) {
+    for (int kt = 0; kt < KT; kt += KG) {
+        const int ng = min(KG, KT - kt);  // stages in this group
         if (loader) {
-            // retire this wave's pieces of stage kt; the later stages stay in flight
-            const int later = min(STAGES - 2, KT - 1 - kt);
-            if (STAGES >= 4 && later >= 2) {
-                if (PMAX == PMIN || npieces == PMAX)
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PMAX) : "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PMIN) : "memory");
-            } else if (STAGES >= 3 && later >= 1) {
-                if (PMAX == PMIN || npieces == PMAX)
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PMAX) : "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PMIN) : "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+            // retire this wave's pieces of the group's stages; the stages issued after them stay in flight
+            const int later = min(KT, kt + STAGES - KG) - (kt + ng);
+            if (PMAX == PMIN || npieces == PMAX)
+                wait_stages<PMAX, STAGES - 2 * KG>(later);
+            else
+                wait_stages<PMIN, STAGES - 2 * KG>(later);
         }
         __builtin_amdgcn_s_barrier();
-        const __bf16* As = lds + (kt % STAGES) * STG;
-        const __bf16* Bs = As + NS * APL;
-        bf16x8 af[NS][TM], bf[NS][TN];
-        if ((FL & FL_READFIRST) && compute) read_frags(As, Bs, 0, af, bf);
-        // the stage consumed in step kt-1 is free: refill it with step kt + STAGES - 1
-        if (!(FL & FL_DIAG_NODMA) && loader && kt + STAGES - 1 < KT) issue((kt + STAGES - 1) % STAGES);
+        // the group consumed before this barrier is free: refill its slots with the stages STAGES - KG ahead
+        if (!(FL & FL_DIAG_NODMA) && loader) {
+#pragma unroll
+            for (int q = 0; q < KG; ++q)
+                if (kt + STAGES - KG + q < KT) issue((kt + STAGES - KG + q) % STAGES);
+        }
         if (!compute) continue;
         if (FL & FL_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int img = 0; img < NB; ++img)
+        for (int q = 0; q < KG; ++q) {
+            if (q >= ng) break;
+            const __bf16* As = lds + ((kt + q) % STAGES) * STG;
+            const __bf16* Bs = As + NS * APL;
+            bf16x8 af[NS][TM], bf[NS][TN];
 #pragma unroll
-            for (int ks = 0; ks < KSUB; ++ks) {
-                if (!(FL & FL_READFIRST) || ks > 0 || img > 0) read_frags(As, Bs, ks, af, bf, img);
-                if (!(FL & FL_DIAG_NOMMA)) mma_split<NS, TM, TN, F16>(acc, af, bf);
-            }
+            for (int img = 0; img < NB; ++img)
+#pragma unroll
+                for (int ks = 0; ks < KSUB; ++ks) {
+                    read_frags(As, Bs, ks, af, bf, img);
+                    if (!(FL & FL_DIAG_NOMMA)) mma_split<NS, TM, TN, F16>(acc, af, bf);
+                }
+        }
         if (FL & FL_PRIO) __builtin_amdgcn_s_setprio(0);
     }
 

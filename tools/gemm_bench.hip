@@ -119,16 +119,24 @@ int main(int argc, char** argv) {
         {"final", 1024, 3, 1, 250, 250, 32, 512},        {"fc1", 512, 1, 1, 8000, 8000, 1, 2048},
         {"fc2", 2048, 1, 1, 8000, 8000, 1, 512},         {"qkv", 512, 1, 1, 250, 250, 32, 1536},
         {"o_proj", 512, 1, 1, 8000, 8000, 1, 512},
+        // batch 1 (launch / latency bound)
+        {"b1_fc2", 2048, 1, 1, 250, 250, 1, 512},        {"b1_fc1", 512, 1, 1, 250, 250, 1, 2048},
+        {"b1_qkv", 512, 1, 1, 250, 250, 1, 1536},        {"b1_oproj", 512, 1, 1, 250, 250, 1, 512},
+        {"b1_down_s3", 512, 16, 8, 2000, 250, 1, 1024},  {"b1_final", 1024, 3, 1, 250, 250, 1, 512},
+        {"b1_down_s1", 128, 10, 5, 60000, 12000, 1, 256}, {"b1_down_s0", 64, 8, 4, 240000, 60000, 1, 128},
     };
     Variant vars[] = {
-        {"h2 256x128 8w mf16 s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
-        {"pair PERSIST", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
-        {"STREAM pair 256x128 +4ld s2", launch_st<256, 128, 4, 2, 2, 4, FL_PAIR>, 64, 12, true},
-        {"STREAM pair 256x128 0ld s2", launch_st<256, 128, 4, 2, 2, 0, FL_PAIR>, 64, 12, true},
-        {"STREAM 256x128 0ld s3", launch_st<256, 128, 4, 2, 3, 0, 0>, 32, 12},
-        {"STREAM 128x128 0ld s2", launch_st<128, 128, 4, 2, 2, 0, 0>, 32, 12},
-        {"STREAM 128x128 +4ld s3", launch_st<128, 128, 2, 2, 3, 4, 0>, 32, 12},
-        {"STREAM pair 128x128 +4ld s2", launch_st<128, 128, 2, 2, 2, 4, FL_PAIR>, 64, 12, true},
+        {"ref 64x64 4w+4ld s4", launch_pl<64, 64, 2, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
+        {"pair ref 64x64 4w+4ld s2", launch_pl<64, 64, 2, 2, 2, 2, 4, 32, 16, FL_PAIR, true>, 64, 12, true},
+        {"64x64 4w+4ld s4 KG2", launch_pl<64, 64, 2, 2, 2, 4, 4, 32, 16, FL_KG2, true>, 32, 12},
+        {"64x64 4w+4ld s8 KG2", launch_pl<64, 64, 2, 2, 2, 8, 4, 32, 16, FL_KG2, true>, 32, 12},
+        {"64x64 4w+4ld s8 KG4", launch_pl<64, 64, 2, 2, 2, 8, 4, 32, 16, FL_KG4, true>, 32, 12},
+        {"64x64 4w s8 KG4", launch_pl<64, 64, 2, 2, 2, 8, 0, 32, 16, FL_KG4, true>, 32, 12},
+        {"pair 64x64 4w+4ld s4 KG2", launch_pl<64, 64, 2, 2, 2, 4, 4, 32, 16, FL_PAIR | FL_KG2, true>, 64, 12, true},
+        {"128x128 8w s2 (fc1)", launch_pl<128, 128, 4, 2, 2, 2, 0, 32, 16, 0, true>, 32, 12},
+        {"128x128 8w s4 KG2", launch_pl<128, 128, 4, 2, 2, 4, 0, 32, 16, FL_KG2, true>, 32, 12},
+        {"128x128 4w+4ld s4 KG2", launch_pl<128, 128, 2, 2, 2, 4, 4, 32, 16, FL_KG2, true>, 32, 12},
+        {"256x128 8w s3 (k3)", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
