@@ -167,10 +167,11 @@ def north_star_groups(prof, steps, pmc_path):
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f).get("kernels", {})
+    base = lambda s: s.split("#")[0]  # noqa: E731  ("fc2#2": the same stage on a second kernel symbol)
     groups = {
-        "conv_stack": [s for s in prof if s.startswith(("res", "down_s", "final"))],
-        "transformer": [s for s in prof if s in ("layernorm", "qkv", "attention", "o_proj", "fc1", "fc2")],
-        "quantizer": [s for s in prof if s in ("downsample", "input_proj", "rvq")],
+        "conv_stack": [s for s in prof if base(s).startswith(("res", "down_s", "final"))],
+        "transformer": [s for s in prof if base(s) in ("layernorm", "qkv", "attention", "o_proj", "fc1", "fc2")],
+        "quantizer": [s for s in prof if base(s) in ("downsample", "input_proj", "rvq")],
     }
     out = {}
     for g, stages in groups.items():
@@ -421,7 +422,10 @@ def main():
         roof, whole, pmc_path = roofline_from_profile(prof, args.steps)
         result["roofline"] = roof
         result["whole_encode"] = whole
-        result["stages_ms_per_step"] = {s: round(v["ms"] / args.steps, 3) for s, v in prof.items()}
+        stages = {}
+        for s_, v in prof.items():  # per stage, summed over the kernel symbols that run it
+            stages[s_.split("#")[0]] = stages.get(s_.split("#")[0], 0.0) + v["ms"] / args.steps
+        result["stages_ms_per_step"] = {s_: round(v, 3) for s_, v in stages.items()}
         result["north_star"] = north_star_groups(prof, args.steps, pmc_path)
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
         cb_batch = args.batch if wl.kind == "batch" else 1

@@ -143,6 +143,9 @@ int64_t mimi_f16_reruns(const mimi_engine* e);
  * Never used while profiling or taps are on.  enable = 0 drops the captured graphs.  Replays so far: */
 int mimi_set_graphs(mimi_engine* e, int32_t enable);
 int64_t mimi_graph_replays(const mimi_engine* e);
+/* MIMI_PRECISION_F16X3 diagnostics: per plane tensor (64-char names), its fixed activation scale and the max|x|
+ * of the last waited encode (-1: not produced by it); an overflow is max * scale >= 2^15. */
+int mimi_act_scales(mimi_engine* e, int32_t max_n, char* names, float* scales, float* last_max, int32_t* n);
 
 /* Frames produced for `length` samples with the default config (reference float32 length math). */
 int64_t mimi_encoded_length(int64_t length);

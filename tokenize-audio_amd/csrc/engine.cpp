@@ -230,6 +230,9 @@ struct mimi_engine {
     std::vector<DevXfmr> xf;
     DevConv ds;
     float* inproj = nullptr;  // [2*vq][hidden]
+    void* inproj_h = nullptr;   // its fp16 planes (PREC_F16X3)
+    float inproj_hs = 1.0f;
+    float* ds_fix = nullptr;    // [2][hidden in][hidden out]: W_0 + W_1 and W_3 of the downsample (replicate edges)
     float* cb_rows = nullptr;
     float* cb_frag = nullptr;
     float* cb_norm = nullptr;
@@ -276,6 +279,7 @@ struct mimi_engine {
     int64_t next_ticket = 1;
     size_t item_codes_cap = 0;
     int f16_reruns = 0;             // encodes that took the overflow fallback (diagnostic)
+    std::vector<float> last_amax;   // per-slot max|x| of the last waited f16x3 encode (diagnostic)
     bool profiling = false;
     std::vector<ProfEvent> pending;  // recorded since last read; first event of each encode named ""
     std::vector<hipEvent_t> event_pool;
@@ -506,6 +510,7 @@ extern "C" int mimi_create(const mimi_config* cfg, int device, mimi_engine** out
     HIP_TRY(hipEventCreateWithFlags(&e->ws_free, hipEventDisableTiming));
     HIP_TRY(hipMalloc(&e->amax_dev, ((size_t)kMaxActSlots * AMAX_SLOT_WORDS + kMaxActSlots) * sizeof(unsigned)));
     e->amax_red = e->amax_dev + (size_t)kMaxActSlots * AMAX_SLOT_WORDS;
+    HIP_TRY(hipMemset(e->amax_dev, 0, ((size_t)kMaxActSlots * AMAX_SLOT_WORDS + kMaxActSlots) * sizeof(unsigned)));
     HIP_TRY(hipHostMalloc(&e->amax_host, kMaxActSlots * sizeof(unsigned), hipHostMallocDefault));
     build_expected(e.get());
     *out = e.release();
@@ -929,6 +934,19 @@ extern "C" int mimi_finalize(mimi_engine* e) {
         }
     }
     if ((rc = make_conv(e, e->ds, "downsample.conv.", h, h, c.downsample_kernel, c.downsample_stride, false))) return rc;
+    if (c.downsample_kernel == 4 && c.downsample_stride == 2) {  // replicate-edge terms of the planes downsample
+        std::vector<float>* w;
+        if ((rc = get_w(e, "downsample.conv.weight", &w))) return rc;
+        const std::vector<float> wl = relayout_conv(*w, h, h, 4);  // [co][kk*h + ci]
+        std::vector<float> fix((size_t)2 * h * h);
+        for (int co = 0; co < h; ++co)
+            for (int ci = 0; ci < h; ++ci) {
+                const size_t r = (size_t)co * 4 * h;
+                fix[(size_t)ci * h + co] = wl[r + ci] + wl[r + h + ci];  // [edge][ci][co]
+                fix[(size_t)h * h + (size_t)ci * h + co] = wl[r + 3 * h + ci];
+            }
+        if ((rc = upload(e, &e->ds_fix, fix))) return rc;
+    }
     {
         std::vector<float>*ps, *pa;
         if ((rc = get_w(e, "quantizer.semantic_residual_vector_quantizer.input_proj.weight", &ps)) ||
@@ -936,7 +954,7 @@ extern "C" int mimi_finalize(mimi_engine* e) {
             return rc;
         std::vector<float> both(*ps);
         both.insert(both.end(), pa->begin(), pa->end());
-        if ((rc = upload(e, &e->inproj, both))) return rc;
+        if ((rc = upload(e, &e->inproj, both)) || (rc = upload_f16(e, &e->inproj_h, both, &e->inproj_hs))) return rc;
     }
     // codebooks: as many consecutive levels as the checkpoint provides (32 for kyutai/mimi)
     const int n = c.codebook_size, D = c.codebook_dim;
@@ -1473,6 +1491,9 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     // ---- transformer (x in t0) ----
     const int64_t rows = (int64_t)B * T;
     const int H = c.num_attention_heads, Dh = c.head_dim;
+    // f16x3: downsample + input projections on fp16 planes too (zero-padded GEMM + replicate-edge fix)
+    const bool ds_planes = h16 && e->ds_fix && e->inproj_h && c.downsample_kernel == 4 && c.downsample_stride == 2;
+    Act dsin, dsouta;
     double att_flops = 0;
     for (int64_t i = 0; i < T; ++i) att_flops += 4.0 * Dh * std::min<int64_t>(i + 1, c.sliding_window);
     att_flops *= (double)B * H;
@@ -1544,6 +1565,12 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         a2.scale = x.ls2;
         if (ns) planes_in(a2, w.ff, rows * (long long)c.intermediate_size);
         use_h(a2, x.w2_h, x.w2_hs, ffa);
+        if (ds_planes && l == c.num_hidden_layers - 1) {  // + planes of the encoder output: the downsample's A
+            a2.Cp = w.t1;
+            a2.c_pstride = nact;
+            dsin = new_act("ds.in");
+            out_act(a2, dsin);
+        }
         LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname, prec), "fc2");
         rec.mark("fc2", gemm_flops(a2), gemm_bytes(a2, true), kname);
         snprintf(nm, sizeof nm, "xfmr%d", l);
@@ -1553,12 +1580,28 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     // ---- downsample (replicate pad) + input projections + RVQ ----
     const int64_t T2 = p.frames12;
     GemmArgs ad = conv_args(e->ds, w.t0, T, w.dsout, T2, B);
+    if (ds_planes) {
+        planes_in(ad, w.t1, rows * Hd);
+        use_h(ad, e->ds.wh, e->ds.wscale, dsin);
+        ad.Cp = w.att;  // planes of the downsample output (the input projection's A); fp32 C beside
+        ad.c_pstride = (long long)B * T2 * Hd;
+        dsouta = new_act("ds.out");
+        out_act(ad, dsouta);
+    }
     LAUNCH_TRY(launch_gemm(ROLE_DOWNSAMPLE, ad, s, &kname, prec), "downsample");
+    if (ds_planes)
+        LAUNCH_TRY(launch_ds_edge_fix(w.t0, e->ds_fix, w.dsout, w.att, ad.c_pstride, dsouta.scale, dsouta.amax, B,
+                                      (int)T, (int)T2, Hd, Hd, s),
+                   "downsample edges");
     rec.mark("downsample", gemm_flops(ad), gemm_bytes(ad, false), kname);
     if ((rc = save_tap(e, "downsample", w.dsout, B, T2, Hd, s))) return rc;
     const int Dq = c.vq_hidden_dim;
     GemmArgs ap = linear_args(w.dsout, (int64_t)B * T2, Hd, e->inproj, 2 * Dq, w.proj);
-    LAUNCH_TRY(launch_gemm(ROLE_INPROJ, ap, s, &kname), "input_proj");
+    if (ds_planes) {
+        planes_in(ap, w.att, (long long)B * T2 * Hd);
+        use_h(ap, e->inproj_h, e->inproj_hs, dsouta);
+    }
+    LAUNCH_TRY(launch_gemm(ROLE_INPROJ, ap, s, &kname, ds_planes ? PREC_F16X3 : PREC_F32), "input_proj");
     rec.mark("input_proj", gemm_flops(ap), gemm_bytes(ap, false), kname);
     if ((rc = save_tap(e, "proj", w.proj, B, T2, 2 * Dq, s))) return rc;
     if ((rc = run_rvq(e, w.proj, (int64_t)B * T2, K, codes, (int)T2, w.rvq, s, rec))) return rc;
@@ -1756,9 +1799,9 @@ static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int
     }
     e->capturing = true;
     int rc = MIMI_OK;
-    if (hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), cs) != hipSuccess)
-        rc = MIMI_ERR_HIP;
-    if (!rc) rc = encode_pass(e, audio, B, L, K, codes, cs, PREC_F16X3);
+    // (no maxima reset node: amax_reduce_kernel leaves every sub-slot at 0 as it reads it, so a replay starts
+    // from the zeros the previous encode's fold left behind)
+    rc = encode_pass(e, audio, B, L, K, codes, cs, PREC_F16X3);
     if (!rc && launch_amax_reduce(e->amax_dev, (int)e->slot_of.size(), e->amax_red, cs) != hipSuccess) rc = MIMI_ERR_HIP;
     e->capturing = false;
     hipGraph_t g = nullptr;
@@ -1885,9 +1928,11 @@ static int encode_wait_locked(mimi_engine* e, int64_t ticket) {
     P->id = 0;
     HIP_TRY(hipEventSynchronize(q.done));
     bool ovf = false;
+    if (q.h16) e->last_amax.assign(q.nslots, 0.0f);
     for (int i = 0; q.h16 && i < q.nslots; ++i) {
         float a;
         std::memcpy(&a, &q.amax[i], 4);
+        e->last_amax[i] = a;
         if (std::isfinite(a) && a * e->act_scale[i] >= kF16Overflow) ovf = true;
     }
     return ovf ? overflow_fallback(e, q.audio, q.B, q.L, q.K, q.codes, q.s) : MIMI_OK;
@@ -2026,6 +2071,26 @@ extern "C" int mimi_set_graphs(mimi_engine* e, int32_t enable) {
 }
 
 extern "C" int64_t mimi_graph_replays(const mimi_engine* e) { return e ? e->graph_replays : -1; }
+
+extern "C" int mimi_act_scales(mimi_engine* e, int32_t max_n, char* names, float* scales, float* last_max,
+                               int32_t* n) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    int i = 0;
+    for (const auto& kv : e->slot_of) {
+        const int slot = kv.second;
+        if (i >= max_n) break;
+        if (names) {
+            std::strncpy(names + 64 * i, kv.first.c_str(), 63);
+            names[64 * i + 63] = 0;
+        }
+        if (scales) scales[i] = slot < (int)e->act_scale.size() ? e->act_scale[slot] : 0.0f;
+        if (last_max) last_max[i] = slot < (int)e->last_amax.size() ? e->last_amax[slot] : -1.0f;
+        ++i;
+    }
+    if (n) *n = i;
+    return MIMI_OK;
+}
 
 extern "C" int mimi_get_precision(const mimi_engine* e) { return e ? e->precision : -1; }
 

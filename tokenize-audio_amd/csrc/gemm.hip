@@ -220,9 +220,22 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
                     return run_planes<64, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, 0, true>(a, s);
                 break;
             case ROLE_FC2:
+                if (a.Cp) {  // the last layer: fp32 residual stream + its planes (the downsample's input)
+                    if (tiles(a, 128, 128) < kSmallGrid)
+                        return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 2, 8, 4, 32, 16, 0, true>(a, s);
+                    return run_planes<128, 128, 2, 2, 2, 3, EPI_SCALE_RES, 2, 8, 4, 32, 16, 0, true>(a, s);
+                }
                 if (tiles(a, 128, 128) < kSmallGrid)
                     return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 0, 8, 4, 32, 16, 0, true>(a, s);
                 break;
+            case ROLE_DOWNSAMPLE:  // zero-padded here; engine.cpp adds the replicate rows (launch_ds_edge_fix)
+                if (tiles(a, 128, 128) < kSmallGrid)
+                    return run_planes<64, 64, 2, 2, 2, 4, EPI_NONE, 2, 9, 4, 32, 16, 0, true>(a, s);
+                return run_planes<128, 128, 4, 2, 2, 2, EPI_NONE, 2, 9, 0, 32, 16, 0, true>(a, s);
+            case ROLE_INPROJ:
+                if (tiles(a, 128, 128) < kSmallGrid)
+                    return run_planes<64, 64, 2, 2, 2, 4, EPI_NONE, 0, 10, 4, 32, 16, 0, true>(a, s);
+                return run_planes<128, 128, 4, 2, 2, 2, EPI_NONE, 0, 10, 0, 32, 16, 0, true>(a, s);
             case ROLE_RES3P:
                 if (tiles(a, 128, 128) < kSmallGrid)
                     return run_planes<64, 64, 2, 2, 2, 3, EPI_BIAS_ELU, 2, 12, 4, 32, 16, 0, true>(a, s);

@@ -83,12 +83,13 @@ __device__ __forceinline__ void store_act8(void* planes, long long pstride, int 
     }
 }
 
-// max over the wave of the lanes' running max|x|, max-ed into one of AMAX_SUB sub-slots of the tensor's slot
-// (picked by workgroup, AMAX_STRIDE words apart) -- only when it exceeds what the sub-slot already holds, so
-// the thousands of waves of a launch do not serialise on one address (atomics execute at the memory side).
-// A stale read can only cost an unneeded atomic (the stored value only grows).  Non-negative floats order as
-// their bit patterns.  Every lane of the wave must call it; amax == null: no-op.  amax_reduce_kernel folds the
-// sub-slots.
+// max over the wave of the lanes' running max|x|, max-ed by one atomic per wave into one of AMAX_SUB sub-slots
+// of the tensor's slot (picked by workgroup, AMAX_STRIDE words apart), so the thousands of waves of a launch do
+// not serialise on one address.  No cached pre-read of the sub-slot: an earlier version skipped the atomic when
+// a plain read showed a larger value, and in hipGraph replays such reads (and the fold's plain reads) could see
+// another XCD's stale line -- spurious maxima, one spurious overflow fallback.  Non-negative floats order as
+// their bit patterns.  Every lane of the wave must call it; amax == null: no-op.  amax_reduce_kernel folds (and
+// resets) the sub-slots.
 constexpr int AMAX_SUB = 64, AMAX_STRIDE = 16, AMAX_SLOT_WORDS = AMAX_SUB * AMAX_STRIDE;
 __device__ __forceinline__ void amax_commit(unsigned* amax, float mx) {
     if (!amax) return;
@@ -96,8 +97,7 @@ __device__ __forceinline__ void amax_commit(unsigned* amax, float mx) {
     for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
     if ((threadIdx.x & 63) == 0 && mx > 0.0f) {
         unsigned* a = amax + ((blockIdx.x + 7 * blockIdx.y + 13 * blockIdx.z) & (AMAX_SUB - 1)) * AMAX_STRIDE;
-        const unsigned u = __float_as_uint(mx);
-        if (*reinterpret_cast<volatile unsigned*>(a) < u) atomicMax(a, u);
+        atomicMax(a, __float_as_uint(mx));  // device scope, at the memory side (no cached pre-read: see amax_reduce)
     }
 }
 
@@ -113,8 +113,8 @@ __device__ __forceinline__ T* io_pointer(T* const* ref, T* direct) {
 // io[0] = audio, io[1] = codes (the pointers of one graph replay)
 hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStream_t s);
 
-// out[i] = max over the AMAX_SUB sub-slots of slot i (one wave per slot)
-hipError_t launch_amax_reduce(const unsigned* amax, int nslots, unsigned* out, hipStream_t s);
+// out[i] = max over the AMAX_SUB sub-slots of slot i (one wave per slot); the sub-slots are left at 0
+hipError_t launch_amax_reduce(unsigned* amax, int nslots, unsigned* out, hipStream_t s);
 
 // Epilogues of the implicit-GEMM conv / linear kernel.
 enum Epi : int {
@@ -244,6 +244,17 @@ hipError_t launch_layernorm(const float* x, const float* g, const float* b, floa
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window,
                             float scale, hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
                             unsigned* oamax, bool h16);
+
+// Replicate-padding fix of the downsample conv (k = 4, s = 2) run as a zero-padded planes GEMM: per item,
+// out[0] += (W_0 + W_1) . x[0] (the 2 left pad rows replicate x[0]) and, when T is odd (one right "extra" pad
+// row), out[F-1] += W_3 . x[T-1]; the fixed rows are re-written as fp32 and as fp16 planes of out * oscale.
+// wfix: fp32 [2][C][N] (W_0 + W_1, W_3, input channel major); x: fp32 [B][T][C]; out: fp32 [B][F][N].
+hipError_t launch_ds_edge_fix(const float* x, const float* wfix, float* out, void* outp, long long out_pstride,
+                              float oscale, unsigned* oamax, int B, int T, int F, int C, int N, hipStream_t s);
+
+// the banded fp16-plane attention at any T (tools/attn_check.hip compares it with the T <= 256 kernel)
+hipError_t launch_attention_band(const float* qkv, int batch, int T, int H, int window, float scale,
+                                 hipStream_t s, void* outp, long long out_pstride, float oscale, unsigned* oamax);
 
 // planes -> fp32 (x0 + x1 [+ x2], or (h0 + h1) / hscale for fp16 planes); used only to materialise per-stage
 // taps of plane-format activations.

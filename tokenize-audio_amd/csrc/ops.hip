@@ -818,6 +818,13 @@ __global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __
     amax_commit(oamax, mx);
 }
 
+hipError_t launch_attention_band(const float* qkv, int batch, int T, int H, int window, float scale,
+                                 hipStream_t s, void* outp, long long out_pstride, float oscale, unsigned* oamax) {
+    hipLaunchKernelGGL(attention_band_h16_kernel, dim3((T + 127) / 128, H, batch), dim3(256), 0, s, qkv, nullptr, T, H,
+                       window, scale, outp, out_pstride, 2, oscale, oamax);
+    return hipGetLastError();
+}
+
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window, float scale,
                             hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
                             unsigned* oamax, bool h16) {
@@ -844,6 +851,57 @@ hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int 
     return hipGetLastError();
 }
 
+// one workgroup per (item, edge, 64 output channels): thread (slice sl of 16, group g of 4 consecutive
+// channels) sums its C/16 terms with 16-B weight loads all in flight at once; the slices are added in a fixed
+// order, then the row and its planes are updated
+__global__ __launch_bounds__(256) void ds_edge_fix_kernel(const float* __restrict__ x, const float* __restrict__ wfix,
+                                                          float* __restrict__ out, void* __restrict__ outp,
+                                                          long long pstride, float oscale, unsigned* __restrict__ oamax,
+                                                          int T, int F, int C, int N) {
+    const int b = blockIdx.x, edge = blockIdx.y;
+    if (edge == 1 && (T & 1) == 0) return;  // no right extra row
+    const int t = edge == 0 ? 0 : T - 1, f = edge == 0 ? 0 : F - 1;
+    const int g = threadIdx.x & 15, sl = threadIdx.x >> 4;
+    const int n0 = blockIdx.z * 64;
+    const int cs = C / 16, c0 = sl * cs;
+    const float* __restrict__ wc = wfix + (long long)edge * C * N + n0 + 4 * g;  // [edge][c][n]
+    const float* __restrict__ xr = x + ((long long)b * T + t) * C;
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 32
+    for (int c = c0; c < c0 + cs; ++c) {
+        const f32x4 w = *reinterpret_cast<const f32x4*>(wc + (long long)c * N);
+        const float xv = xr[c];
+        a.x = __builtin_fmaf(w.x, xv, a.x);
+        a.y = __builtin_fmaf(w.y, xv, a.y);
+        a.z = __builtin_fmaf(w.z, xv, a.z);
+        a.w = __builtin_fmaf(w.w, xv, a.w);
+    }
+    __shared__ float part[16][64];
+    part[sl][4 * g] = a.x;
+    part[sl][4 * g + 1] = a.y;
+    part[sl][4 * g + 2] = a.z;
+    part[sl][4 * g + 3] = a.w;
+    __syncthreads();
+    if (threadIdx.x >= 64) return;  // (wave-uniform: wave 0 finishes)
+    const int lane = threadIdx.x;
+    float sum = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sum += part[q][lane];
+    const long long o = ((long long)b * F + f) * N + n0 + lane;
+    const float v = out[o] + sum;
+    out[o] = v;
+    float mx = 0.0f;
+    if (outp) store_act(nullptr, outp, pstride, 2, o, v, oscale, &mx);
+    if (outp) amax_commit(oamax, mx);
+}
+hipError_t launch_ds_edge_fix(const float* x, const float* wfix, float* out, void* outp, long long out_pstride,
+                              float oscale, unsigned* oamax, int B, int T, int F, int C, int N, hipStream_t s) {
+    if (B <= 0 || T <= 0 || F <= 0 || N % 64 || C % 16 || (outp && !(oscale > 0.0f))) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ds_edge_fix_kernel, dim3(B, 2, N / 64), dim3(256), 0, s, x, wfix, out, outp, out_pstride,
+                       oscale, oamax, T, F, C, N);
+    return hipGetLastError();
+}
+
 __global__ __launch_bounds__(64) void set_io_kernel(void** io, const float* audio, int32_t* codes) {
     if (threadIdx.x == 0) {
         io[0] = const_cast<float*>(audio);
@@ -855,15 +913,18 @@ hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStrea
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(64) void amax_reduce_kernel(const unsigned* __restrict__ amax, unsigned* __restrict__ out) {
-    const unsigned* a = amax + (long long)blockIdx.x * AMAX_SLOT_WORDS;
-    unsigned v = threadIdx.x < AMAX_SUB ? a[threadIdx.x * AMAX_STRIDE] : 0u;
+// Each sub-slot is read AND reset to 0 by one device-scope atomic exchange (at the memory side, like the
+// producers' atomicMax): no XCD's L2 can hand this fold a stale line, and the next encode (or graph replay)
+// starts from zeros without a memset.
+__global__ __launch_bounds__(64) void amax_reduce_kernel(unsigned* __restrict__ amax, unsigned* __restrict__ out) {
+    unsigned* a = amax + (long long)blockIdx.x * AMAX_SLOT_WORDS;
+    unsigned v = threadIdx.x < AMAX_SUB ? atomicExch(a + threadIdx.x * AMAX_STRIDE, 0u) : 0u;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
     if (threadIdx.x == 0) out[blockIdx.x] = v;
 }
 
-hipError_t launch_amax_reduce(const unsigned* amax, int nslots, unsigned* out, hipStream_t s) {
+hipError_t launch_amax_reduce(unsigned* amax, int nslots, unsigned* out, hipStream_t s) {
     if (nslots <= 0) return hipSuccess;
     static_assert(AMAX_SUB <= 64, "one wave per slot");
     hipLaunchKernelGGL(amax_reduce_kernel, dim3(nslots), dim3(64), 0, s, amax, out);

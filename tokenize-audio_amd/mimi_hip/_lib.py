@@ -24,7 +24,7 @@ STATUS_NAMES = {
 # every symbol include/mimi_hip.h declares (tests check the library exports exactly these)
 EXPORTED_SYMBOLS = (
     "mimi_config_default", "mimi_create", "mimi_set_weight", "mimi_load_safetensors", "mimi_finalize",
-    "mimi_encode", "mimi_encode_async", "mimi_encode_wait", "mimi_rvq_encode", "mimi_set_precision", "mimi_get_precision", "mimi_f16_reruns", "mimi_set_graphs", "mimi_graph_replays", "mimi_encoded_length",
+    "mimi_encode", "mimi_encode_async", "mimi_encode_wait", "mimi_rvq_encode", "mimi_set_precision", "mimi_get_precision", "mimi_f16_reruns", "mimi_set_graphs", "mimi_graph_replays", "mimi_act_scales", "mimi_encoded_length",
     "mimi_encoded_length_cfg",
     "mimi_workspace_bytes", "mimi_destroy", "mimi_last_error", "mimi_set_profiling", "mimi_profile_read",
     "mimi_profile_reset", "mimi_set_taps", "mimi_get_tap", "mimi_resample_poly",
@@ -89,6 +89,8 @@ def _declare(lib):
         "mimi_f16_reruns": (c.c_int64, [vp]),
         "mimi_set_graphs": (c.c_int, [vp, c.c_int32]),
         "mimi_graph_replays": (c.c_int64, [vp]),
+        "mimi_act_scales": (c.c_int, [vp, c.c_int32, c.c_char_p, c.POINTER(c.c_float), c.POINTER(c.c_float),
+                                      c.POINTER(c.c_int32)]),
         "mimi_encoded_length": (c.c_int64, [c.c_int64]),
         "mimi_encoded_length_cfg": (c.c_int64, [c.POINTER(MimiConfigC), c.c_int64]),
         "mimi_workspace_bytes": (c.c_int64, [vp, c.c_int32, c.c_int64]),

@@ -272,6 +272,21 @@ class MimiHipModel:
     def graph_replays(self) -> int:
         return int(self._lib.mimi_graph_replays(self._h))
 
+    def act_scales(self):
+        """f16x3 diagnostics: {tensor: (fixed scale, max|x| of the last encode, headroom 2^15 / (scale * max))}."""
+        n = 256
+        names = ctypes.create_string_buffer(64 * n)
+        sc = (ctypes.c_float * n)()
+        mx = (ctypes.c_float * n)()
+        cnt = ctypes.c_int32()
+        _lib.check(self._lib.mimi_act_scales(self._h, n, names, sc, mx, ctypes.byref(cnt)))
+        out = {}
+        for i in range(cnt.value):
+            name = names.raw[64 * i:64 * (i + 1)].split(b"\0", 1)[0].decode()
+            head = 32768.0 / (sc[i] * mx[i]) if sc[i] > 0 and mx[i] > 0 else float("inf")
+            out[name] = (sc[i], mx[i], head)
+        return out
+
     def set_profiling(self, enable: bool = True):
         _lib.check(self._lib.mimi_set_profiling(self._h, int(enable)))
 
@@ -290,7 +305,10 @@ class MimiHipModel:
         for i in range(cnt.value):
             nm = names.raw[128 * i:128 * (i + 1)].split(b"\0", 1)[0].decode()
             stage, _, kernel = nm.partition("|")
-            out[stage] = dict(kernel=kernel, ms=ms[i], launches=launches[i], flops=fb[2 * i], bytes=fb[2 * i + 1])
+            key, j = stage, 2
+            while key in out:  # one stage run by two kernel symbols (e.g. the last layer's fc2): "fc2#2"
+                key, j = f"{stage}#{j}", j + 1
+            out[key] = dict(kernel=kernel, ms=ms[i], launches=launches[i], flops=fb[2 * i], bytes=fb[2 * i + 1])
         return out
 
     def set_taps(self, enable: bool = True):

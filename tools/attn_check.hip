@@ -72,5 +72,27 @@ int main(int argc, char** argv) {
         printf("rep %d: max|h16 - f32| / max|f32| = %.3e, differs from rep 0 in %zu halves (first: b %zu t %zu h %zu d %zu)\n",
                rep, md / mx, ndiff, fi / ((size_t)T * H * D), (fi / (H * D)) % T, (fi / D) % H, fi % D);
     }
+    // timing: the two fp16-plane kernels on this shape (T <= 256 only for the whole-head one)
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto timeit = [&](auto&& launch, const char* name) {
+        for (int i = 0; i < 3; ++i) launch();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < 20; ++i) launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("%-28s B %d T %d: %8.2f us per launch\n", name, B, T, ms * 1000.0f / 20);
+    };
+    timeit([&] { (void)launch_attention(q, nullptr, B, T, H, D, W, 0.125f, 0, pl, (long long)no, 2, os, amax, true); },
+           T <= 256 ? "attention_t256_h16" : "attention_band_h16");
+    if (T <= 256)
+        timeit([&] { (void)launch_attention_band(q, B, T, H, W, 0.125f, 0, pl, (long long)no, os, amax); },
+               "attention_band_h16");
+    timeit([&] { (void)launch_attention(q, ref, B, T, H, D, W, 0.125f, 0, nullptr, 0, 0, 0.0f, nullptr, false); },
+           "fp32");
     return 0;
 }

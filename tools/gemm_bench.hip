@@ -126,17 +126,14 @@ int main(int argc, char** argv) {
         {"b1_down_s1", 128, 10, 5, 60000, 12000, 1, 256}, {"b1_down_s0", 64, 8, 4, 240000, 60000, 1, 128},
     };
     Variant vars[] = {
-        {"ref 64x64 4w+4ld s4", launch_pl<64, 64, 2, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
-        {"pair ref 64x64 4w+4ld s2", launch_pl<64, 64, 2, 2, 2, 2, 4, 32, 16, FL_PAIR, true>, 64, 12, true},
-        {"64x64 4w+4ld s4 KG2", launch_pl<64, 64, 2, 2, 2, 4, 4, 32, 16, FL_KG2, true>, 32, 12},
-        {"64x64 4w+4ld s8 KG2", launch_pl<64, 64, 2, 2, 2, 8, 4, 32, 16, FL_KG2, true>, 32, 12},
-        {"64x64 4w+4ld s8 KG4", launch_pl<64, 64, 2, 2, 2, 8, 4, 32, 16, FL_KG4, true>, 32, 12},
-        {"64x64 4w s8 KG4", launch_pl<64, 64, 2, 2, 2, 8, 0, 32, 16, FL_KG4, true>, 32, 12},
-        {"pair 64x64 4w+4ld s4 KG2", launch_pl<64, 64, 2, 2, 2, 4, 4, 32, 16, FL_PAIR | FL_KG2, true>, 64, 12, true},
-        {"128x128 8w s2 (fc1)", launch_pl<128, 128, 4, 2, 2, 2, 0, 32, 16, 0, true>, 32, 12},
-        {"128x128 8w s4 KG2", launch_pl<128, 128, 4, 2, 2, 4, 0, 32, 16, FL_KG2, true>, 32, 12},
-        {"128x128 4w+4ld s4 KG2", launch_pl<128, 128, 2, 2, 2, 4, 4, 32, 16, FL_KG2, true>, 32, 12},
-        {"256x128 8w s3 (k3)", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
+        {"h2 256x128 8w mf16 s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
+        {"pair PERSIST (current)", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair PERSIST mf32 bk16 s4", launch_pl<256, 128, 4, 2, 2, 4, 4, 16, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair PERSIST mf32 bk16 s3", launch_pl<256, 128, 4, 2, 2, 3, 4, 16, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair PERSIST mf32 bk16 s4 KG2", launch_pl<256, 128, 4, 2, 2, 4, 4, 16, 32, FL_PAIR | FL_PERSIST | FL_KG2, true>, 64, 12, true},
+        {"pair PERSIST mf32 bk16 s4 0ld", launch_pl<256, 128, 4, 2, 2, 4, 0, 16, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair PERSIST mf32 bk32 s2", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"nonpair mf32 bk16 s4 PERSIST", launch_pl<256, 128, 4, 2, 2, 4, 4, 16, 32, FL_PERSIST, true>, 16, 12},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
