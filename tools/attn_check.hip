@@ -89,9 +89,10 @@ int main(int argc, char** argv) {
     };
     timeit([&] { (void)launch_attention(q, nullptr, B, T, H, D, W, 0.125f, 0, pl, (long long)no, 2, os, amax, true); },
            T <= 256 ? "attention_t256_h16" : "attention_band_h16");
-    if (T <= 256)
+    if (T <= 256) {
         timeit([&] { (void)launch_attention_band(q, B, T, H, W, 0.125f, 0, pl, (long long)no, os, amax); },
                "attention_band_h16");
+    }
     timeit([&] { (void)launch_attention(q, ref, B, T, H, D, W, 0.125f, 0, nullptr, 0, 0, 0.0f, nullptr, false); },
            "fp32");
     return 0;

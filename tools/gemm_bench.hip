@@ -1,5 +1,7 @@
-// Microbenchmark of gemm_f32_kernel variants on the encode's real GEMM shapes (tuning aid, not shipped).
-//   hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I tokenize-audio_amd/csrc tools/gemm_bench.hip -o tools/bin/gemm_bench
+// Microbenchmark of planes-GEMM variants on the encode's real GEMM shapes (tuning aid, not shipped).
+//   hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I tokenize-audio_amd/csrc -I tools \
+//     tools/gemm_bench.hip -o tools/bin/gemm_bench
+//   tools/bin/gemm_bench REPS down_s0,down_s1,...   (shape names, comma-separated)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -10,6 +12,7 @@
 #include <vector>
 
 #include "gemm_planes.h"
+#include "gemm_stream_proto.h"
 
 using namespace mimi;
 
