@@ -129,14 +129,17 @@ int main(int argc, char** argv) {
         {"b1_down_s1", 128, 10, 5, 60000, 12000, 1, 256}, {"b1_down_s0", 64, 8, 4, 240000, 60000, 1, 128},
     };
     Variant vars[] = {
-        {"h2 256x128 8w mf16 s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
-        {"pair PERSIST (current)", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
-        {"pair PERSIST mf32 bk16 s4", launch_pl<256, 128, 4, 2, 2, 4, 4, 16, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
-        {"pair PERSIST mf32 bk16 s3", launch_pl<256, 128, 4, 2, 2, 3, 4, 16, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
-        {"pair PERSIST mf32 bk16 s4 KG2", launch_pl<256, 128, 4, 2, 2, 4, 4, 16, 32, FL_PAIR | FL_PERSIST | FL_KG2, true>, 64, 12, true},
-        {"pair PERSIST mf32 bk16 s4 0ld", launch_pl<256, 128, 4, 2, 2, 4, 0, 16, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
-        {"pair PERSIST mf32 bk32 s2", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
-        {"nonpair mf32 bk16 s4 PERSIST", launch_pl<256, 128, 4, 2, 2, 4, 4, 16, 32, FL_PERSIST, true>, 16, 12},
+        {"ref 64x64 4w+4ld s4", launch_pl<64, 64, 2, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
+        {"pair ref 64x64 4w+4ld s2", launch_pl<64, 64, 2, 2, 2, 2, 4, 32, 16, FL_PAIR, true>, 64, 12, true},
+        {"64x64 4w+8ld s4", launch_pl<64, 64, 2, 2, 2, 4, 8, 32, 16, 0, true>, 32, 12},
+        {"64x64 4w+12ld s4", launch_pl<64, 64, 2, 2, 2, 4, 12, 32, 16, 0, true>, 32, 12},
+        {"32x32 1w+8ld s4", launch_pl<32, 32, 1, 1, 2, 4, 8, 32, 16, 0, true>, 32, 12},
+        {"32x32 1w+8ld s8", launch_pl<32, 32, 1, 1, 2, 8, 8, 32, 16, 0, true>, 32, 12},
+        {"32x32 1w+4ld s6", launch_pl<32, 32, 1, 1, 2, 6, 4, 32, 16, 0, true>, 32, 12},
+        {"32x64 2w+8ld s4", launch_pl<32, 64, 1, 2, 2, 4, 8, 32, 16, 0, true>, 32, 12},
+        {"32x64 2w+12ld s4", launch_pl<32, 64, 1, 2, 2, 4, 12, 32, 16, 0, true>, 32, 12},
+        {"pair 64x64 4w+8ld s2", launch_pl<64, 64, 2, 2, 2, 2, 8, 32, 16, FL_PAIR, true>, 64, 12, true},
+        {"pair 32x64 2w+8ld s2", launch_pl<32, 64, 1, 2, 2, 2, 8, 32, 16, FL_PAIR, true>, 64, 12, true},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
