@@ -16,6 +16,7 @@
 // layer scale + residual, RoPE (rotate-half pairs (d, d+32) live in the same lane of tiles tn, tn+1).
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 
 
 #include "gemm_planes.h"
@@ -264,13 +265,14 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
             return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);
         case ROLE_FC2: return run_planes_small_ld<EPI_SCALE_RES, 8>(a, s, prec);
         case ROLE_DOWN_XE: return run_planes_big<EPI_BIAS, 3 | 8, 2 | 8, 11>(a, s, prec);
-        case ROLE_RES3P:  // fp16: 128x128 on a 2-stage ring (two workgroups per CU), -4 % vs 256x128 x 3
-            if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 2, EPI_BIAS_ELU, 2, 12, 0, 32, 16, 0, true>(a, s);
+        case ROLE_RES3P:  // fp16: 256x128 on a 3-stage ring fed by 4 loader waves: -8 / -13 % vs 128x128 x 2
+            if (prec == PREC_F16X3)  // without loaders (stage 2 / 3, profiles/r2c_ab_dispatch.log)
+                return run_planes<256, 128, 4, 2, 2, 3, EPI_BIAS_ELU, 2, 12, 4, 32, 16, 0, true>(a, s);
             return run_planes_big<EPI_BIAS_ELU, 3, 2, 12>(a, s, prec);
-        case ROLE_RES1P:  // K = C/2 = 128 / 256: short K, output-heavy -> 74 KiB tiles, two workgroups per CU
-            if (prec == PREC_F16X3)  // fp16: a 2-stage ring (48 KiB, three workgroups per CU): -10..-14 % vs 3
-                                     // stages, 4 loader waves or 64x64 tiles (profiles/r1l_ab_small_kernels.txt)
-                return run_planes<128, 64, 2, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13, 0, 32, 16, 0, true>(a, s);
+        case ROLE_RES1P:  // K = C/2 = 128 / 256: short K, output-heavy
+            if (prec == PREC_F16X3)  // fp16: 128x128 x 8 waves on a 2-stage ring (64 KiB, two workgroups per CU):
+                                     // -18 % vs 128x64 x 4 waves (profiles/r2c_ab_dispatch.log)
+                return run_planes<128, 128, 4, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13, 0, 32, 16, 0, true>(a, s);
             if (prec == PREC_BF16X6) return run_planes<128, 64, 2, 2, 3, 2, EPI_BIAS_RES_ELU, 3, 13>(a, s);
             return run_planes<128, 64, 2, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13>(a, s);
         default: return hipErrorInvalidValue;

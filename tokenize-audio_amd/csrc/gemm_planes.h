@@ -257,6 +257,92 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     // KG ring stages per barrier (FL_KG2 / FL_KG4): the loaders retire a group of KG stages at once and the
     // compute waves run its KG K steps back to back (their fragment reads free to overlap the previous step's
     // MFMAs); the ring keeps the next group(s) in flight, STAGES >= 2 KG
+    if constexpr (LW > 0) {
+        // Warp-specialised: the loading and the computing waves run separate loops that meet at the same
+        // barriers, so neither keeps the other's registers live.  Loading wave W issues the pieces j = W + q LW
+        // of every stage -- compile-time once unrolled (no per-piece branches) -- from two 32-bit lane offsets
+        // into buffer resources (A planes per batch item, all weight planes), plus wave-uniform piece and K
+        // offsets.  Rows past M / N read data that only feeds never-stored outputs, or 0 past a buffer's end.
+        if (loader) {
+            const __amdgpu_buffer_rsrc_t wrsrc = make_rsrc(Wp, (long long)NS * N * K * 2);
+            const int c = pch ^ chunk_swz<BK, MF>(prow);  // the swizzle depends on the row's low bits only
+            const int a_lane = (int)((p.a_off + (long long)(m0 + prow) * p.a_rs + c * 8) * 2);
+            const int b_lane = ((n0 + prow) * K + c * 8) * 2;
+            const int a_rb = RPP * p.a_rs * 2, b_rb = RPP * K * 2, b_pl = N * K * 2;
+            auto run_loader = [&](auto Wc) {
+                constexpr int W = decltype(Wc)::value;
+                constexpr int PW = (TP - W + NLD - 1) / NLD;  // this wave's pieces per stage
+                auto issue_w = [&](int stage) {
+                    __bf16* st = lds + stage * STG;
+                    const int kb = ko.offset() * 2;
+                    ko.next();
+#pragma unroll
+                    for (int q = 0; q < PW; ++q) {
+                        const int j = W + q * NLD;
+                        if (j < TPA) {
+                            const int pl = j / (AR / RPP), rb = j % (AR / RPP);
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                                arsrc[pl], (__attribute__((address_space(3))) void*)(st + pl * APL + rb * RPP * BK),
+                                16, a_lane + rb * a_rb + kb, 0, 0, 0);
+                        } else {
+                            const int jb = j - TPA;
+                            const int pi = jb / (BN / RPP), rb = jb % (BN / RPP);  // pi = plane * NB + image
+                            const int pl = pi / NB, img = pi % NB;
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                                wrsrc,
+                                (__attribute__((address_space(3))) void*)(st + NS * APL + pi * BPL + rb * RPP * BK),
+                                16, b_lane + pl * b_pl + rb * b_rb + kb + img * kimg * 2, 0, 0, 0);
+                        }
+                    }
+                };
+#pragma unroll
+                for (int s = 0; s < STAGES - KG; ++s)
+                    if (s < KT) issue_w(s);
+                for (int kt = 0; kt < KT; kt += KG) {
+                    const int ng = min(KG, KT - kt);
+                    wait_stages<PW, STAGES - 2 * KG>(min(KT, kt + STAGES - KG) - (kt + ng));
+                    __builtin_amdgcn_s_barrier();
+                    if (!(FL & FL_DIAG_NODMA)) {
+#pragma unroll
+                        for (int q = 0; q < KG; ++q)
+                            if (kt + STAGES - KG + q < KT) issue_w((kt + STAGES - KG + q) % STAGES);
+                    }
+                }
+            };
+            static_assert(LW <= 8, "loader waves");
+            switch (ldw) {
+                case 0: run_loader(std::integral_constant<int, 0>()); break;
+                case 1: if constexpr (LW > 1) run_loader(std::integral_constant<int, 1>()); break;
+                case 2: if constexpr (LW > 2) run_loader(std::integral_constant<int, 2>()); break;
+                case 3: if constexpr (LW > 3) run_loader(std::integral_constant<int, 3>()); break;
+                case 4: if constexpr (LW > 4) run_loader(std::integral_constant<int, 4>()); break;
+                case 5: if constexpr (LW > 5) run_loader(std::integral_constant<int, 5>()); break;
+                case 6: if constexpr (LW > 6) run_loader(std::integral_constant<int, 6>()); break;
+                default: if constexpr (LW > 7) run_loader(std::integral_constant<int, 7>()); break;
+            }
+        } else {
+            for (int kt = 0; kt < KT; kt += KG) {
+                const int ng = min(KG, KT - kt);
+                __builtin_amdgcn_s_barrier();
+                if (FL & FL_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int q = 0; q < KG; ++q) {
+                    if (q >= ng) break;
+                    const __bf16* As = lds + ((kt + q) % STAGES) * STG;
+                    const __bf16* Bs = As + NS * APL;
+                    bf16x8 af[NS][TM], bf[NS][TN];
+#pragma unroll
+                    for (int img = 0; img < NB; ++img)
+#pragma unroll
+                        for (int ks = 0; ks < KSUB; ++ks) {
+                            read_frags(As, Bs, ks, af, bf, img);
+                            if (!(FL & FL_DIAG_NOMMA)) mma_split<NS, TM, TN, F16>(acc, af, bf);
+                        }
+                }
+                if (FL & FL_PRIO) __builtin_amdgcn_s_setprio(0);
+            }
+        }
+    } else {
     if (loader) {
 #pragma unroll
         for (int s = 0; s < STAGES - KG; ++s)
@@ -298,6 +384,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         }
         if (FL & FL_PRIO) __builtin_amdgcn_s_setprio(0);
     }
+    }  // LW == 0
 
     // ---- epilogue.  Phase 1 (MFMA layout): the epilogue math, into a wave-private fp32 tile in the (now idle)
     // LDS ring.  32x32 tiles: lane holds col lane&31, rows (r&3) + 8(r>>2) + 4(lane>>5); 16x16 tiles: col

@@ -122,6 +122,8 @@ int main(int argc, char** argv) {
         {"final", 1024, 3, 1, 250, 250, 32, 512},        {"fc1", 512, 1, 1, 8000, 8000, 1, 2048},
         {"fc2", 2048, 1, 1, 8000, 8000, 1, 512},         {"qkv", 512, 1, 1, 250, 250, 32, 1536},
         {"o_proj", 512, 1, 1, 8000, 8000, 1, 512},
+        {"res3_s2", 256, 3, 1, 12000, 12000, 32, 128},   {"res1_s2", 128, 1, 1, 12000, 12000, 32, 256},
+        {"res3_s3", 512, 3, 1, 2000, 2000, 32, 256},     {"res1_s3", 256, 1, 1, 2000, 2000, 32, 512},
         // batch 1 (launch / latency bound)
         {"b1_fc2", 2048, 1, 1, 250, 250, 1, 512},        {"b1_fc1", 512, 1, 1, 250, 250, 1, 2048},
         {"b1_qkv", 512, 1, 1, 250, 250, 1, 1536},        {"b1_oproj", 512, 1, 1, 250, 250, 1, 512},
@@ -129,17 +131,23 @@ int main(int argc, char** argv) {
         {"b1_down_s1", 128, 10, 5, 60000, 12000, 1, 256}, {"b1_down_s0", 64, 8, 4, 240000, 60000, 1, 128},
     };
     Variant vars[] = {
-        {"ref 64x64 4w+4ld s4", launch_pl<64, 64, 2, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
-        {"pair ref 64x64 4w+4ld s2", launch_pl<64, 64, 2, 2, 2, 2, 4, 32, 16, FL_PAIR, true>, 64, 12, true},
-        {"64x64 4w+8ld s4", launch_pl<64, 64, 2, 2, 2, 4, 8, 32, 16, 0, true>, 32, 12},
-        {"64x64 4w+12ld s4", launch_pl<64, 64, 2, 2, 2, 4, 12, 32, 16, 0, true>, 32, 12},
-        {"32x32 1w+8ld s4", launch_pl<32, 32, 1, 1, 2, 4, 8, 32, 16, 0, true>, 32, 12},
-        {"32x32 1w+8ld s8", launch_pl<32, 32, 1, 1, 2, 8, 8, 32, 16, 0, true>, 32, 12},
-        {"32x32 1w+4ld s6", launch_pl<32, 32, 1, 1, 2, 6, 4, 32, 16, 0, true>, 32, 12},
-        {"32x64 2w+8ld s4", launch_pl<32, 64, 1, 2, 2, 4, 8, 32, 16, 0, true>, 32, 12},
-        {"32x64 2w+12ld s4", launch_pl<32, 64, 1, 2, 2, 4, 12, 32, 16, 0, true>, 32, 12},
-        {"pair 64x64 4w+8ld s2", launch_pl<64, 64, 2, 2, 2, 2, 8, 32, 16, FL_PAIR, true>, 64, 12, true},
-        {"pair 32x64 2w+8ld s2", launch_pl<32, 64, 1, 2, 2, 2, 8, 32, 16, FL_PAIR, true>, 64, 12, true},
+        // references: loader-free kernels (the LW > 0 loop under test must give the same bits)
+        {"ref 256x128 8w s3", launch_pl<256, 128, 4, 2, 2, 3, 0, 32, 16, 0, true>, 32, 12},
+        {"pair ref 256x128 8w s2 0ld", launch_pl<256, 128, 4, 2, 2, 2, 0, 32, 16, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair PERSIST 8w+4ld s2", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair 64x64 4w+4ld s2", launch_pl<64, 64, 2, 2, 2, 2, 4, 32, 16, FL_PAIR, true>, 64, 12, true},
+        {"pair 64x64 4w+4ld s4 KG2", launch_pl<64, 64, 2, 2, 2, 4, 4, 32, 16, FL_PAIR | FL_KG2, true>, 64, 12, true},
+        {"64x64 4w+4ld s4", launch_pl<64, 64, 2, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
+        {"128x128 4w+4ld s3", launch_pl<128, 128, 2, 2, 2, 3, 4, 32, 16, 0, true>, 32, 12},
+        {"128x128 8w+4ld s2", launch_pl<128, 128, 4, 2, 2, 2, 4, 32, 16, 0, true>, 32, 12},
+        {"256x128 8w+4ld s3", launch_pl<256, 128, 4, 2, 2, 3, 4, 32, 16, 0, true>, 32, 12},
+        {"128x128 8w s2 (fc1/qkv/res3)", launch_pl<128, 128, 4, 2, 2, 2, 0, 32, 16, 0, true>, 32, 12},
+        {"128x64 4w s2 (res1)", launch_pl<128, 64, 2, 2, 2, 2, 0, 32, 16, 0, true>, 32, 12},
+        {"128x64 4w+4ld s2", launch_pl<128, 64, 2, 2, 2, 2, 4, 32, 16, 0, true>, 32, 12},
+        {"128x64 4w+4ld s3", launch_pl<128, 64, 2, 2, 2, 3, 4, 32, 16, 0, true>, 32, 12},
+        {"128x128 4w+4ld s4", launch_pl<128, 128, 2, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
+        {"128x128 8w+4ld s3", launch_pl<128, 128, 4, 2, 2, 3, 4, 32, 16, 0, true>, 32, 12},
+        {"64x128 2w+4ld s4", launch_pl<64, 128, 1, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
