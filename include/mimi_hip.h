@@ -167,6 +167,18 @@ int mimi_resample_poly(const float* dev_in, const int64_t* dev_in_off, const int
                        void* stream);
 
 /*
+ * FLAC decode for host ingest (replaces libFLAC behind librosa.load -> soundfile -> libsndfile on the LibriSpeech
+ * path: librispeech-mimi/process_librispeech_dev-test.py:136, utils.py:84-87).  `data` holds a whole .flac file
+ * (an ID3v2 tag in front is skipped).  mimi_flac_info reads STREAMINFO.  mimi_flac_decode decodes every frame
+ * into `out`, planar int32 [channels][cap_per_channel] at the stream's bit depth (out = NULL: count only), and
+ * sets *n_samples (per channel); CRC-8 / CRC-16 mismatches, malformed frames and a sample count that differs
+ * from STREAMINFO's return MIMI_ERR_IO.  Host-only, re-entrant (no engine handle).
+ */
+int mimi_flac_info(const uint8_t* data, int64_t nbytes, int32_t* sample_rate, int32_t* channels,
+                   int32_t* bits_per_sample, int64_t* total_samples);
+int mimi_flac_decode(const uint8_t* data, int64_t nbytes, int32_t* out, int64_t cap_per_channel, int64_t* n_samples);
+
+/*
  * Codec-BPE training over code strings (replaces the BpeTrainer run of codec-bpe/bpe_trainer.py:147-156; driven
  * by mimi_hip/bpe.py).  The corpus: words of symbol ids (0 .. n_initial_tokens-1 = special tokens, then the
  * alphabet), concatenated in `symbols`, word w = symbols[word_offsets[w] .. word_offsets[w+1]), occurring

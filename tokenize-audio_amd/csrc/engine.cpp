@@ -58,6 +58,14 @@ static int set_err(int code, const char* fmt, ...) {
 
 extern "C" const char* mimi_last_error(void) { return g_last_error.c_str(); }
 
+namespace mimi {
+// for the host-side C ABI files (flac.cpp): one thread-local last error behind mimi_last_error
+int set_last_error(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+}  // namespace mimi
+
 int mimi::set_error_message(int code, const char* msg) {
     g_last_error = msg;
     return code;

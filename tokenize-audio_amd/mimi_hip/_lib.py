@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = (
     "mimi_encoded_length_cfg",
     "mimi_workspace_bytes", "mimi_destroy", "mimi_last_error", "mimi_set_profiling", "mimi_profile_read",
     "mimi_profile_reset", "mimi_set_taps", "mimi_get_tap", "mimi_resample_poly",
-    "mimi_bpe_create", "mimi_bpe_best", "mimi_bpe_merge", "mimi_bpe_destroy",
+    "mimi_bpe_create", "mimi_bpe_best", "mimi_bpe_merge", "mimi_bpe_destroy", "mimi_flac_info", "mimi_flac_decode",
 )
 RESAMPLE_MAX_TAPS = 8192  # MIMI_RESAMPLE_MAX_TAPS
 
@@ -107,6 +107,9 @@ def _declare(lib):
         "mimi_bpe_best": (c.c_int, [vp, c.POINTER(c.c_int32), c.POINTER(c.c_int32), c.POINTER(c.c_int64)]),
         "mimi_bpe_merge": (c.c_int, [vp, c.c_int32, c.c_int32, c.c_int32, c.c_int32]),
         "mimi_bpe_destroy": (None, [vp]),
+        "mimi_flac_info": (c.c_int, [vp, c.c_int64, c.POINTER(c.c_int32), c.POINTER(c.c_int32),
+                                     c.POINTER(c.c_int32), c.POINTER(c.c_int64)]),
+        "mimi_flac_decode": (c.c_int, [vp, c.c_int64, vp, c.c_int64, c.POINTER(c.c_int64)]),
         "mimi_resample_poly": (c.c_int, [vp, vp, vp, c.c_int32, vp, vp, vp, c.c_int64, vp, c.c_int32, c.c_int32,
                                          c.c_int32, c.c_int64, vp]),
     }

@@ -9,10 +9,16 @@ Replaces ``librosa.load(path, sr=24000)`` on the shard scripts' load path (``lib
   ``ceil(n * target_sr / orig_sr)``), computed by the HIP kernel ``resample_poly_kernel`` through the C ABI
   (``mimi_resample_poly``), bit-exact with scipy on float32 input.  Ragged clips go in ONE launch.
 
+* ``load_flac``: FLAC (the LibriSpeech corpus files, ``librispeech-mimi/process_librispeech_dev-test.py:136``)
+  decoded by the library's spec-written decoder (``mimi_flac_decode``, csrc/flac.cpp), then the same float
+  conversion and channel mean.
+
 Parity limits: librosa is not installed, so its DEFAULT mode (``soxr_hq``, libsoxr) is
 unpinned -- a script that wants bit-identical inputs to an existing soxr-resampled shard must keep librosa;
-what is pinned is the polyphase mode, against scipy itself.  Compressed formats (flac / mp3 / opus) need a
-decoder this image lacks and are out of scope.
+what is pinned is the polyphase mode, against scipy itself.  FLAC is lossless, so a correct decoder returns
+exactly the encoded PCM; libFLAC is absent here, so the decoder is checked by round trips through a test-side
+encoder written from the format specification (tests/flac_writer.py), not against libFLAC itself.  mp3 / opus
+(Emilia's tar members) need decoders this image lacks and are out of scope.
 
 Only the filter design (61 taps for 16 -> 24 kHz) runs on the host, with ``scipy.signal.firwin`` exactly as
 ``resample_poly`` designs it; there is no CPU resampling path.
@@ -25,7 +31,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["resample_plan", "resample", "resample_packed", "load_wav", "load"]
+__all__ = ["resample_plan", "resample", "resample_packed", "load_wav", "load_flac", "decode_flac", "load"]
 
 
 def resample_plan(orig_sr: int, target_sr: int) -> Tuple[int, int, np.ndarray, int]:
@@ -136,11 +142,53 @@ def load_wav(path: str) -> Tuple[np.ndarray, int]:
     return np.ascontiguousarray(y), int(sr)
 
 
+def decode_flac(data: bytes) -> Tuple[np.ndarray, int, int]:
+    """A whole .flac file's bytes -> (int32 samples [channels, n], sample rate, bits per sample)."""
+    import ctypes
+    lib = _lib.load()
+    buf = np.frombuffer(data, dtype=np.uint8)
+    if buf.size == 0:
+        raise ValueError("empty FLAC buffer")
+    rate, ch, bps, total = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+    ptr = buf.ctypes.data
+    _lib.check(lib.mimi_flac_info(ptr, buf.size, ctypes.byref(rate), ctypes.byref(ch), ctypes.byref(bps),
+                                  ctypes.byref(total)))
+    n = ctypes.c_int64()
+    cap = total.value
+    if cap == 0:  # length unknown in STREAMINFO: count first
+        _lib.check(lib.mimi_flac_decode(ptr, buf.size, None, 0, ctypes.byref(n)))
+        cap = n.value
+    out = np.zeros((ch.value, max(cap, 1)), dtype=np.int32)
+    _lib.check(lib.mimi_flac_decode(ptr, buf.size, out.ctypes.data, out.shape[1], ctypes.byref(n)))
+    return out[:, :n.value], rate.value, bps.value
+
+
+def load_flac(path: str) -> Tuple[np.ndarray, int]:
+    """FLAC file -> (float32 mono samples, sample rate), as librosa.load(path, sr=None) returns it: libsndfile's
+    float conversion (samples / 2^(bits-1)) and librosa's ``to_mono`` (float32 mean over channels)."""
+    with open(path, "rb") as f:
+        pcm, sr, bps = decode_flac(f.read())
+    y = (pcm.astype(np.float64) / float(1 << (bps - 1))).astype(np.float32)  # exact for bps <= 24
+    y = np.mean(y, axis=0, dtype=np.float32) if y.shape[0] > 1 else y[0]
+    return np.ascontiguousarray(y), int(sr)
+
+
+def _is_flac(path: str) -> bool:
+    with open(path, "rb") as f:
+        head = f.read(10)
+    if head[:3] == b"ID3" and len(head) == 10:
+        size = ((head[6] & 0x7F) << 21) | ((head[7] & 0x7F) << 14) | ((head[8] & 0x7F) << 7) | (head[9] & 0x7F)
+        with open(path, "rb") as f:
+            f.seek(10 + size + (10 if head[5] & 0x10 else 0))
+            return f.read(4) == b"fLaC"
+    return head[:4] == b"fLaC"
+
+
 def load(path: str, sr: Optional[int] = 24000, device: Union[str, torch.device] = "cuda",
          as_numpy: bool = True):
-    """``librosa.load(path, sr=sr, res_type='polyphase')`` for WAV: returns (samples, sr).  Samples are a numpy
-    float32 array (``as_numpy``) or the device tensor, ready for ``MimiHipModel.encode``."""
-    y, file_sr = load_wav(path)
+    """``librosa.load(path, sr=sr, res_type='polyphase')`` for WAV and FLAC files: returns (samples, sr).  Samples
+    are a numpy float32 array (``as_numpy``) or the device tensor, ready for ``MimiHipModel.encode``."""
+    y, file_sr = load_flac(path) if _is_flac(path) else load_wav(path)
     if sr is None or sr == file_sr:
         t = torch.from_numpy(y)
         return (y if as_numpy else t.to(_device(device))), file_sr
