@@ -223,11 +223,12 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
             case ROLE_FC2:
                 if (a.Cp) {  // the last layer: fp32 residual stream + its planes (the downsample's input)
                     if (tiles(a, 128, 128) < kSmallGrid)
-                        return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 2, 8, 4, 32, 16, 0, true>(a, s);
+                        return run_planes<64, 32, 2, 2, 2, 6, EPI_SCALE_RES, 2, 8, 4, 32, 16, FL_KG2, true>(a, s);
                     return run_planes<128, 128, 2, 2, 2, 3, EPI_SCALE_RES, 2, 8, 4, 32, 16, 0, true>(a, s);
                 }
-                if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 0, 8, 4, 32, 16, 0, true>(a, s);
+                if (tiles(a, 128, 128) < kSmallGrid)  // K = 2048: 64x32 tiles (twice the workgroups streaming the
+                    // weights) on a 6-deep ring retired 2 stages per barrier: -14 % at batch 1 (profiles/r2c_ab_b1.log)
+                    return run_planes<64, 32, 2, 2, 2, 6, EPI_SCALE_RES, 0, 8, 4, 32, 16, FL_KG2, true>(a, s);
                 break;
             case ROLE_DOWNSAMPLE:  // zero-padded here; engine.cpp adds the replicate rows (launch_ds_edge_fix)
                 if (tiles(a, 128, 128) < kSmallGrid)

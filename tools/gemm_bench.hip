@@ -128,7 +128,8 @@ int main(int argc, char** argv) {
         {"b1_fc2", 2048, 1, 1, 250, 250, 1, 512},        {"b1_fc1", 512, 1, 1, 250, 250, 1, 2048},
         {"b1_qkv", 512, 1, 1, 250, 250, 1, 1536},        {"b1_oproj", 512, 1, 1, 250, 250, 1, 512},
         {"b1_down_s3", 512, 16, 8, 2000, 250, 1, 1024},  {"b1_final", 1024, 3, 1, 250, 250, 1, 512},
-        {"b1_down_s1", 128, 10, 5, 60000, 12000, 1, 256}, {"b1_down_s0", 64, 8, 4, 240000, 60000, 1, 128},
+        {"b1_down_s1", 128, 10, 5, 60000, 12000, 1, 256},
+        {"b8_dn_s1", 128, 10, 5, 60000, 12000, 8, 256}, {"b1_down_s0", 64, 8, 4, 240000, 60000, 1, 128},
     };
     Variant vars[] = {
         // references: loader-free kernels (the LW > 0 loop under test must give the same bits)
@@ -148,6 +149,16 @@ int main(int argc, char** argv) {
         {"128x128 4w+4ld s4", launch_pl<128, 128, 2, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
         {"128x128 8w+4ld s3", launch_pl<128, 128, 4, 2, 2, 3, 4, 32, 16, 0, true>, 32, 12},
         {"64x128 2w+4ld s4", launch_pl<64, 128, 1, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
+        {"pair PERSIST bk16 mf32 s4", launch_pl<256, 128, 4, 2, 2, 4, 4, 16, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair PERSIST bk16 mf32 s3", launch_pl<256, 128, 4, 2, 2, 3, 4, 16, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair PERSIST bk16 mf32 s4 KG2", launch_pl<256, 128, 4, 2, 2, 4, 4, 16, 32, FL_PAIR | FL_PERSIST | FL_KG2, true>, 64, 12, true},
+        {"pair PERSIST mf32 s2", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair PERSIST 4w(2x2)+4ld s2", launch_pl<256, 128, 2, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair PERSIST 4w(4x1)+4ld s2", launch_pl<256, 128, 4, 1, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair PERSIST 4w(2x2) mf32+4ld s2", launch_pl<256, 128, 2, 2, 2, 2, 4, 32, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair PERSIST DIAG nodma", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NODMA, true>, 64, 12, true},
+        {"pair PERSIST DIAG nomma", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NOMMA, true>, 64, 12, true},
+        {"pair PERSIST DIAG both", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NODMA | FL_DIAG_NOMMA, true>, 64, 12, true},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
