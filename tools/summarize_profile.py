@@ -48,6 +48,27 @@ def main(tag):
     for d in out["kernels"].values():
         if "fetch_bytes" in d and "write_bytes" in d:
             d["traffic_bytes"] = d["fetch_bytes"] + d["write_bytes"]
+    # the dominant kernel's steady-state launches in the kernel trace (the bench's own timed steps: the last
+    # `launches` of that kernel; calibration / warm-up launches excluded) next to the bench's HIP-event figure
+    if os.path.exists(bj):
+        b = json.loads(open(bj).read().strip().splitlines()[-1])
+        rl = b.get("roofline", {})
+        kern, nl = rl.get("kernel"), int(rl.get("launches", 0))
+        tr = os.path.join(src, "trace", "run_kernel_trace.csv")
+        if kern and nl and os.path.exists(tr):
+            rows = sorted(csv.DictReader(open(tr)), key=lambda r: int(r["Start_Timestamp"]))
+            key = kern.replace("mimi::", "")
+            d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows
+                 if r["Kernel_Name"].replace("void ", "").replace("mimi::", "").startswith(key)]
+            last = d[-nl:]
+            dom = {"kernel": kern, "trace_launches_total": len(d), "trace_launches_steady": len(last),
+                   "trace_steady_mean_ms": sum(last) / max(1, len(last)),
+                   "bench_event_mean_ms": rl.get("avg_launch_ms"),
+                   "note": "rocprofv3 kernel trace of the same bench run; steady = the last `launches` dispatches "
+                           "(the bench's timed steps), excluding the finalize-time calibration encodes"}
+            with open(os.path.join(dst, f"{tag}_dominant_kernel.json"), "w") as f:
+                json.dump(dom, f, indent=1)
+            print("dominant kernel:", json.dumps(dom))
     for name in (f"{tag}_pmc_summary.json", "pmc_summary.json"):
         with open(os.path.join(dst, name), "w") as f:
             json.dump(out, f, indent=1, sort_keys=True)
