@@ -262,6 +262,8 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         case ROLE_FC1:  // planes out: fc2; fp16: 128x128 on a 2-stage ring (two workgroups per CU): -4 % vs
                         // 256x256 x 2 stages, which beat 256x128 x 3 by 8-11 % (profiles/r1j_gemm_bench_256.log,
                         // r1l_ab_small_kernels.txt)
+            // (256x128 persistent tiles with FL_PF: -8 % in tools/gemm_bench.hip, +5 % in the engine with the GELU
+            // planes epilogue -- profiles/r2c_gemm_bench_pf.log, r2c_ab_fc1.log)
             if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 2, EPI_GELU, 2, 7, 0, 32, 16, 0, true>(a, s);
             return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);
         case ROLE_FC2: return run_planes_small_ld<EPI_SCALE_RES, 8>(a, s, prec);

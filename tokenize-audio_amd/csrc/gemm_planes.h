@@ -84,7 +84,10 @@ __device__ __forceinline__ int chunk_swz(int row) {
 //           gridDim.x, the XCD map applied to the tile index): a tile's epilogue stores drain while the same
 //           workgroup already streams its next tile's first stages (the barrier between them waits for LDS
 //           only, never for the stores), and no workgroup launch / ring fill per tile.
-enum : int { FL_PRIO = 2, FL_PAIR = 4, FL_PERSIST = 8, FL_KG2 = 16, FL_KG4 = 32 };
+//           FL_PF -- (with FL_PERSIST and loader waves) the loaders issue the next tile's first ring stages while
+//           the compute waves run this tile's epilogue (the staging moves past those slots, in more passes if
+//           needed).
+enum : int { FL_PRIO = 2, FL_PAIR = 4, FL_PERSIST = 8, FL_KG2 = 16, FL_KG4 = 32, FL_PF = 256 };
 // tuning diagnostics (tools/gemm_bench.hip only; results are garbage): no DMA refills after the prologue / no MFMAs
 enum : int { FL_DIAG_NODMA = 64, FL_DIAG_NOMMA = 128 };
 
@@ -127,12 +130,20 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     constexpr int NACC = MF == 32 ? 16 : 4;
 
     // epilogue staging (wave-private fp32 tiles) reuses the ring; a wave's CW columns go through it in JH
-    // passes of CWC when the whole tile would not fit (256x256 tiles)
+    // passes of CWC when the whole tile would not fit (256x256 tiles).  PF (FL_PF): the loaders issue the next
+    // tile's first STAGES - KG stages while the compute waves run this tile's epilogue, so the staging sits
+    // past those ring slots (PFS halves in)
     constexpr int CW = TN * MF, RW = TM * MF;
-    constexpr int JH = NW * RW * (CW + 4) * 4 <= 160 * 1024 ? 1 : 2;
+    constexpr int PFS0 = (STAGES - KG) * STG;
+    constexpr bool PFIT1 = PFS0 * 2 + NW * RW * (CW + 4) * 4 <= 160 * 1024;
+    constexpr bool PFIT2 = TN % 2 == 0 && PFS0 * 2 + NW * RW * (CW / 2 + 4) * 4 <= 160 * 1024;
+    constexpr bool PFIT4 = TN % 4 == 0 && PFS0 * 2 + NW * RW * (CW / 4 + 4) * 4 <= 160 * 1024;
+    constexpr bool PF = (FL & FL_PF) && (FL & FL_PERSIST) && LW > 0 && (PFIT1 || PFIT2 || PFIT4);
+    constexpr int PFS = PF ? PFS0 : 0;
+    constexpr int JH = PF ? (PFIT1 ? 1 : PFIT2 ? 2 : 4) : (NW * RW * (CW + 4) * 4 <= 160 * 1024 ? 1 : 2);
     constexpr int TNC = TN / JH, CWC = TNC * MF, LDE = CWC + 4;
     static_assert(TNC * JH == TN, "epilogue passes");  // (RoPE pairs are read from acc, not from the staging)
-    constexpr int LDS_EL = STAGES * STG > NW * RW * LDE * 2 ? STAGES * STG : NW * RW * LDE * 2;
+    constexpr int LDS_EL = STAGES * STG > PFS + NW * RW * LDE * 2 ? STAGES * STG : PFS + NW * RW * LDE * 2;
     static_assert(LDS_EL * 2 <= 160 * 1024, "LDS");
     __shared__ __attribute__((aligned(16))) __bf16 lds[LDS_EL];
 
@@ -148,6 +159,106 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     const int MT = (M + BM - 1) / BM, NTn = (N + BN - 1) / BN;
     const int ntiles = MT * NTn * p.batch;
     float omx = 0.0f;  // max|planes value| (fp16 planes: the engine's range check), over this workgroup's tiles
+    const int KT = K / BK / NB;
+
+    if constexpr (LW > 0) {
+        // Warp-specialised: the loading waves run their own tile loop, meeting the compute waves at the same
+        // barriers (one per ring group, the epilogue's __syncthreads, the persistent tiles' barrier), so neither
+        // keeps the other's registers live.  Loading wave W issues the pieces j = W + q LW of every stage --
+        // compile-time once unrolled (no per-piece branches) -- from two 32-bit lane offsets into buffer
+        // resources (A planes per batch item, all weight planes), plus wave-uniform piece and K offsets.  Rows
+        // past M / N read data that only feeds never-stored outputs, or 0 past a buffer's end.
+        if (loader) {
+            const int prow = lane / CPR, pch = lane % CPR;
+            const int c = pch ^ chunk_swz<BK, MF>(prow);  // the swizzle depends on the row's low bits only
+            const __bf16* __restrict__ Wp = reinterpret_cast<const __bf16*>(p.Wsplit);
+            const __amdgpu_buffer_rsrc_t wrsrc = make_rsrc(Wp, (long long)NS * N * K * 2);
+            const int a_rb = RPP * p.a_rs * 2, b_rb = RPP * K * 2, b_pl = N * K * 2;
+            auto run_loader = [&](auto Wc) {
+                constexpr int W = decltype(Wc)::value;
+                constexpr int PW = (TP - W + NLD - 1) / NLD;  // this wave's pieces per stage
+                __amdgpu_buffer_rsrc_t arsrc[NS];
+                int a_lane = 0, b_lane = 0, kimg = 0;
+                KOrderT<BK> ko;  // K steps are issued in order: the cursor follows the issues
+                auto setup = [&](int tile) {  // this wave's sources for `tile`, K cursor at its first step
+                    const int logical = xcd_remap(tile, ntiles);
+                    const int nt = logical % NTn, rest = logical / NTn;
+                    const int m0 = (rest % MT) * BM, n0 = nt * BN, b = rest / MT;
+                    const __bf16* __restrict__ Abase = reinterpret_cast<const __bf16*>(p.Ap) + (long long)b * p.a_bstride;
+#pragma unroll
+                    for (int pl = 0; pl < NS; ++pl)
+                        arsrc[pl] = make_rsrc(Abase + (long long)pl * p.a_pstride, p.a_len * 2);
+                    a_lane = (int)((p.a_off + (long long)(m0 + prow) * p.a_rs + c * 8) * 2);
+                    b_lane = ((n0 + prow) * K + c * 8) * 2;
+                    ko.init(p, PAIR);
+                    kimg = PAIR ? ko.s * ko.cin : 0;  // K offset of a stage's second tap
+                };
+                auto issue_w = [&](int stage) {
+                    __bf16* st = lds + stage * STG;
+                    const int kb = ko.offset() * 2;
+                    ko.next();
+#pragma unroll
+                    for (int q = 0; q < PW; ++q) {
+                        const int j = W + q * NLD;
+                        if (j < TPA) {
+                            const int pl = j / (AR / RPP), rb = j % (AR / RPP);
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                                arsrc[pl], (__attribute__((address_space(3))) void*)(st + pl * APL + rb * RPP * BK),
+                                16, a_lane + rb * a_rb + kb, 0, 0, 0);
+                        } else {
+                            const int jb = j - TPA;
+                            const int pi = jb / (BN / RPP), rb = jb % (BN / RPP);  // pi = plane * NB + image
+                            const int pl = pi / NB, img = pi % NB;
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                                wrsrc,
+                                (__attribute__((address_space(3))) void*)(st + NS * APL + pi * BPL + rb * RPP * BK),
+                                16, b_lane + pl * b_pl + rb * b_rb + kb + img * kimg * 2, 0, 0, 0);
+                        }
+                    }
+                };
+                auto prologue = [&](int tile) {
+                    setup(tile);
+#pragma unroll
+                    for (int s2 = 0; s2 < STAGES - KG; ++s2)
+                        if (s2 < KT) issue_w(s2);
+                };
+                if ((int)blockIdx.x < ntiles) prologue(blockIdx.x);
+                for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+                    for (int kt = 0; kt < KT; kt += KG) {
+                        const int ng = min(KG, KT - kt);
+                        wait_stages<PW, STAGES - 2 * KG>(min(KT, kt + STAGES - KG) - (kt + ng));
+                        __builtin_amdgcn_s_barrier();
+                        if (!(FL & FL_DIAG_NODMA)) {
+#pragma unroll
+                            for (int q = 0; q < KG; ++q)
+                                if (kt + STAGES - KG + q < KT) issue_w((kt + STAGES - KG + q) % STAGES);
+                        }
+                    }
+                    __syncthreads();  // the compute waves' epilogue starts (the ring is free)
+                    const int next = tile + (int)gridDim.x;
+                    if (PF && next < ntiles) prologue(next);  // lands in slots [0, STAGES - KG) under the epilogue
+                    if (FL & FL_PERSIST) {
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        __builtin_amdgcn_s_barrier();
+                    }
+                    if (!PF && next < ntiles) prologue(next);
+                }
+            };
+            static_assert(LW <= 8, "loader waves");
+            switch (ldw) {
+                case 0: run_loader(std::integral_constant<int, 0>()); break;
+                case 1: if constexpr (LW > 1) run_loader(std::integral_constant<int, 1>()); break;
+                case 2: if constexpr (LW > 2) run_loader(std::integral_constant<int, 2>()); break;
+                case 3: if constexpr (LW > 3) run_loader(std::integral_constant<int, 3>()); break;
+                case 4: if constexpr (LW > 4) run_loader(std::integral_constant<int, 4>()); break;
+                case 5: if constexpr (LW > 5) run_loader(std::integral_constant<int, 5>()); break;
+                case 6: if constexpr (LW > 6) run_loader(std::integral_constant<int, 6>()); break;
+                default: if constexpr (LW > 7) run_loader(std::integral_constant<int, 7>()); break;
+            }
+            return;  // (no barrier follows in the compute waves)
+        }
+    }
+
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int logical = xcd_remap(tile, ntiles);
     const int nt = logical % NTn;
@@ -228,7 +339,6 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
 #pragma unroll
             for (int r = 0; r < NACC; ++r) acc[i][j][r] = 0.0f;
 
-    const int KT = K / BK / NB;
     const int arow = wm * TM * MF + (lane & (MF - 1));
     const int brow = wn * TN * MF + (lane & (MF - 1));
     const int hsel = MF == 32 ? lane >> 5 : lane >> 4;  // k chunk of the lane within an MFMA k-step
@@ -258,69 +368,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     // compute waves run its KG K steps back to back (their fragment reads free to overlap the previous step's
     // MFMAs); the ring keeps the next group(s) in flight, STAGES >= 2 KG
     if constexpr (LW > 0) {
-        // Warp-specialised: the loading and the computing waves run separate loops that meet at the same
-        // barriers, so neither keeps the other's registers live.  Loading wave W issues the pieces j = W + q LW
-        // of every stage -- compile-time once unrolled (no per-piece branches) -- from two 32-bit lane offsets
-        // into buffer resources (A planes per batch item, all weight planes), plus wave-uniform piece and K
-        // offsets.  Rows past M / N read data that only feeds never-stored outputs, or 0 past a buffer's end.
-        if (loader) {
-            const __amdgpu_buffer_rsrc_t wrsrc = make_rsrc(Wp, (long long)NS * N * K * 2);
-            const int c = pch ^ chunk_swz<BK, MF>(prow);  // the swizzle depends on the row's low bits only
-            const int a_lane = (int)((p.a_off + (long long)(m0 + prow) * p.a_rs + c * 8) * 2);
-            const int b_lane = ((n0 + prow) * K + c * 8) * 2;
-            const int a_rb = RPP * p.a_rs * 2, b_rb = RPP * K * 2, b_pl = N * K * 2;
-            auto run_loader = [&](auto Wc) {
-                constexpr int W = decltype(Wc)::value;
-                constexpr int PW = (TP - W + NLD - 1) / NLD;  // this wave's pieces per stage
-                auto issue_w = [&](int stage) {
-                    __bf16* st = lds + stage * STG;
-                    const int kb = ko.offset() * 2;
-                    ko.next();
-#pragma unroll
-                    for (int q = 0; q < PW; ++q) {
-                        const int j = W + q * NLD;
-                        if (j < TPA) {
-                            const int pl = j / (AR / RPP), rb = j % (AR / RPP);
-                            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                                arsrc[pl], (__attribute__((address_space(3))) void*)(st + pl * APL + rb * RPP * BK),
-                                16, a_lane + rb * a_rb + kb, 0, 0, 0);
-                        } else {
-                            const int jb = j - TPA;
-                            const int pi = jb / (BN / RPP), rb = jb % (BN / RPP);  // pi = plane * NB + image
-                            const int pl = pi / NB, img = pi % NB;
-                            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                                wrsrc,
-                                (__attribute__((address_space(3))) void*)(st + NS * APL + pi * BPL + rb * RPP * BK),
-                                16, b_lane + pl * b_pl + rb * b_rb + kb + img * kimg * 2, 0, 0, 0);
-                        }
-                    }
-                };
-#pragma unroll
-                for (int s = 0; s < STAGES - KG; ++s)
-                    if (s < KT) issue_w(s);
-                for (int kt = 0; kt < KT; kt += KG) {
-                    const int ng = min(KG, KT - kt);
-                    wait_stages<PW, STAGES - 2 * KG>(min(KT, kt + STAGES - KG) - (kt + ng));
-                    __builtin_amdgcn_s_barrier();
-                    if (!(FL & FL_DIAG_NODMA)) {
-#pragma unroll
-                        for (int q = 0; q < KG; ++q)
-                            if (kt + STAGES - KG + q < KT) issue_w((kt + STAGES - KG + q) % STAGES);
-                    }
-                }
-            };
-            static_assert(LW <= 8, "loader waves");
-            switch (ldw) {
-                case 0: run_loader(std::integral_constant<int, 0>()); break;
-                case 1: if constexpr (LW > 1) run_loader(std::integral_constant<int, 1>()); break;
-                case 2: if constexpr (LW > 2) run_loader(std::integral_constant<int, 2>()); break;
-                case 3: if constexpr (LW > 3) run_loader(std::integral_constant<int, 3>()); break;
-                case 4: if constexpr (LW > 4) run_loader(std::integral_constant<int, 4>()); break;
-                case 5: if constexpr (LW > 5) run_loader(std::integral_constant<int, 5>()); break;
-                case 6: if constexpr (LW > 6) run_loader(std::integral_constant<int, 6>()); break;
-                default: if constexpr (LW > 7) run_loader(std::integral_constant<int, 7>()); break;
-            }
-        } else {
+        {  // compute waves (the loaders run their own loop above)
             for (int kt = 0; kt < KT; kt += KG) {
                 const int ng = min(KG, KT - kt);
                 __builtin_amdgcn_s_barrier();
@@ -393,7 +441,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     // per plane) store per value.
     __syncthreads();  // every wave is done with the ring
     if (compute) {
-    float* stg = reinterpret_cast<float*>(lds) + wave * (RW * LDE);
+    float* stg = reinterpret_cast<float*>(lds + PFS) + wave * (RW * LDE);
     const float* __restrict__ Rb = p.R ? p.R + (long long)b * p.c_bstride : nullptr;
     const int rbase = m0 + wm * RW;
     const int cbase = n0 + wn * CW + (lane & (MF - 1));

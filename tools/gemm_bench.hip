@@ -156,6 +156,10 @@ int main(int argc, char** argv) {
         {"pair PERSIST 4w(2x2)+4ld s2", launch_pl<256, 128, 2, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
         {"pair PERSIST 4w(4x1)+4ld s2", launch_pl<256, 128, 4, 1, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
         {"pair PERSIST 4w(2x2) mf32+4ld s2", launch_pl<256, 128, 2, 2, 2, 2, 4, 32, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"128x128 8w+4ld s2 P", launch_pl<128, 128, 4, 2, 2, 2, 4, 32, 16, FL_PERSIST | FL_PF, true>, 32, 12},
+        {"128x128 8w+4ld s3 P", launch_pl<128, 128, 4, 2, 2, 3, 4, 32, 16, FL_PERSIST | FL_PF, true>, 32, 12},
+        {"128x128 4w+4ld s3 P", launch_pl<128, 128, 2, 2, 2, 3, 4, 32, 16, FL_PERSIST | FL_PF, true>, 32, 12},
+        {"256x128 8w+4ld s3 P", launch_pl<256, 128, 4, 2, 2, 3, 4, 32, 16, FL_PERSIST | FL_PF, true>, 32, 12},
         {"pair PERSIST DIAG nodma", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NODMA, true>, 64, 12, true},
         {"pair PERSIST DIAG nomma", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NOMMA, true>, 64, 12, true},
         {"pair PERSIST DIAG both", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NODMA | FL_DIAG_NOMMA, true>, 64, 12, true},

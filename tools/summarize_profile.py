@@ -27,13 +27,21 @@ def main(tag):
         shutil.copy(bj, os.path.join(dst, f"{tag}_bench_under_trace.json"))
     out = {"tag": tag, "units": "bytes per launch", "fetch_correction": 2.0,
            "note": "FETCH_SIZE (KB) x 1024 x 2 (gfx950 reports half of wide streaming reads), WRITE_SIZE (KB) x 1024;"
-                   " separate --pmc passes of `bench.py --steps 2 --warmup 1`", "kernels": {}}
+                   " separate --pmc passes of `bench.py --steps 2 --warmup 1`; dispatches after bench.py's spin_kernel marker"
+                   " only (the finalize-time calibration encode precedes it)", "kernels": {}}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         p = os.path.join(src, f"pmc_{counter}", "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
         agg = collections.defaultdict(list)
-        for r in csv.DictReader(open(p)):
+        rows = list(csv.DictReader(open(p)))
+        if "Dispatch_Id" in rows[0]:
+            rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        mk = [i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]]
+        if mk:  # bench.py's marker: the bench's own dispatches follow it (calibration encodes precede it)
+            rows = rows[mk[0] + 1:]
+            out["after_marker"] = True
+        for r in rows:
             agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
         for k, v in agg.items():
             name = k.replace("void ", "", 1).split("(")[0].strip()
@@ -58,6 +66,8 @@ def main(tag):
         if kern and nl and os.path.exists(tr):
             rows = sorted(csv.DictReader(open(tr)), key=lambda r: int(r["Start_Timestamp"]))
             key = kern.replace("mimi::", "")
+            mk = [i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]]
+            rows = rows[mk[0] + 1:] if mk else rows
             d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows
                  if r["Kernel_Name"].replace("void ", "").replace("mimi::", "").startswith(key)]
             last = d[-nl:]
