@@ -83,6 +83,9 @@ def parse():
                     help="wall budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: this process's CPU affinity, capped by OMP_NUM_THREADS)")
+    ap.add_argument("--concurrency", type=int, default=0,
+                    help="mls workload: engines encoding different utterances at once through "
+                         "MimiEncoder.encode_audio_chunks (0 = 4)")
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage events")
     ap.add_argument("--no-f32-mode", action="store_true", help="skip the fp32-MFMA comparison run")
     ap.add_argument("--precision", default=None, help="GEMM precision mode (default: the engine's)")
@@ -266,7 +269,8 @@ class Workload:
             self.desc = (f"LibriTTS-R-style batch encode (configs[{1 if B <= 32 else 2}]): batch={B} x "
                          f"{args.seconds:g} s @ 24 kHz resident in HBM, K={K} codebooks, 1 encode per step per GPU")
             return
-        enc = MimiEncoder(device=dev, model=model, num_quantizers=K)
+        conc = (args.concurrency or 4) if self.kind == "mls" else 1
+        enc = MimiEncoder(device=dev, model=model, num_quantizers=K, concurrency=conc)
         lo, hi = (1.5, 20.0) if self.kind == "yodas2" else (10.0, 20.0)
         n_steps = args.warmup + args.steps
         # the whole shard's utterance list; this rank takes i % world == rank (sharding.py), in batches of B
@@ -287,11 +291,11 @@ class Workload:
                          f"D2H, trim), K={K}, utterance round-robin over {world} GPU(s)")
         else:
             def step():
-                for a in self.clips[self.i]:
-                    enc.encode_audio_chunk(a, 24000)
+                enc.encode_audio_chunks(self.clips[self.i], 24000)
                 self.i += 1
             self.desc = (f"MLS-style stream (configs[4], encode part): {B} utterances U[{lo:g}, {hi:g}] s per step, "
-                         f"each through MimiEncoder.encode_audio_chunk (batch 1, H2D + D2H included), K={K}, "
+                         f"each encoded alone at its own length (encode_audio_chunk semantics, batch 1, H2D + D2H "
+                         f"included) through MimiEncoder.encode_audio_chunks with {conc} engine(s) at once, K={K}, "
                          f"utterance round-robin over {world} GPU(s)")
         self.step = step
         self._np = np

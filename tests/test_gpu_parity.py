@@ -160,6 +160,26 @@ def test_batch_wrapper_matches_reference_wrapper(engine, golden, state_dict):
     assert np.array_equal(c, arrays["chunk_item3"].astype(np.int64))
 
 
+def test_encode_audio_chunks_equals_per_utterance_calls(engine, golden):
+    """MimiEncoder.encode_audio_chunks (the per-utterance callers: MLS, LibriSpeech) = encode_audio_chunk per item,
+    bit for bit, with 3 engines (clones: same weights and calibration) encoding different items at once; the
+    golden item 3 (the reference wrapper's own encode_audio_chunk output) among them."""
+    from mimi_hip.encoder import MimiEncoder
+    arrays, meta = golden
+    enc = MimiEncoder(device="cuda:0", model=engine, concurrency=3)
+    rng = np.random.default_rng(5)
+    lens = [int(x) for x in rng.integers(2000, 24000 * 14, size=7)] + [1, 1921]
+    audio = [synthetic.speech_like(L, 31, i) for i, L in enumerate(lens)]
+    audio.insert(4, synthetic.speech_like(meta["batch_lengths"][3], meta["audio_seed"], 203))
+    got = enc.encode_audio_chunks(audio, 24000)
+    assert len(got) == len(audio)
+    for i, a in enumerate(audio):
+        want = enc.encode_audio_chunk(a, 24000)
+        assert got[i].dtype == np.int64 and np.array_equal(got[i], want), i
+    assert np.array_equal(got[4], arrays["chunk_item3"].astype(np.int64))
+    assert enc.encode_audio_chunks([], 24000) == []
+
+
 def test_padded_batch_b32_vs_reference_wrapper(engine):
     """B = 32 mixed lengths U[1.5, 20] s (17 items > 10.24 s: window-250 attention path; items 3 and 7 at -40 /
     -60 dB) through our MimiEncoder vs the reference's own MimiEncoder.encode_audio_batch

@@ -10,6 +10,13 @@ in ``libritts-r-mimi/process_libritts_r.py:33-105``, ``yodas2-mimi/process_shard
   single item; otherwise pad-to-longest, ONE encode, trim item i to ``int(ceil(L_i / (sr / 12.5)))``
   frames                                                                                        ``:88-140``
 
+Added for the per-utterance callers (MLS ``mls-en-mimi-pretrain/process_shard.py:268-307`` and LibriSpeech call
+``encode_audio_chunk`` once per utterance): ``encode_audio_chunks(list, sr)`` returns exactly
+``[encode_audio_chunk(a, sr) for a in list]`` -- each item encoded alone at its own length, batch 1 -- but runs
+``concurrency`` engines (same weights and calibration, so the same codes) on their own streams from as many host
+threads, so several batch-1 encodes fill the GPU at once.  A driver keeps its per-utterance loop semantics by
+encoding a window of upcoming utterances per call.
+
 The inputs and outputs are the reference's; the data path is leaner.  The reference runs the feature
 extractor and moves ``input_values`` and the int64 ``padding_mask`` (8 B per sample) to the device, although
 the model ignores the mask (``TF/modeling_mimi.py:1244, :1247``).  Here the items are copied straight into a
@@ -21,6 +28,8 @@ A shard script switches by replacing its ``class MimiEncoder`` with ``from mimi_
 from __future__ import annotations
 
 import logging
+import threading
+from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional
 
 import numpy as np
@@ -36,7 +45,7 @@ class MimiEncoder:
     """Wrapper for Mimi model encoding (HIP engine)."""
 
     def __init__(self, model_id: str = "kyutai/mimi", device: str = "cuda", model: Optional[MimiHipModel] = None,
-                 num_quantizers: Optional[int] = None):
+                 num_quantizers: Optional[int] = None, concurrency: int = 1):
         logger.info(f"Loading Mimi model: {model_id}")
         self.device = device
         self.feature_extractor = MimiFeatureExtractor.from_pretrained(model_id)
@@ -47,6 +56,9 @@ class MimiEncoder:
         # first K levels do not depend on the later ones (split RVQ, TF/modeling_mimi.py:1060-1066), so a
         # caller that only keeps K may set num_quantizers=K for the same result with less work.
         self.num_quantizers = num_quantizers
+        self.concurrency = max(1, int(concurrency))
+        self._lanes = None  # [(engine, stream)] built on the first encode_audio_chunks call
+        self._lanes_lock = threading.Lock()
         logger.info("Mimi model loaded successfully")
 
     def _check(self, arrays, sample_rate):
@@ -95,12 +107,48 @@ class MimiEncoder:
         if len(audio_arrays) == 1:
             return [self.encode_audio_chunk(audio_arrays[0], sample_rate)]
         with torch.no_grad():
-            arrays = self._check(audio_arrays, sample_rate)
-            original_lengths = [len(audio) for audio in arrays]
-            audio_codes = self._encode_padded(arrays)
-            frame_rate = sample_rate / 12.5
-            results = []
-            for i, orig_length in enumerate(original_lengths):
-                actual_frames = int(np.ceil(orig_length / frame_rate))
-                results.append(audio_codes[i, :, :actual_frames].astype(np.int64))
-            return results
+            items = self._check(audio_arrays, sample_rate)
+            codes = self._encode_padded(items)
+            samples_per_frame = sample_rate / 12.5
+            # item i keeps the frames its own samples produce, int(ceil(L_i / samples_per_frame)), of the padded
+            # batch's codes (the reference's trim)
+            return [codes[i, :, :int(np.ceil(len(a) / samples_per_frame))].astype(np.int64)
+                    for i, a in enumerate(items)]
+
+    def _get_lanes(self):
+        with self._lanes_lock:
+            if self._lanes is None:
+                engines = [self.model] + [self.model.clone() for _ in range(self.concurrency - 1)]
+                self._lanes = [(e, torch.cuda.Stream(device=e.device)) for e in engines]
+            return self._lanes
+
+    def encode_audio_chunks(self, audio_arrays: List[np.ndarray], sample_rate: int = 24000) -> List[np.ndarray]:
+        """``[self.encode_audio_chunk(a, sample_rate) for a in audio_arrays]``, with ``concurrency`` engines
+        encoding different items at once (item i on lane i mod concurrency, in order within a lane)."""
+        if not hasattr(self.model, "encode_async") or self.concurrency == 1 or len(audio_arrays) <= 1:
+            return [self.encode_audio_chunk(a, sample_rate) for a in audio_arrays]
+        items = self._check(audio_arrays, sample_rate)
+        if any(a.shape[0] == 0 for a in items):
+            raise ValueError("empty audio")
+        lanes = self._get_lanes()
+        K = self.num_quantizers or self.model.config.num_quantizers
+        out: List[Optional[np.ndarray]] = [None] * len(items)
+
+        def run(k):  # lane k: its items in order, the next one enqueued before the previous one is waited for
+            engine, stream = lanes[k]
+            pending = None
+            with torch.no_grad(), torch.cuda.stream(stream):
+                for i in list(range(k, len(items), len(lanes))) + [None]:
+                    ticket = None
+                    if i is not None:
+                        x = torch.from_numpy(items[i]).to(engine.device, non_blocking=False).reshape(1, -1)
+                        ticket = (i, engine.encode_async(x, K))
+                    if pending is not None:
+                        j, t = pending
+                        out[j] = t.wait()[0].cpu().numpy().astype(np.int64)
+                    pending = ticket
+
+        n = min(len(lanes), len(items))
+        with ThreadPoolExecutor(n) as ex:
+            list(ex.map(run, range(n)))
+        return out

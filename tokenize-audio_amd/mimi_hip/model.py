@@ -106,6 +106,7 @@ class MimiHipModel:
         _lib.check(self._lib.mimi_create(ctypes.byref(self._cfg_c), self.device.index, ctypes.byref(handle)))
         self._h = handle
         self._lock = threading.Lock()
+        self._src = (state_dict, config, safetensors_path)  # for clone()
         try:
             if safetensors_path is not None:
                 _lib.check(self._lib.mimi_load_safetensors(self._h, safetensors_path.encode()))
@@ -138,6 +139,14 @@ class MimiHipModel:
                 raise FileNotFoundError(f"no .safetensors file in {path}")
             path = files[0]
         return cls(config=cfg, device=device, safetensors_path=path, **kw)
+
+    def clone(self, device: Union[str, torch.device, None] = None) -> "MimiHipModel":
+        """Another engine with the same weights and config (its own workspace; same calibration, so the same codes):
+        independent encodes on several engines run concurrently (``MimiEncoder.encode_audio_chunks``)."""
+        sd, cfg, path = self._src
+        m = MimiHipModel(sd, config=cfg or self.config, device=device or self.device, safetensors_path=path)
+        m.set_precision(self.precision)
+        return m
 
     def close(self):
         h = getattr(self, "_h", None)
