@@ -202,49 +202,49 @@ static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
     return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP, TAG, 0, 32, 16, 0, true>(a, s);
 }
 
+// Small grids, f16x3 (fewer than kSmallGrid 128x128 tiles: 1-4 utterances): per role three tile sizes of the same
+// kernel family -- 64, 32 and 16 rows -- and the largest one that still gives >= 256 workgroups (one per CU) runs,
+// else the smallest.  These GEMMs are latency-bound at this size (a few K steps per microsecond per workgroup, each
+// workgroup streaming its own A and W slices), so more, smaller tiles finish sooner even though they re-read more.
+// Measured per role at B = 1 and B = 4 (profiles/r2d_ab_small_tiles.log): the rule picks the fastest of the three
+// everywhere; B = 1: 7.3k -> 8.0k audio-s/s.
+template <int EPI, int OUTP, int TAG, int BN0, int BM1, int BN1, int WM1, int WN1, int BN2, int WN2, int ST = 4,
+          int FL = 0, int BM0 = 64, int WN0 = 2>
+static hipError_t run_small_h16(const GemmArgs& a, hipStream_t s) {
+    if (tiles(a, BM0, BN0) >= 256) return run_planes<BM0, BN0, 2, WN0, 2, ST, EPI, OUTP, TAG, 4, 32, 16, FL, true>(a, s);
+    if (tiles(a, BM1, BN1) >= 256) return run_planes<BM1, BN1, WM1, WN1, 2, ST, EPI, OUTP, TAG, 4, 32, 16, FL, true>(a, s);
+    return run_planes<16, BN2, 1, WN2, 2, ST, EPI, OUTP, TAG, 4, 32, 16, FL, true>(a, s);
+}
+
 static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
     const int prec = g_prec;
     if (prec != PREC_BF16X6 && prec != PREC_BF16X3 && prec != PREC_F16X3) return hipErrorInvalidValue;
+    if (prec == PREC_F16X3 && tiles(a, 128, 128) < kSmallGrid) {
+        // <EPI, OUTP, TAG, 64-row BN, 32-row BM x BN / waves, 16-row BN / waves>; 16 x 16 wave tiles are too small for
+        // the staged epilogue (64 lanes x 8 columns), and RoPE needs 64 columns per wave
+        switch (role) {
+            case ROLE_FINAL: return run_small_h16<EPI_BIAS_OUT, 0, 4, 64, 32, 64, 2, 2, 64, 2>(a, s);
+            case ROLE_QKV: return run_small_h16<EPI_ROPE, 0, 5, 128, 32, 128, 2, 2, 64, 1>(a, s);
+            case ROLE_OPROJ: return run_small_h16<EPI_SCALE_RES, 0, 6, 64, 32, 64, 2, 2, 64, 2>(a, s);
+            case ROLE_FC1: return run_small_h16<EPI_GELU, 2, 7, 64, 32, 64, 2, 2, 64, 2>(a, s);
+            case ROLE_FC2:  // K = 2048: 6-deep rings retired 2 stages per barrier (-14 % at batch 1, profiles/r2c_ab_b1.log)
+                if (a.Cp)  // the last layer: fp32 residual stream + its planes (the downsample's input)
+                    return run_small_h16<EPI_SCALE_RES, 2, 8, 32, 32, 32, 1, 2, 32, 1, 6, FL_KG2>(a, s);
+                return run_small_h16<EPI_SCALE_RES, 0, 8, 32, 32, 32, 1, 2, 32, 1, 6, FL_KG2>(a, s);
+            case ROLE_DOWNSAMPLE:  // zero-padded here; engine.cpp adds the replicate rows (launch_ds_edge_fix)
+                return run_small_h16<EPI_NONE, 2, 9, 64, 32, 64, 2, 2, 64, 2>(a, s);
+            case ROLE_INPROJ: return run_small_h16<EPI_NONE, 0, 10, 64, 32, 64, 2, 2, 64, 2>(a, s);
+            case ROLE_RES3P: return run_small_h16<EPI_BIAS_ELU, 2, 12, 64, 32, 64, 2, 2, 64, 2, 3>(a, s);
+            default: break;
+        }
+    }
     if (prec == PREC_F16X3) {
         switch (role) {
-            case ROLE_FINAL:
-                if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 4, EPI_BIAS_OUT, 0, 4, 4, 32, 16, 0, true>(a, s);
-                break;
-            case ROLE_QKV:  // (RoPE pairs need 4 column tiles per wave: 64 x 128)
-                if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 128, 2, 2, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, 0, true>(a, s);
-                break;
-            case ROLE_OPROJ:
-                if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 4, EPI_SCALE_RES, 0, 6, 4, 32, 16, 0, true>(a, s);
-                break;
-            case ROLE_FC1:
-                if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, 0, true>(a, s);
-                break;
             case ROLE_FC2:
-                if (a.Cp) {  // the last layer: fp32 residual stream + its planes (the downsample's input)
-                    if (tiles(a, 128, 128) < kSmallGrid)
-                        return run_planes<64, 32, 2, 2, 2, 6, EPI_SCALE_RES, 2, 8, 4, 32, 16, FL_KG2, true>(a, s);
-                    return run_planes<128, 128, 2, 2, 2, 3, EPI_SCALE_RES, 2, 8, 4, 32, 16, 0, true>(a, s);
-                }
-                if (tiles(a, 128, 128) < kSmallGrid)  // K = 2048: 64x32 tiles (twice the workgroups streaming the
-                    // weights) on a 6-deep ring retired 2 stages per barrier: -14 % at batch 1 (profiles/r2c_ab_b1.log)
-                    return run_planes<64, 32, 2, 2, 2, 6, EPI_SCALE_RES, 0, 8, 4, 32, 16, FL_KG2, true>(a, s);
+                if (a.Cp) return run_planes<128, 128, 2, 2, 2, 3, EPI_SCALE_RES, 2, 8, 4, 32, 16, 0, true>(a, s);
                 break;
-            case ROLE_DOWNSAMPLE:  // zero-padded here; engine.cpp adds the replicate rows (launch_ds_edge_fix)
-                if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 4, EPI_NONE, 2, 9, 4, 32, 16, 0, true>(a, s);
-                return run_planes<128, 128, 4, 2, 2, 2, EPI_NONE, 2, 9, 0, 32, 16, 0, true>(a, s);
-            case ROLE_INPROJ:
-                if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 4, EPI_NONE, 0, 10, 4, 32, 16, 0, true>(a, s);
-                return run_planes<128, 128, 4, 2, 2, 2, EPI_NONE, 0, 10, 0, 32, 16, 0, true>(a, s);
-            case ROLE_RES3P:
-                if (tiles(a, 128, 128) < kSmallGrid)
-                    return run_planes<64, 64, 2, 2, 2, 3, EPI_BIAS_ELU, 2, 12, 4, 32, 16, 0, true>(a, s);
-                break;
+            case ROLE_DOWNSAMPLE: return run_planes<128, 128, 4, 2, 2, 2, EPI_NONE, 2, 9, 0, 32, 16, 0, true>(a, s);
+            case ROLE_INPROJ: return run_planes<128, 128, 4, 2, 2, 2, EPI_NONE, 0, 10, 0, 32, 16, 0, true>(a, s);
             default: break;
         }
         switch (role) {

@@ -500,6 +500,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     __bf16* __restrict__ Cpb = ONS ? reinterpret_cast<__bf16*>(p.Cp) + (long long)b * p.c_bstride : nullptr;
     constexpr int LPR = CWC / 8;  // lanes per row
     constexpr int RPS = 64 / LPR;  // rows per pass
+    static_assert(RW % RPS == 0, "epilogue: a wave's tile holds whole passes of 64 lanes x 8 columns");
 #pragma unroll
     for (int ps = 0; ps < RW / RPS; ++ps) {
         const int lr = ps * RPS + lane / LPR, lc = (lane % LPR) * 8;

@@ -1,5 +1,6 @@
 // Non-GEMM kernels of the Mimi encode path for gfx950: the Cin = 1 input conv, LayerNorm, the
 // sliding-window attention and the split residual-VQ argmin.
+#include <cstdlib>
 #include "kernels.h"
 
 namespace mimi {
@@ -829,6 +830,7 @@ hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int 
                             hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
                             unsigned* oamax, bool h16) {
     if (D != 64 || (outns != 0 && !outp) || (outns == 0 && !out) || (oscale > 0.0f && outns != 2)) return hipErrorInvalidValue;
+    // (the banded kernel at T <= 256 measured slower at B = 1 and B = 32: profiles/r2d_ab_attention_band.log)
     if (h16 && T <= 256) {  // fp16-plane output (the engine's plane path at these lengths)
         if (!(oscale > 0.0f && outns == 2)) return hipErrorInvalidValue;
         hipLaunchKernelGGL(attention_t256_h16_kernel, dim3(H, batch), dim3(512), 0, s, qkv, T, H, window, scale, outp,
@@ -1207,12 +1209,13 @@ __global__ __launch_bounds__(256) void rvq_final_kernel(RvqArgs p, int L) {
 // overflow the LDS list (degenerate codebooks, e.g. all-equal entries), it scores every code exactly.
 // Per level one launch of (frames / 32) x 8 slices: each level's work is spread over ~1000 workgroups (a
 // single launch chaining all levels per 32-frame workgroup measured 25 % slower: too few, too serial).
-constexpr int RVQ_H16_FT = 32;
 constexpr int RVQ_CAND = 2048;
 
-template <int D>
-__global__ __launch_bounds__(512, 2) void rvq_level_h16_kernel(RvqArgs p, int L) {
-    constexpr int FT = RVQ_H16_FT;
+// FT frames per workgroup (32 or 64): each wave streams its 32 codes' 32 KB of codebook planes from L2 once per
+// workgroup, so 64-frame tiles halve the per-CU codebook stream (one workgroup per CU: 145 KB of LDS)
+template <int D, int FT>
+__global__ __launch_bounds__(512, FT == 32 ? 2 : 1) void rvq_level_h16_kernel(RvqArgs p, int L) {
+    constexpr int RT = FT / 32;  // 32-frame row tiles per wave
     constexpr int LDH = D / 2 + 4;
     constexpr int RLD = D + 8;  // fp16 plane rows: 528 B = 132 dwords (conflict-free b128 fragment reads)
     constexpr int NSL = 2048 / RVQ_CS;
@@ -1269,9 +1272,9 @@ __global__ __launch_bounds__(512, 2) void rvq_level_h16_kernel(RvqArgs p, int L)
         img[1][i][(k >> 1) + 1] = -2.0f * r.w;
     }
     __syncthreads();
-    // |r|^2 in torch's order (rvq_level_kernel) and max|r| per frame (16 threads per frame)
-    {
-        const int fi = tid >> 4, l = tid & 15;
+    // |r|^2 in torch's order (rvq_level_kernel) and max|r| per frame (16 threads per frame, 32 frames per pass)
+    for (int fi = tid >> 4; fi < FT; fi += 32) {
+        const int l = tid & 15;
         if (l < 8) {
             float a[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
@@ -1316,9 +1319,11 @@ __global__ __launch_bounds__(512, 2) void rvq_level_h16_kernel(RvqArgs p, int L)
     const int code0 = slice * RVQ_CS + wave * 32;
     const h8* bp = reinterpret_cast<const h8*>(p.cb_h16) +
                    ((long long)L * (p.ncodes / 32) + code0 / 32) * (D / 16) * 2 * 64 + lane;
-    f32x16 acc;
+    f32x16 acc[RT];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
     constexpr int PF = 4;
     h8 bq[PF][2];
 #pragma unroll
@@ -1334,25 +1339,30 @@ __global__ __launch_bounds__(512, 2) void rvq_level_h16_kernel(RvqArgs p, int L)
             bq[cur][0] = bp[(ks + PF) * 128];
             bq[cur][1] = bp[(ks + PF) * 128 + 64];
         }
-        const h8 a0 = *reinterpret_cast<const h8*>(&rpl[0][lane & 31][ks * 16 + 8 * h]);
-        const h8 a1 = *reinterpret_cast<const h8*>(&rpl[1][lane & 31][ks * 16 + 8 * h]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+            const h8 a0 = *reinterpret_cast<const h8*>(&rpl[0][i * 32 + (lane & 31)][ks * 16 + 8 * h]);
+            const h8 a1 = *reinterpret_cast<const h8*>(&rpl[1][i * 32 + (lane & 31)][ks * 16 + 8 * h]);
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc[i], 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc[i], 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc[i], 0, 0, 0);
+        }
     }
     const int code = code0 + (lane & 31);
     const float yn = p.cb_norm[(long long)L * p.ncodes + code];
     const float cus = p.cb_unscale[L];
-    float ad[16];
+    float ad[RT][16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        ad[r] = (-2.0f * (acc[r] * (rus[row] * cus)) + xn[row]) + yn;
-        float m = ad[r];
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o));
-        if ((lane & 31) == 0) redd[wave][row] = m;
-    }
+        for (int r = 0; r < 16; ++r) {
+            const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            ad[i][r] = (-2.0f * (acc[i][r] * (rus[row] * cus)) + xn[row]) + yn;
+            float m = ad[i][r];
+#pragma unroll
+            for (int o = 16; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+            if ((lane & 31) == 0) redd[wave][row] = m;
+        }
     __syncthreads();
     if (tid < FT) {
         float m = redd[0][tid];
@@ -1365,10 +1375,12 @@ __global__ __launch_bounds__(512, 2) void rvq_level_h16_kernel(RvqArgs p, int L)
     }
     __syncthreads();
 #pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         // NaN distances (a non-finite residual) are candidates too: the exact path decides
-        if (!(ad[r] > smin[row] + win[row]) && f0 + row < p.frames) {
+        if (!(ad[i][r] > smin[row] + win[row]) && f0 + row < p.frames) {
             const unsigned slot = atomicAdd(&ncand, 1u);
             if (slot < RVQ_CAND) cand[slot] = ((unsigned)row << 16) | (unsigned)(code - slice * RVQ_CS);
         }
@@ -1416,9 +1428,11 @@ hipError_t launch_rvq(const RvqArgs& a, hipStream_t s) {
     if (a.D != 256 || a.ncodes != 2048 || !a.work) return hipErrorInvalidValue;
     if (a.frames <= 0) return hipSuccess;
     if (a.cb_h16 && a.cb_unscale && a.cb_emax) {
-        const dim3 grid((unsigned)((a.frames + RVQ_H16_FT - 1) / RVQ_H16_FT), 2048 / RVQ_CS);
+        // (64-frame tiles, which halve the per-CU codebook stream, measured slower at B = 32: 0.56 vs 0.42 ms for 8
+        // levels -- one workgroup per CU and 16 spilled VGPRs; profiles/r2d_rvq_ft64.log)
+        const dim3 grid((unsigned)((a.frames + 31) / 32), 2048 / RVQ_CS);
         for (int L = 0; L < a.levels; ++L) {
-            hipLaunchKernelGGL((rvq_level_h16_kernel<256>), grid, dim3(512), 0, s, a, L);
+            hipLaunchKernelGGL((rvq_level_h16_kernel<256, 32>), grid, dim3(512), 0, s, a, L);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
