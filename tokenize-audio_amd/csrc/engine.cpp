@@ -1290,7 +1290,7 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     r.frames_per_item = frames_per_item;
     LAUNCH_TRY(launch_rvq(r, s), "rvq");
     rec.mark("rvq", 2.0 * frames * r.D * r.ncodes * K, (double)frames * (2 * r.D) * 4 + (double)frames * K * 4,
-             e->cb_h16 ? "mimi::rvq_level_h16_kernel<256, 32>" : "mimi::rvq_level_kernel<256>");
+             e->cb_h16 ? "mimi::rvq_level_h16_kernel<256>" : "mimi::rvq_level_kernel<256>");
     return MIMI_OK;
 }
 

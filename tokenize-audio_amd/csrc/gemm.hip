@@ -191,8 +191,13 @@ static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
     // small grids: long K (down_s3, K = 8192) retires 2 pair stages per barrier from a 4-deep ring (batch 1:
     // 100 -> 83 us in the engine; the same grouping made the K <= 3072 transformer GEMMs slower there although
     // faster in tools/gemm_bench.hip with warm caches, profiles/r2_gemm_bench_kg.log); shorter K: 2-stage ring
-    if (pair_ok(a) && tiles(a, 256, 128) < kSmallGrid && a.K >= 4096)
+    if (pair_ok(a) && tiles(a, 256, 128) < kSmallGrid && a.K >= 4096) {
+        // batch 1: 64x64 tiles leave 64 workgroups, each at its CU's LDS-DMA ceiling for 8192 / 64 pair stages;
+        // 32x32 tiles spread the same stream over 256 CUs
+        if (tiles(a, 64, 64) < 256)
+            return run_planes<32, 32, 1, 2, 2, 4, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR | FL_KG2, true>(a, s);
         return run_planes<64, 64, 2, 2, 2, 4, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR | FL_KG2, true>(a, s);
+    }
     if (pair_ok(a) && tiles(a, 256, 128) < kSmallGrid)
         return run_planes<64, 64, 2, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR, true>(a, s);
     // fp32-only output (down_s0): the next tile's first stage loads under the epilogue (FL_PF: -2.6 %; with the

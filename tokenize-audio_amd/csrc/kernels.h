@@ -283,6 +283,7 @@ struct RvqArgs {
     int32_t* const* codes_ref;  // non-null (a captured hipGraph): the codes pointer is read from here
     int frames_per_item;    // T (for [b][level][t] output); 0 -> [level][frame]
     void* work;             // rvq_work_bytes(frames): residual ping-pong + per-slice partial argmins
+    int sem_split;          // (set by launch_rvq) semantic + first acoustic level in one launch
 };
 size_t rvq_work_bytes(long long frames);
 hipError_t launch_rvq(const RvqArgs& a, hipStream_t s);

@@ -1000,21 +1000,27 @@ constexpr int RVQ_CS = 256;
 size_t rvq_work_bytes(long long frames) {
     const long long fp = (frames + RVQ_FT - 1) / RVQ_FT * RVQ_FT;
     const int nsl = 2048 / RVQ_CS;
-    return (size_t)(2 * fp * 256 * 4 + 2 * 2 * fp * nsl * 4);
+    return (size_t)(2 * fp * 256 * 4 + 2 * 3 * fp * nsl * 4);
 }
 
-// work layout: res[2][Fp][D] | pd[2][Fp][nsl] | pi[2][Fp][nsl]; parity = level & 1 (selected without
-// indexing a pointer array, which would live in scratch)
+// work layout: res[2][Fp][D] | pd[3][Fp][nsl] | pi[3][Fp][nsl]; residual parity = level & 1, partial-argmin slot =
+// rvq_slot (selected by arithmetic, not by indexing a pointer array, which would live in scratch)
 struct RvqWork {
     float* base;
     long long fp;
     int D, nsl;
     __device__ float* res(int par) const { return base + (par ? fp * D : 0); }
-    __device__ float* pd(int par) const { return base + 2 * fp * D + (par ? fp * nsl : 0); }
-    __device__ int* pi(int par) const {
-        return reinterpret_cast<int*>(base + 2 * fp * D + 2 * fp * nsl) + (par ? fp * nsl : 0);
+    __device__ float* pd(int slot) const { return base + 2 * fp * D + slot * fp * nsl; }
+    __device__ int* pi(int slot) const {
+        return reinterpret_cast<int*>(base + 2 * fp * D + 3 * fp * nsl) + slot * fp * nsl;
     }
 };
+
+// The split quantizer's semantic level (nsem = 1) and first acoustic level both start from the projection, so
+// they run as ONE launch (grid.z = 2, rvq_level_h16_kernel); the semantic level's partial argmins then go to a
+// third slot that no later level overwrites, and rvq_final_kernel writes code 0 from it.
+__device__ __forceinline__ bool rvq_sem_split(const RvqArgs& p) { return p.sem_split != 0; }
+__device__ __forceinline__ int rvq_slot(const RvqArgs& p, int L) { return (L == 0 && rvq_sem_split(p)) ? 2 : (L & 1); }
 
 __device__ __forceinline__ RvqWork rvq_work(const RvqArgs& p, int nsl) {
     RvqWork r;
@@ -1036,9 +1042,9 @@ __device__ __forceinline__ void rvq_store_code(const RvqArgs& p, int level, long
 }
 
 // merged argmin of level L over its slices (ties -> lower index; an all-NaN row keeps index 0)
-__device__ __forceinline__ int rvq_merge(const RvqWork& w, int L, long long f, int nsl, int ncodes) {
-    const float* pd = w.pd(L & 1) + f * nsl;
-    const int* pi = w.pi(L & 1) + f * nsl;
+__device__ __forceinline__ int rvq_merge(const RvqWork& w, int slot, long long f, int nsl, int ncodes) {
+    const float* pd = w.pd(slot) + f * nsl;
+    const int* pi = w.pi(slot) + f * nsl;
     float d = pd[0];
     int ix = pi[0];
     for (int q = 1; q < nsl; ++q) {
@@ -1071,7 +1077,7 @@ __global__ __launch_bounds__(512) void rvq_level_kernel(RvqArgs p, int L) {
         const long long f = f0 + tid;
         int ix = 0;
         if (f < p.frames) {
-            ix = rvq_merge(w, L - 1, f, NSL, p.ncodes);
+            ix = rvq_merge(w, rvq_slot(p, L - 1), f, NSL, p.ncodes);
             if (slice == 0) rvq_store_code(p, L - 1, f, ix);
         }
         prev[tid] = ix;
@@ -1183,8 +1189,8 @@ __global__ __launch_bounds__(512) void rvq_level_kernel(RvqArgs p, int L) {
             if (od < d || (od == d && oi < ix)) { d = od; ix = oi; }
         }
         const long long f = f0 + tid;
-        w.pd(L & 1)[f * NSL + slice] = d;
-        w.pi(L & 1)[f * NSL + slice] = ix;
+        w.pd(rvq_slot(p, L))[f * NSL + slice] = d;
+        w.pi(rvq_slot(p, L))[f * NSL + slice] = ix;
     }
 }
 
@@ -1193,7 +1199,8 @@ __global__ __launch_bounds__(256) void rvq_final_kernel(RvqArgs p, int L) {
     if (f >= p.frames) return;
     constexpr int NSL = 2048 / RVQ_CS;
     const RvqWork w = rvq_work(p, NSL);
-    rvq_store_code(p, L, f, rvq_merge(w, L, f, NSL, p.ncodes));
+    rvq_store_code(p, L, f, rvq_merge(w, rvq_slot(p, L), f, NSL, p.ncodes));
+    if (rvq_sem_split(p) && L > 0) rvq_store_code(p, 0, f, rvq_merge(w, rvq_slot(p, 0), f, NSL, p.ncodes));
 }
 
 // Approximate-then-exact form (default).  The distances above are exact only for the code that wins: per frame
@@ -1211,11 +1218,14 @@ __global__ __launch_bounds__(256) void rvq_final_kernel(RvqArgs p, int L) {
 // single launch chaining all levels per 32-frame workgroup measured 25 % slower: too few, too serial).
 constexpr int RVQ_CAND = 2048;
 
-// FT frames per workgroup (32 or 64): each wave streams its 32 codes' 32 KB of codebook planes from L2 once per
-// workgroup, so 64-frame tiles halve the per-CU codebook stream (one workgroup per CU: 145 KB of LDS)
-template <int D, int FT>
-__global__ __launch_bounds__(512, FT == 32 ? 2 : 1) void rvq_level_h16_kernel(RvqArgs p, int L) {
-    constexpr int RT = FT / 32;  // 32-frame row tiles per wave
+// 32 frames per workgroup (64-frame tiles, which halve the per-CU codebook stream, were slower: 1 workgroup per CU,
+// profiles/r2d_rvq_ft64.log).  PF: codebook k-steps in flight per wave (4: two workgroups per CU; 16 = all of them, for small batches whose few
+// workgroups wait on L2 / Infinity-Cache latency); EX: float4 of a code row in flight per exact re-score round
+template <int D, int PF = 4, int EX = 16>
+// (HIP's second launch bound is waves per SIMD: 4 = two 8-wave workgroups per CU, i.e. <= 128 VGPRs)
+__global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(RvqArgs p, int L0) {
+    const int L = L0 + (int)blockIdx.z;  // (grid.z = 2: the semantic and first acoustic levels together)
+    constexpr int FT = 32;
     constexpr int LDH = D / 2 + 4;
     constexpr int RLD = D + 8;  // fp16 plane rows: 528 B = 132 dwords (conflict-free b128 fragment reads)
     constexpr int NSL = 2048 / RVQ_CS;
@@ -1234,11 +1244,13 @@ __global__ __launch_bounds__(512, FT == 32 ? 2 : 1) void rvq_level_h16_kernel(Rv
     const RvqWork w = rvq_work(p, NSL);
 
     // ---- prologue (as rvq_level_kernel): finish level L-1, form r_L
+    // (the first acoustic level of a combined launch, blockIdx.z = 1, does not merge the semantic level running beside
+    // it: rvq_final_kernel does.  The test sits inside the merge branch: on the outer branch it cost 28 VGPRs)
     if (L >= 1 && tid < FT) {
         const long long f = f0 + tid;
         int ix = 0;
-        if (f < p.frames) {
-            ix = rvq_merge(w, L - 1, f, NSL, p.ncodes);
+        if (f < p.frames && blockIdx.z == 0) {
+            ix = rvq_merge(w, rvq_slot(p, L - 1), f, NSL, p.ncodes);
             if (slice == 0) rvq_store_code(p, L - 1, f, ix);
         }
         prev[tid] = ix;
@@ -1272,9 +1284,9 @@ __global__ __launch_bounds__(512, FT == 32 ? 2 : 1) void rvq_level_h16_kernel(Rv
         img[1][i][(k >> 1) + 1] = -2.0f * r.w;
     }
     __syncthreads();
-    // |r|^2 in torch's order (rvq_level_kernel) and max|r| per frame (16 threads per frame, 32 frames per pass)
-    for (int fi = tid >> 4; fi < FT; fi += 32) {
-        const int l = tid & 15;
+    // |r|^2 in torch's order (rvq_level_kernel) and max|r| per frame (16 threads per frame)
+    {
+        const int fi = tid >> 4, l = tid & 15;
         if (l < 8) {
             float a[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
@@ -1319,50 +1331,63 @@ __global__ __launch_bounds__(512, FT == 32 ? 2 : 1) void rvq_level_h16_kernel(Rv
     const int code0 = slice * RVQ_CS + wave * 32;
     const h8* bp = reinterpret_cast<const h8*>(p.cb_h16) +
                    ((long long)L * (p.ncodes / 32) + code0 / 32) * (D / 16) * 2 * 64 + lane;
-    f32x16 acc[RT];
+    f32x16 acc;
 #pragma unroll
-    for (int i = 0; i < RT; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
-    constexpr int PF = 4;
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
     h8 bq[PF][2];
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
         bq[q][0] = bp[q * 128];
         bq[q][1] = bp[q * 128 + 64];
     }
-#pragma unroll PF
-    for (int ks = 0; ks < D / 16; ++ks) {
+    auto kstep = [&](int ks) {
         const int cur = ks % PF;
         const h8 b0 = bq[cur][0], b1 = bq[cur][1];
         if (ks + PF < D / 16) {
             bq[cur][0] = bp[(ks + PF) * 128];
             bq[cur][1] = bp[(ks + PF) * 128 + 64];
         }
-#pragma unroll
-        for (int i = 0; i < RT; ++i) {
-            const h8 a0 = *reinterpret_cast<const h8*>(&rpl[0][i * 32 + (lane & 31)][ks * 16 + 8 * h]);
-            const h8 a1 = *reinterpret_cast<const h8*>(&rpl[1][i * 32 + (lane & 31)][ks * 16 + 8 * h]);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc[i], 0, 0, 0);
+        const h8 a0 = *reinterpret_cast<const h8*>(&rpl[0][lane & 31][ks * 16 + 8 * h]);
+        const h8 a1 = *reinterpret_cast<const h8*>(&rpl[1][lane & 31][ks * 16 + 8 * h]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
+    };
+    // (a template-dependent `#pragma unroll PF` is not honoured by hipcc -- the loop is then fully unrolled and
+    // the prefetch loads sunk to their uses -- so the two depths spell their unroll factor out)
+    if constexpr (PF == 4) {
+#pragma unroll 4
+        for (int ks = 0; ks < D / 16; ++ks) {
+            const int cur = ks % 4;
+            const h8 b0 = bq[cur][0], b1 = bq[cur][1];
+            if (ks + 4 < D / 16) {
+                bq[cur][0] = bp[(ks + 4) * 128];
+                bq[cur][1] = bp[(ks + 4) * 128 + 64];
+            }
+            const h8 a0 = *reinterpret_cast<const h8*>(&rpl[0][lane & 31][ks * 16 + 8 * h]);
+            const h8 a1 = *reinterpret_cast<const h8*>(&rpl[1][lane & 31][ks * 16 + 8 * h]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
         }
+    } else {
+        __builtin_amdgcn_sched_barrier(0);  // all PF k-steps' loads issued before the first MFMA
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) kstep(ks);
     }
     const int code = code0 + (lane & 31);
     const float yn = p.cb_norm[(long long)L * p.ncodes + code];
     const float cus = p.cb_unscale[L];
-    float ad[RT][16];
+    float ad[16];
 #pragma unroll
-    for (int i = 0; i < RT; ++i)
+    for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        ad[r] = (-2.0f * (acc[r] * (rus[row] * cus)) + xn[row]) + yn;
+        float m = ad[r];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            ad[i][r] = (-2.0f * (acc[i][r] * (rus[row] * cus)) + xn[row]) + yn;
-            float m = ad[i][r];
-#pragma unroll
-            for (int o = 16; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o));
-            if ((lane & 31) == 0) redd[wave][row] = m;
-        }
+        for (int o = 16; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+        if ((lane & 31) == 0) redd[wave][row] = m;
+    }
     __syncthreads();
     if (tid < FT) {
         float m = redd[0][tid];
@@ -1375,12 +1400,10 @@ __global__ __launch_bounds__(512, FT == 32 ? 2 : 1) void rvq_level_h16_kernel(Rv
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < RT; ++i)
-#pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
         // NaN distances (a non-finite residual) are candidates too: the exact path decides
-        if (!(ad[i][r] > smin[row] + win[row]) && f0 + row < p.frames) {
+        if (!(ad[r] > smin[row] + win[row]) && f0 + row < p.frames) {
             const unsigned slot = atomicAdd(&ncand, 1u);
             if (slot < RVQ_CAND) cand[slot] = ((unsigned)row << 16) | (unsigned)(code - slice * RVQ_CS);
         }
@@ -1397,12 +1420,12 @@ __global__ __launch_bounds__(512, FT == 32 ? 2 : 1) void rvq_level_h16_kernel(Rv
         if (f0 + row >= p.frames) continue;
         const f32x4* e = reinterpret_cast<const f32x4*>(cbr + (long long)c * D);
         float a = 0.0f;
-        for (int k0 = 0; k0 < D / 4; k0 += 16) {  // 16 float4 of the code row in flight, then the in-order chain
-            f32x4 ev[16];
+        for (int k0 = 0; k0 < D / 4; k0 += EX) {  // EX float4 of the code row in flight, then the in-order chain
+            f32x4 ev[EX];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) ev[j] = e[k0 + j];
+            for (int j = 0; j < EX; ++j) ev[j] = e[k0 + j];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
+            for (int j = 0; j < EX; ++j) {
                 const int k4 = k0 + j;
                 a = __builtin_fmaf(img[0][row][2 * k4], ev[j].x, a);
                 a = __builtin_fmaf(img[1][row][2 * k4], ev[j].y, a);
@@ -1419,20 +1442,30 @@ __global__ __launch_bounds__(512, FT == 32 ? 2 : 1) void rvq_level_h16_kernel(Rv
     if (tid < FT && f0 + tid < p.frames) {
         const unsigned long long b = best[tid];
         const long long f = f0 + tid;
-        w.pd(L & 1)[f * NSL + slice] = __uint_as_float((unsigned)(b >> 32));
-        w.pi(L & 1)[f * NSL + slice] = (int)(b & 0xffffffffu);
+        w.pd(rvq_slot(p, L))[f * NSL + slice] = __uint_as_float((unsigned)(b >> 32));
+        w.pi(rvq_slot(p, L))[f * NSL + slice] = (int)(b & 0xffffffffu);
     }
 }
 
-hipError_t launch_rvq(const RvqArgs& a, hipStream_t s) {
-    if (a.D != 256 || a.ncodes != 2048 || !a.work) return hipErrorInvalidValue;
+hipError_t launch_rvq(const RvqArgs& args, hipStream_t s) {
+    if (args.D != 256 || args.ncodes != 2048 || !args.work) return hipErrorInvalidValue;
+    RvqArgs a = args;
+    a.sem_split = (a.nsem == 1 && a.levels > 1 && a.cb_h16 && a.cb_unscale && a.cb_emax) ? 1 : 0;
     if (a.frames <= 0) return hipSuccess;
     if (a.cb_h16 && a.cb_unscale && a.cb_emax) {
         // (64-frame tiles, which halve the per-CU codebook stream, measured slower at B = 32: 0.56 vs 0.42 ms for 8
         // levels -- one workgroup per CU and 16 spilled VGPRs; profiles/r2d_rvq_ft64.log)
+        // small batches (fewer workgroups than CUs): every codebook k-step in flight at once and half a code row per
+        // exact round -- the same arithmetic, latency-bound waves wait once instead of four times
         const dim3 grid((unsigned)((a.frames + 31) / 32), 2048 / RVQ_CS);
-        for (int L = 0; L < a.levels; ++L) {
-            hipLaunchKernelGGL((rvq_level_h16_kernel<256, 32>), grid, dim3(512), 0, s, a, L);
+        const bool small = grid.x * grid.y < 256;
+        const bool split = a.sem_split != 0;  // levels 0 and 1 in one launch (rvq_sem_split)
+        for (int L = 0; L < a.levels; L += (split && L == 0) ? 2 : 1) {
+            const dim3 g(grid.x, grid.y, (split && L == 0) ? 2 : 1);
+            if (small)
+                hipLaunchKernelGGL((rvq_level_h16_kernel<256, 16, 32>), g, dim3(512), 0, s, a, L);
+            else
+                hipLaunchKernelGGL((rvq_level_h16_kernel<256>), g, dim3(512), 0, s, a, L);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

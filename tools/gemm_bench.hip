@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "gemm_planes.h"
@@ -160,6 +161,9 @@ int main(int argc, char** argv) {
         {"128x128 8w+4ld s3 P", launch_pl<128, 128, 4, 2, 2, 3, 4, 32, 16, FL_PERSIST | FL_PF, true>, 32, 12},
         {"128x128 4w+4ld s3 P", launch_pl<128, 128, 2, 2, 2, 3, 4, 32, 16, FL_PERSIST | FL_PF, true>, 32, 12},
         {"256x128 8w+4ld s3 P", launch_pl<256, 128, 4, 2, 2, 3, 4, 32, 16, FL_PERSIST | FL_PF, true>, 32, 12},
+        {"pair 256x256 bk16 mf32 8w(2x4) s3 0ld", launch_pl<256, 256, 2, 4, 2, 3, 0, 16, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair 256x256 bk16 mf32 8w(2x4)+4ld s3", launch_pl<256, 256, 2, 4, 2, 3, 4, 16, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
+        {"pair 256x256 bk16 mf32 8w(4x2)+4ld s3", launch_pl<256, 256, 4, 2, 2, 3, 4, 16, 32, FL_PAIR | FL_PERSIST, true>, 64, 12, true},
         {"pair PERSIST DIAG nodma", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NODMA, true>, 64, 12, true},
         {"pair PERSIST DIAG nomma", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NOMMA, true>, 64, 12, true},
         {"pair PERSIST DIAG both", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NODMA | FL_DIAG_NOMMA, true>, 64, 12, true},
@@ -250,7 +254,18 @@ int main(int argc, char** argv) {
         a.ldc = sh.N;
         const double flops = 2.0 * sh.batch * sh.tout * sh.N * K;
         std::vector<float> ref(nC), out(nC);
+        const char* vonly = argc > 3 ? argv[3] : nullptr;  // variant-name substrings, '|'-separated
         for (int v = 0; v < nv; ++v) {
+            if (vonly) {
+                bool hit = false;
+                for (const char* q = vonly; *q;) {
+                    const char* e = strchr(q, '|');
+                    const size_t n = e ? (size_t)(e - q) : strlen(q);
+                    if (n && std::string(vars[v].name).find(std::string(q, n)) != std::string::npos) hit = true;
+                    q += n + (e ? 1 : 0);
+                }
+                if (!hit) continue;
+            }
             if (K % vars[v].bk) continue;
             if (vars[v].pair && sh.k != 2 * sh.s) continue;
             a.C = v == 0 ? Cref : (v == 1 ? Cref2 : C);
