@@ -315,6 +315,9 @@ def test_full_size_batch_properties(engine):
     assert torch.equal(one[0], c1[5])
     c32 = engine.encode_int32(audio[:4].contiguous(), 32)
     assert torch.equal(c32[:, :8], c1[:4])
+    # B = 2 and 3 take the 16- and 32-row small-grid tiles (gemm.hip run_small_h16): same bits as B = 32
+    for nb in (2, 3):
+        assert torch.equal(engine.encode_int32(audio[6:6 + nb].contiguous(), 8), c1[6:6 + nb])
     # codes are not degenerate
     assert len(torch.unique(c1[:, 0])) > 500
 
