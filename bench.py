@@ -1,6 +1,6 @@
 """Throughput of the Mimi encode hot path on MI355X: audio-seconds encoded per wall-second (K = 8, 24 kHz).
 
-    python bench.py [--gpus N --steps K --warmup W --batch B --seconds S --workload batch|yodas2|mls]
+    python bench.py [--gpus N --steps K --warmup W --batch B --seconds S --workload batch|yodas2|mls [--bpe]]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 ``--gpus N`` without torchrun's environment launches N ranks itself (``torch.distributed.run`` as a child
@@ -86,6 +86,10 @@ def parse():
     ap.add_argument("--concurrency", type=int, default=0,
                     help="mls workload: engines encoding different utterances at once through "
                          "MimiEncoder.encode_audio_chunks (0 = 4)")
+    ap.add_argument("--bpe", action="store_true",
+                    help="mls workload: after the timed encodes, train codec-BPE (GPU merge loop) over the emitted "
+                         "codes on rank 0, timed separately (configs[4])")
+    ap.add_argument("--bpe-vocab-extra", type=int, default=2000, help="--bpe: learned tokens beyond the codes")
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage events")
     ap.add_argument("--no-f32-mode", action="store_true", help="skip the fp32-MFMA comparison run")
     ap.add_argument("--precision", default=None, help="GEMM precision mode (default: the engine's)")
@@ -290,13 +294,19 @@ class Workload:
                          f"from host memory through MimiEncoder.encode_audio_batch (pad to longest, H2D, encode, "
                          f"D2H, trim), K={K}, utterance round-robin over {world} GPU(s)")
         else:
+            self.emitted = []  # codes of the timed steps, for --bpe
+
             def step():
-                enc.encode_audio_chunks(self.clips[self.i], 24000)
+                out = enc.encode_audio_chunks(self.clips[self.i], 24000)
+                if self.i >= args.warmup:
+                    self.emitted.extend(out)
                 self.i += 1
             self.desc = (f"MLS-style stream (configs[4], encode part): {B} utterances U[{lo:g}, {hi:g}] s per step, "
                          f"each encoded alone at its own length (encode_audio_chunk semantics, batch 1, H2D + D2H "
                          f"included) through MimiEncoder.encode_audio_chunks with {conc} engine(s) at once, K={K}, "
-                         f"utterance round-robin over {world} GPU(s)")
+                         f"utterance round-robin over {world} GPU(s)" +
+                         ("; then codec-BPE training over the timed steps' codes on rank 0 (`bpe`, `pipeline_value`)"
+                          if args.bpe else ""))
         self.step = step
         self._np = np
 
@@ -304,6 +314,34 @@ class Workload:
         if self.kind == "batch":
             return self.audio_seconds * count
         return sum(self.step_seconds[first:first + count])
+
+
+def train_bpe_over_codes(args, wl, dist, rank, world, local, encode_s):
+    """configs[4]'s second half: codec-BPE over the codes this run emitted (codec-bpe/train_bpe_recipe.txt:18-28:
+    30 s chunks, max_token_codebook_ngrams 2), on rank 0 after the ranks' codes are gathered (host objects).
+    Reports the training time and the pipeline rate = timed audio-seconds / (encode + train)."""
+    from mimi_hip import bpe
+    codes = wl.emitted
+    if dist is not None:
+        parts = [None] * world if rank == 0 else None
+        dist.gather_object(codes, parts, dst=0)
+        codes = [c for p in parts for c in p] if rank == 0 else []
+    out = {}
+    if rank == 0:
+        K = args.num_quantizers
+        tr = bpe.Trainer(K, 2048, codec_framerate=12.5, chunk_size_secs=30,
+                         vocab_size=K * 2048 + 1 + args.bpe_vocab_extra, min_frequency=2, pad_token="<pad>",
+                         max_token_codebook_ngrams=2, device=local)
+        t0 = time.perf_counter()
+        tr.train_codes(codes)
+        bpe_s = time.perf_counter() - t0
+        audio_s = wl.timed_seconds(args.warmup, args.steps) * world
+        out = {"bpe": {"utterances": len(codes), "merges": len(tr.last_merges), "train_s": round(bpe_s, 3),
+                       "stats": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in tr.last_stats.items()}},
+               "pipeline_value": round(audio_s / (encode_s + bpe_s), 2)}
+    if dist is not None:
+        dist.barrier()
+    return out
 
 
 def main():
@@ -436,6 +474,8 @@ def main():
             stages[s_.split("#")[0]] = stages.get(s_.split("#")[0], 0.0) + v["ms"] / args.steps
         result["stages_ms_per_step"] = {s_: round(v, 3) for s_, v in stages.items()}
         result["north_star"] = north_star_groups(prof, args.steps, pmc_path)
+    if args.bpe and wl.kind == "mls":
+        result.update(train_bpe_over_codes(args, wl, dist, rank, world, local, elapsed))
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
         cb_batch = args.batch if wl.kind == "batch" else 1
         result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, cpu_threads(args.cpu_threads),

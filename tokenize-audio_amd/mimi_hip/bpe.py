@@ -41,6 +41,7 @@ import ctypes
 import glob
 import json
 import os
+import time
 import warnings
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple, Union
 
@@ -202,6 +203,10 @@ class Trainer:
                 "10,000) to allow for wide coverage of the most common codebook ngrams in your training data.")
         self._model = None
         self.last_stats: Dict[str, float] = {}
+        # the last training's learned tokens (alphabet-index tuples) and merges (left id, right id), ids counted
+        # from the special tokens: oracle/bpe_ref.train_bpe's convention
+        self.last_tokens: List[Tuple[int, ...]] = []
+        self.last_merges: List[Tuple[int, int]] = []
 
     # ---- corpus ----------------------------------------------------------------------------------
     def iterate_codepoints(self, codes_list: Iterable[np.ndarray]) -> Iterable[np.ndarray]:
@@ -248,12 +253,19 @@ class Trainer:
         if max_len == 1:
             tokens, merges = [], []
         else:
+            t0 = time.perf_counter()
             words, counts = self.words(codes_list)
+            corpus_s = time.perf_counter() - t0
             # tokenizers treats max_token_length as exclusive: codec_bpe passes the limit + 1
             tokens, merges = train_words_gpu(words, counts, n_base, len(self.special_tokens), self.vocab_size,
                                              self.min_frequency, max_len + 1 if max_len is not None else None,
                                              self.device, self.last_stats)
-        return self._assemble(tokens, merges)
+            self.last_stats["corpus_s"] = corpus_s  # host: chunks -> code points -> words (NFKC model)
+        self.last_tokens, self.last_merges = tokens, merges
+        t0 = time.perf_counter()
+        tok = self._assemble(tokens, merges)
+        self.last_stats["assemble_s"] = time.perf_counter() - t0  # tokenizers / transformers objects
+        return tok
 
     def train(self, codes_path: str, codes_filter: Optional[Union[str, List[str]]] = None,
               num_files: Optional[int] = None):
