@@ -1056,17 +1056,28 @@ __device__ __forceinline__ void rvq_store_code(const RvqArgs& p, int level, long
     }
 }
 
-// merged argmin of level L over its slices (ties -> lower index; an all-NaN row keeps index 0)
-__device__ __forceinline__ int rvq_merge(const RvqWork& w, int slot, long long f, int nsl, int ncodes) {
-    const float* pd = w.pd(slot) + f * nsl;
-    const int* pi = w.pi(slot) + f * nsl;
-    float d = pd[0];
-    int ix = pi[0];
-    for (int q = 1; q < nsl; ++q) {
-        const float od = pd[q];
-        const int oi = pi[q];
-        if (od < d || (od == d && oi < ix)) { d = od; ix = oi; }
+// merged argmin of level L over its slices (ties -> lower index; an all-NaN row keeps index 0).  All NSL
+// (distance, index) pairs are loaded as 16-B vectors before the first compare: a runtime-length loop waited out
+// one memory round trip per slice, on the critical path of every level's prologue.
+template <int NSL>
+__device__ __forceinline__ int rvq_merge(const RvqWork& w, int slot, long long f, int ncodes) {
+    static_assert(NSL % 4 == 0, "slices in 16-B groups");
+    const float* pd = w.pd(slot) + f * NSL;  // 16-B aligned: the work layout's offsets are multiples of 4 floats
+    const int* pi = w.pi(slot) + f * NSL;
+    float dv[NSL];
+    int iv[NSL];
+#pragma unroll
+    for (int q = 0; q < NSL; q += 4) {
+        const float4 a = *reinterpret_cast<const float4*>(pd + q);
+        const int4 b = *reinterpret_cast<const int4*>(pi + q);
+        dv[q] = a.x; dv[q + 1] = a.y; dv[q + 2] = a.z; dv[q + 3] = a.w;
+        iv[q] = b.x; iv[q + 1] = b.y; iv[q + 2] = b.z; iv[q + 3] = b.w;
     }
+    float d = dv[0];
+    int ix = iv[0];
+#pragma unroll
+    for (int q = 1; q < NSL; ++q)
+        if (dv[q] < d || (dv[q] == d && iv[q] < ix)) { d = dv[q]; ix = iv[q]; }
     return (ix < 0 || ix >= ncodes) ? 0 : ix;
 }
 
@@ -1092,7 +1103,7 @@ __global__ __launch_bounds__(512) void rvq_level_kernel(RvqArgs p, int L) {
         const long long f = f0 + tid;
         int ix = 0;
         if (f < p.frames) {
-            ix = rvq_merge(w, rvq_slot(p, L - 1), f, NSL, p.ncodes);
+            ix = rvq_merge<NSL>(w, rvq_slot(p, L - 1), f, p.ncodes);
             if (slice == 0) rvq_store_code(p, L - 1, f, ix);
         }
         prev[tid] = ix;
@@ -1214,8 +1225,8 @@ __global__ __launch_bounds__(256) void rvq_final_kernel(RvqArgs p, int L) {
     if (f >= p.frames) return;
     constexpr int NSL = 2048 / RVQ_CS;
     const RvqWork w = rvq_work(p, NSL);
-    rvq_store_code(p, L, f, rvq_merge(w, rvq_slot(p, L), f, NSL, p.ncodes));
-    if (rvq_sem_split(p) && L > 0) rvq_store_code(p, 0, f, rvq_merge(w, rvq_slot(p, 0), f, NSL, p.ncodes));
+    rvq_store_code(p, L, f, rvq_merge<NSL>(w, rvq_slot(p, L), f, p.ncodes));
+    if (rvq_sem_split(p) && L > 0) rvq_store_code(p, 0, f, rvq_merge<NSL>(w, rvq_slot(p, 0), f, p.ncodes));
 }
 
 // Approximate-then-exact form (default).  The distances above are exact only for the code that wins: per frame
@@ -1265,7 +1276,7 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
         const long long f = f0 + tid;
         int ix = 0;
         if (f < p.frames && blockIdx.z == 0) {
-            ix = rvq_merge(w, rvq_slot(p, L - 1), f, NSL, p.ncodes);
+            ix = rvq_merge<NSL>(w, rvq_slot(p, L - 1), f, p.ncodes);
             if (slice == 0) rvq_store_code(p, L - 1, f, ix);
         }
         prev[tid] = ix;
