@@ -316,7 +316,7 @@ class Workload:
         return sum(self.step_seconds[first:first + count])
 
 
-def train_bpe_over_codes(args, wl, dist, rank, world, local, encode_s):
+def train_bpe_over_codes(args, wl, dist, rank, world, device, encode_s):
     """configs[4]'s second half: codec-BPE over the codes this run emitted (codec-bpe/train_bpe_recipe.txt:18-28:
     30 s chunks, max_token_codebook_ngrams 2), on rank 0 after the ranks' codes are gathered (host objects).
     Reports the training time and the pipeline rate = timed audio-seconds / (encode + train)."""
@@ -331,7 +331,7 @@ def train_bpe_over_codes(args, wl, dist, rank, world, local, encode_s):
         K = args.num_quantizers
         tr = bpe.Trainer(K, 2048, codec_framerate=12.5, chunk_size_secs=30,
                          vocab_size=K * 2048 + 1 + args.bpe_vocab_extra, min_frequency=2, pad_token="<pad>",
-                         max_token_codebook_ngrams=2, device=local)
+                         max_token_codebook_ngrams=2, device=device)
         t0 = time.perf_counter()
         tr.train_codes(codes)
         bpe_s = time.perf_counter() - t0
@@ -357,13 +357,26 @@ def main():
 
     import torch
     dist = None
+    # one GPU per rank (LOCAL_RANK); MIMI_BENCH_DIST_BACKEND=gloo rehearses the N-rank path on a box with fewer
+    # GPUs than ranks (ranks share cuda:(LOCAL_RANK mod devices); barrier and reductions go over gloo on the host)
+    backend = os.environ.get("MIMI_BENCH_DIST_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        sys.exit(f"bench.py: MIMI_BENCH_DIST_BACKEND={backend}: expected nccl or gloo")
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        sys.exit("bench.py: no HIP device")
+    if backend == "nccl" and world > ndev:
+        sys.exit(f"bench.py: {world} ranks but {ndev} GPU(s) (MIMI_BENCH_DIST_BACKEND=gloo shares GPUs)")
+    dev = torch.device("cuda", local % ndev)
+    torch.cuda.set_device(dev)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from mimi_hip import synthetic
     from mimi_hip.model import MimiHipModel
@@ -404,7 +417,7 @@ def main():
     elapsed = t1 - t0
     audio_s = wl.timed_seconds(args.warmup, args.steps)
     if dist is not None:
-        t = torch.tensor([elapsed, audio_s], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, audio_s], dtype=torch.float64, device=red_dev)
         tmax = t[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -475,7 +488,7 @@ def main():
         result["stages_ms_per_step"] = {s_: round(v, 3) for s_, v in stages.items()}
         result["north_star"] = north_star_groups(prof, args.steps, pmc_path)
     if args.bpe and wl.kind == "mls":
-        result.update(train_bpe_over_codes(args, wl, dist, rank, world, local, elapsed))
+        result.update(train_bpe_over_codes(args, wl, dist, rank, world, dev.index, elapsed))
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
         cb_batch = args.batch if wl.kind == "batch" else 1
         result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, cpu_threads(args.cpu_threads),
