@@ -263,8 +263,9 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         case ROLE_DOWN: return run_planes_big<EPI_BIAS, 0, 0, 2>(a, s, prec);
         case ROLE_DOWN_ELU: return run_planes_big_ld<EPI_BIAS_ELU, 3, 2, 3>(a, s, prec);  // planes out: final conv
         case ROLE_FINAL: return run_planes_small_ld<EPI_BIAS_OUT, 4>(a, s, prec);
-        case ROLE_QKV:  // fp16: a 2-stage ring, -10 % vs 4 stages (profiles/r1l_ab_small_kernels.txt)
-            if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 2, EPI_ROPE, 0, 5, 0, 32, 16, 0, true>(a, s);
+        case ROLE_QKV:  // fp16: a 2-stage ring, -10 % vs 4 stages (profiles/r1l_ab_small_kernels.txt); 4 loader waves:
+                        // -3.6 % (fc1 +11 % with them; 3 stages +1 %: profiles/r2e_ab_loaders_*.log)
+            if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 2, EPI_ROPE, 0, 5, 4, 32, 16, 0, true>(a, s);
             return run_planes_small<EPI_ROPE, 5>(a, s, prec);  // (256x256: -11 % alone, 0 in the engine)
         case ROLE_OPROJ: return run_planes_small_ld<EPI_SCALE_RES, 6>(a, s, prec);
         case ROLE_FC1:  // planes out: fc2; fp16: 128x128 on a 2-stage ring (two workgroups per CU): -4 % vs
@@ -282,8 +283,9 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
             return run_planes_big<EPI_BIAS_ELU, 3, 2, 12>(a, s, prec);
         case ROLE_RES1P:  // K = C/2 = 128 / 256: short K, output-heavy
             if (prec == PREC_F16X3)  // fp16: 128x128 x 8 waves on a 2-stage ring (64 KiB, two workgroups per CU):
-                                     // -18 % vs 128x64 x 4 waves (profiles/r2c_ab_dispatch.log)
-                return run_planes<128, 128, 4, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13, 0, 32, 16, 0, true>(a, s);
+                                     // -18 % vs 128x64 x 4 waves (profiles/r2c_ab_dispatch.log); + 4 loader
+                                     // waves: -4..-5 % (profiles/r2e_ab_loaders_res1.log)
+                return run_planes<128, 128, 4, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13, 4, 32, 16, 0, true>(a, s);
             if (prec == PREC_BF16X6) return run_planes<128, 64, 2, 2, 3, 2, EPI_BIAS_RES_ELU, 3, 13>(a, s);
             return run_planes<128, 64, 2, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13>(a, s);
         default: return hipErrorInvalidValue;
