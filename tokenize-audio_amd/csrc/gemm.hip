@@ -124,8 +124,10 @@ static hipError_t run_planes_small(const GemmArgs& a, hipStream_t s, int prec) {
 }
 template <int EPI, int TAG>
 static hipError_t run_planes_small_ld(const GemmArgs& a, hipStream_t s, int prec) {
-    // fp16: 3 stages (o_proj / fc2 -2 %, final conv equal vs 4; profiles/r1l_ab_small_kernels.txt)
-    if (prec == PREC_F16X3) return run_planes<128, 128, 2, 2, 2, 3, EPI, 0, TAG, 4, 32, 16, 0, true>(a, s);
+    // fp16: 3 stages (o_proj / fc2 -2 %, final conv equal vs 4; profiles/r1l_ab_small_kernels.txt); 8 compute
+    // waves instead of 4 (N = 512: 252 tiles, one round, so shorter per-tile chains win): o_proj -3 %, fc2 -1.4 %
+    // (profiles/r2e_ab_8waves_oproj_fc2.log)
+    if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 3, EPI, 0, TAG, 4, 32, 16, 0, true>(a, s);
     if (prec == PREC_BF16X6) return run_planes<128, 128, 2, 2, 3, 3, EPI, 0, TAG, 4>(a, s);
     return run_planes<128, 128, 2, 2, 2, 3, EPI, 0, TAG, 4>(a, s);
 }
@@ -246,7 +248,7 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
     if (prec == PREC_F16X3) {
         switch (role) {
             case ROLE_FC2:
-                if (a.Cp) return run_planes<128, 128, 2, 2, 2, 3, EPI_SCALE_RES, 2, 8, 4, 32, 16, 0, true>(a, s);
+                if (a.Cp) return run_planes<128, 128, 4, 2, 2, 3, EPI_SCALE_RES, 2, 8, 4, 32, 16, 0, true>(a, s);
                 break;
             case ROLE_DOWNSAMPLE: return run_planes<128, 128, 4, 2, 2, 2, EPI_NONE, 2, 9, 0, 32, 16, 0, true>(a, s);
             case ROLE_INPROJ: return run_planes<128, 128, 4, 2, 2, 2, EPI_NONE, 0, 10, 0, 32, 16, 0, true>(a, s);
