@@ -94,6 +94,10 @@ def parse():
     ap.add_argument("--no-f32-mode", action="store_true", help="skip the fp32-MFMA comparison run")
     ap.add_argument("--precision", default=None, help="GEMM precision mode (default: the engine's)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--dump-sequence", default=None,
+                    help="write the engine's per-encode (stage, kernel) launch sequence here (PMC stage keys)")
+    ap.add_argument("--pmc-pass", action="store_true",
+                    help="counter pass: the timed steps only (no PCIe / f32 / B=64 extras, no CPU baseline)")
     return ap.parse_args()
 
 
@@ -108,23 +112,48 @@ def self_launch(args) -> int:
     return subprocess.call(cmd)
 
 
-def cpu_threads(requested: int) -> int:
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup's CPU quota (v2 cpu.max / v1 cfs_quota_us), or None when unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_threads(requested: int):
+    """(threads, note): the CPUs this process may use -- its affinity, capped by a cgroup CPU quota and by the
+    pool's per-GPU CPU share when one is set (OMP_NUM_THREADS on the GPU box: 16 CPUs per GPU; running more threads
+    there would take other jobs' cores) -- and the reason for the number."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = cgroup_cpu_quota()
     if requested > 0:
-        return requested
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    cap = os.environ.get("OMP_NUM_THREADS")
-    if cap and cap.isdigit() and int(cap) > 0:
-        n = min(n, int(cap))
-    return max(1, n)
+        return requested, f"{requested} threads requested (affinity {aff}, cgroup quota {quota or 'none'})"
+    n, why = aff, f"all {aff} CPUs of the process affinity"
+    if quota is not None and int(quota) < n:
+        n, why = max(1, int(quota)), f"cgroup CPU quota {quota:g} CPUs (affinity {aff})"
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and 0 < int(share) < n:
+        n, why = int(share), (f"the pool's per-GPU CPU share OMP_NUM_THREADS={share} (process affinity {aff}, "
+                              f"cgroup quota {'%g' % quota if quota else 'none'})")
+    return max(1, n), why
 
 
-def cpu_baseline(seconds_budget: float, threads: int, clip_s: float, batch: int):
+def cpu_baseline(seconds_budget: float, threads_why, clip_s: float, batch: int):
     """The oracle on the host cores, same metric: whole clips at batch 1 (config 1 of BASELINE.json) and at the
     GPU workload's batch, each on about half the budget.  ``value`` is the rate at the GPU's batch size."""
     import torch
 
     from mimi_hip import synthetic
     from oracle import mimi_ref
+    threads, why = threads_why
     torch.set_num_threads(threads)
     sd = synthetic.make_state_dict(seed=0, num_quantizers=8)
     sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
@@ -148,9 +177,8 @@ def cpu_baseline(seconds_budget: float, threads: int, clip_s: float, batch: int)
     sample = "; ".join(f"batch {b}: {d} encode(s) of {b} x {clip_s:g} s = {r:.1f} audio-s/s"
                        for b, (r, d) in rates.items())
     return {"value": round(rates[batch][0], 3), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
-            "sample": f"{sample}; K=8, oracle/mimi_ref.py (torch {torch.__version__} CPU, {threads} threads of "
-                      f"{len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else '?'} in this "
-                      f"process's affinity, {cpu_model})",
+            "sample": f"{sample}; K=8, oracle/mimi_ref.py (torch {torch.__version__} CPU, {threads} threads: {why}; "
+                      f"{cpu_model})",
             "batch1_value": round(rates[1][0], 3)}
 
 
@@ -165,15 +193,29 @@ def pmc_lookup(pmc_kernels, name):
     return pmc_kernels.get(bare, {})
 
 
+def pmc_stage(pmc, stage, kernel):
+    """PMC bytes of a stage: the stage-keyed entry (tools/summarize_profile.py aligns the counter rows to the engine's
+    launch sequence), else the kernel-symbol entry.  Returns (bytes per launch or None, the measured kernel,
+    whether that kernel is this run's)."""
+    bare = lambda k: (k or "").replace("void ", "", 1).split("(")[0].strip()  # noqa: E731
+    st = pmc.get("stages", {}).get(stage.split("#")[0])
+    if st and "traffic_bytes" in st:
+        return st["traffic_bytes"], st.get("kernel"), bare(st.get("kernel")) == bare(kernel)
+    k = pmc_lookup(pmc.get("kernels", {}), kernel)
+    if "traffic_bytes" in k:
+        return k["traffic_bytes"], kernel, True
+    return None, None, False
+
+
 def north_star_groups(prof, steps, pmc_path):
     """BASELINE.json's reporting asks: HBM GB/s and TFLOP/s of the SEANet conv stack, MFMA utilisation of the
     transformer.  Device ms and algorithmic FLOPs from the engine's events; HBM bytes = the PMC passes'
-    FETCH_SIZE x 2 + WRITE_SIZE per launch of each kernel symbol (profiles/pmc_summary.json; a symbol shared
-    by several stages carries its average) x that stage's launches."""
+    FETCH_SIZE x 2 + WRITE_SIZE per launch of each STAGE (profiles/pmc_summary.json, keyed by stage; by kernel
+    symbol as a fallback) x that stage's launches."""
     pmc = {}
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
-            pmc = json.load(f).get("kernels", {})
+            pmc = json.load(f)
     base = lambda s: s.split("#")[0]  # noqa: E731  ("fc2#2": the same stage on a second kernel symbol)
     groups = {
         "conv_stack": [s for s in prof if base(s).startswith(("res", "down_s", "final"))],
@@ -186,14 +228,17 @@ def north_star_groups(prof, steps, pmc_path):
             continue
         ms = sum(prof[s]["ms"] for s in stages) / steps
         fl = sum(prof[s]["flops"] for s in stages) / steps
-        hbm = [pmc_lookup(pmc, prof[s]["kernel"]).get("traffic_bytes") for s in stages]
+        looked = [pmc_stage(pmc, s, prof[s]["kernel"]) for s in stages]
         d = {"stages": stages, "ms_per_step": round(ms, 3), "tflops": round(fl / (ms / 1e3) / 1e12, 1),
              "frac_f16x3_peak": round(fl / (ms / 1e3) / 1e12 / F16X3_PEAK_TFLOPS, 4)}
-        missing = [prof[s]["kernel"] for s, b in zip(stages, hbm) if b is None]
+        missing = [s for s, (b, _, _) in zip(stages, looked) if b is None]
+        stale = [s for s, (b, _, same) in zip(stages, looked) if b is not None and not same]
+        if stale:
+            d["hbm_measured_on_other_kernel"] = stale
         if missing:
-            d["hbm_unmeasured_kernels"] = sorted(set(missing))
+            d["hbm_unmeasured_stages"] = missing
         else:
-            by = sum(b * prof[s]["launches"] / steps for b, s in zip(hbm, stages))
+            by = sum(b * prof[s]["launches"] / steps for (b, _, _), s in zip(looked, stages))
             d.update({"hbm_bytes_per_step": round(by), "hbm_GBps": round(by / (ms / 1e3) / 1e9, 1),
                       "frac_hbm_peak": round(by / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)})
         out[g] = d
@@ -227,11 +272,19 @@ def roofline_from_profile(prof, steps):
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f)
-        k = pmc_lookup(pmc.get("kernels", {}), dom_name)
-        if "traffic_bytes" in k:
-            traffic = round(k["traffic_bytes"])
+        # the dominant kernel's stages, launch-weighted
+        looked = [(pmc_stage(pmc, st, dom_name), prof[st]["launches"]) for st in dom["stages"]]
+        if all(b is not None for (b, _, _), _ in looked):
+            n = sum(l for _, l in looked)
+            traffic = round(sum(b * l for (b, _, _), l in looked) / n)
             traffic_src = {"source": f"profiles/{pmc['tag']}_pmc_summary.json", "unit": "bytes per launch",
-                           "fetch_bytes": round(k["fetch_bytes"]), "write_bytes": round(k["write_bytes"])}
+                           "keyed_by": "stage" if all(st.split("#")[0] in pmc.get("stages", {}) for st in dom["stages"])
+                           else "kernel", "measured_kernel_is_this_build": all(same for (_, _, same), _ in looked)}
+            ks = [pmc.get("stages", {}).get(st.split("#")[0]) or pmc_lookup(pmc.get("kernels", {}), dom_name)
+                  for st in dom["stages"]]
+            if all("fetch_bytes" in k and "write_bytes" in k for k in ks):
+                traffic_src["fetch_bytes"] = round(sum(k["fetch_bytes"] for k in ks) / len(ks))
+                traffic_src["write_bytes"] = round(sum(k["write_bytes"] for k in ks) / len(ks))
     roof.update({"traffic": traffic, "traffic_detail": traffic_src, "kernel": dom_name, "stages": dom["stages"],
                  "avg_launch_ms": round(1000 * t_launch, 4), "launches": dom["launches"],
                  "algorithmic_per_launch": dom["flops"] / dom["launches"] if gemm_like
@@ -390,8 +443,10 @@ def main():
     if args.precision:
         model.set_precision(args.precision)
     wl = Workload(args, model, dev, world, rank)
+    if model.precision == "f16x3":
+        model.calibrate()  # (otherwise inside the first encode) -- before the trace marker
     # trace marker (a torch `spin_kernel`): rocprofv3 summaries keep the dispatches after it, i.e. drop the
-    # calibration encode mimi_finalize ran at model creation (tools/summarize_profile.py)
+    # f16x3 calibration encode (tools/summarize_profile.py)
     torch.cuda.synchronize()
     torch.cuda._sleep(100)
     torch.cuda.synchronize()
@@ -436,6 +491,9 @@ def main():
     if profile:
         model.set_profiling(False)
         prof = model.profile_read()
+        if args.dump_sequence and rank == 0:
+            with open(args.dump_sequence, "w") as f:
+                json.dump(model.profile_sequence(), f)
 
     value = audio_s / elapsed
     result = {
@@ -456,7 +514,15 @@ def main():
                    "num_quantizers": K, "parallelism": f"utterance round-robin x{world} (no collective)",
                    "gemm_precision": model.precision},
     }
-    if wl.kind == "batch":
+    if model.precision == "f16x3":
+        # fixed activation scales on these weights: overflow fallbacks taken, and the tightest tensor's headroom
+        # (2^15 / (scale x max|x|) of the last encode; < 1 = an overflow)
+        sc = {k: v for k, v in model.act_scales().items() if v[1] > 0}
+        tight = min(sc.items(), key=lambda kv: kv[1][2]) if sc else None
+        result["f16x3"] = {"f16_reruns": model.f16_reruns,
+                           "min_headroom": round(tight[1][2], 2) if tight else None,
+                           "min_headroom_tensor": tight[0] if tight else None}
+    if wl.kind == "batch" and not args.pmc_pass:
         # PCIe-inclusive rate (host f32 in -> device codes -> host): reported beside, never as `value`
         n = max(1, min(args.steps, 3))
         torch.cuda.synchronize()
@@ -479,6 +545,28 @@ def main():
             torch.cuda.synchronize()
             result["f32_mode_value"] = round(world * n32 * wl.audio_seconds / (time.perf_counter() - tf0), 2)
             model.set_precision(prev)
+        if args.batch == 32 and args.seconds == 10.0:
+            # BASELINE configs[2] (Emilia, batch 64 x 10 s), the largest single-GPU config, beside the headline
+            import numpy as np  # noqa: F401
+            from mimi_hip import synthetic
+            from mimi_hip.config import encoded_length
+            L = 240000
+            a64 = torch.from_numpy(synthetic.clip_batch(64, L, seed=2000 + rank)).to(dev)
+            c64 = torch.empty((64, K, encoded_length(L)), dtype=torch.int32, device=dev)
+            for _ in range(2):
+                model.encode_int32(a64, K, out=c64)
+            n64 = max(1, min(args.steps, 10))
+            barrier()
+            torch.cuda.synchronize()
+            t640 = time.perf_counter()
+            for _ in range(n64):
+                model.encode_int32(a64, K, out=c64)
+            torch.cuda.synchronize()
+            el64 = time.perf_counter() - t640
+            result["configs2_b64"] = {"value": round(world * n64 * 64 * 10.0 / el64, 2),
+                                      "ms_per_step": round(1000 * el64 / n64, 3), "steps": n64,
+                                      "workload": "Emilia-style batch (configs[2]): 64 x 10 s resident in HBM, K=8"}
+            del a64, c64
     if profile_separately:
         result["stages_source"] = "a separate profiled pass of the same steps (timed region: hipGraph replays)"
     result["graph_replays"] = model.graph_replays
@@ -493,7 +581,7 @@ def main():
         result["north_star"] = north_star_groups(prof, args.steps, pmc_path)
     if args.bpe and wl.kind == "mls":
         result.update(train_bpe_over_codes(args, wl, dist, rank, world, dev.index, elapsed))
-    if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0 and not args.pmc_pass:
         cb_batch = args.batch if wl.kind == "batch" else 1
         result["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, cpu_threads(args.cpu_threads),
                                               args.seconds if wl.kind == "batch" else 15.0, cb_batch)

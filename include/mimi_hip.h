@@ -126,9 +126,9 @@ int mimi_rvq_encode(mimi_engine* e, const float* dev_embedding, int64_t frames, 
  *   MIMI_PRECISION_BF16X3  2 planes, 3 products (~1e-5 relative, 5.3x MFMA rate)
  *   MIMI_PRECISION_F16X3   (default) fp32 emulated on the fp16 matrix cores: both operands split into 2 fp16
  *                          planes (22-bit significand) at power-of-two scales, 3 products.  Activation scales
- *                          are fixed per tensor at mimi_finalize from a calibration encode (never from the
- *                          caller's audio: an item's codes depend on its own samples and the padded length
- *                          only).  mimi_encode reads the activations' maxima back after the encode (it
+ *                          are fixed per tensor by a calibration encode on built-in signals, run once before
+ *                          the engine's first f16x3 encode or by mimi_calibrate (never from the caller's audio:
+ *                          an item's codes depend on its own samples and the padded length only).  mimi_encode reads the activations' maxima back after the encode (it
  *                          synchronises its stream in this mode); on an overflow of a fixed scale each item is
  *                          re-encoded alone, and in bf16x6 if it overflows alone.
  */
@@ -136,6 +136,9 @@ enum { MIMI_PRECISION_F32 = 0, MIMI_PRECISION_BF16X6 = 1, MIMI_PRECISION_BF16X3 
 /* default: MIMI_PRECISION_F16X3 */
 int mimi_set_precision(mimi_engine* e, int32_t mode);
 int mimi_get_precision(const mimi_engine* e);
+/* MIMI_PRECISION_F16X3: run the activation-scale calibration now (idempotent; otherwise it runs inside the first
+ * f16x3 encode).  Synchronises the device. */
+int mimi_calibrate(mimi_engine* e);
 /* MIMI_PRECISION_F16X3: encodes that took the overflow fallback so far (diagnostic). */
 int64_t mimi_f16_reruns(const mimi_engine* e);
 /* hipGraph replay of MIMI_PRECISION_F16X3 encodes (default on): the second encode of a (batch, length, K) shape
@@ -215,6 +218,9 @@ int mimi_set_profiling(mimi_engine* e, int enable);
 int mimi_profile_read(mimi_engine* e, int32_t max_stages, char* names /* max_stages*128 */,
                       double* total_ms, int64_t* launches, double* flops_bytes, int32_t* n_stages);
 int mimi_profile_reset(mimi_engine* e);
+/* The "stage|kernel symbol" names of the last profiled encode, in launch order (one entry per stage event; a
+ * stage's first dispatch is its named kernel).  Lets a rocprofv3 counter pass key its dispatches by stage. */
+int mimi_profile_sequence(mimi_engine* e, int32_t max_stages, char* names /* max_stages*128 */, int32_t* n_stages);
 
 /* When enabled, mimi_encode keeps a copy of each stage's output (for per-stage parity tests). */
 int mimi_set_taps(mimi_engine* e, int enable);

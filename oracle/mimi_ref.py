@@ -236,9 +236,11 @@ def encode(input_values, sd, num_quantizers: Optional[int] = None, cfg: Optional
     return codes.transpose(0, 1)
 
 
-def rvq_from_embedding(emb, sd, K: int, cfg: Optional[RefConfig] = None, return_margins: bool = False):
+def rvq_from_embedding(emb, sd, K: int, cfg: Optional[RefConfig] = None, return_margins: bool = False,
+                       return_second: bool = False):
     """Quantizer alone on a given pre-quantizer embedding [B,512,T] -> codes [B,K,T] (+ per-code relative
-    margin between best and second-best distance, for the near-tie audit)."""
+    margin (d2 - d1) / d2 between the best and second-best distance, for the near-tie audit; + d2 itself with
+    return_second, for the perturbation-derived audit threshold of tests/audit.py)."""
     cfg = cfg or RefConfig()
     sdt = {k: (v if torch.is_tensor(v) else torch.from_numpy(np.asarray(v))) for k, v in sd.items()}
     emb = emb if torch.is_tensor(emb) else torch.from_numpy(np.asarray(emb))
@@ -246,7 +248,7 @@ def rvq_from_embedding(emb, sd, K: int, cfg: Optional[RefConfig] = None, return_
         codes = split_rvq_encode(emb.float(), sdt, K, cfg).transpose(0, 1)
         if not return_margins:
             return codes
-        margins = []
+        margins, seconds = [], []
         for which, levels in (("semantic", range(cfg.num_semantic_quantizers)),
                               ("acoustic", range(K - cfg.num_semantic_quantizers))):
             pre = f"quantizer.{which}_residual_vector_quantizer."
@@ -259,6 +261,9 @@ def rvq_from_embedding(emb, sd, K: int, cfg: Optional[RefConfig] = None, return_
                 d = torch.cdist(flat[None], embed[None], p=2)[0]
                 top2 = torch.topk(d, 2, dim=-1, largest=False).values
                 margins.append(((top2[:, 1] - top2[:, 0]) / top2[:, 1].clamp_min(1e-30)).view(B, T))
+                seconds.append(top2[:, 1].view(B, T))
                 idx = d.argmin(dim=-1).view(B, T)
                 r = r - F.embedding(idx, embed).permute(0, 2, 1)
+        if return_second:
+            return codes, torch.stack(margins, dim=1), torch.stack(seconds, dim=1)
         return codes, torch.stack(margins, dim=1)

@@ -12,8 +12,31 @@ for p in (PKG, ROOT):
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+_PARITY_LOG = []
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def parity_log():
+    """Parity tests append {test, codes, exact, chain_flips, max_flip_margin, ...}; the session writes them to
+    gpurun_out/parity_report.json (copied into profiles/ with the round's evidence)."""
+    return _PARITY_LOG
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if not _PARITY_LOG:
+        return
+    import json
+    out = os.path.join(ROOT, "gpurun_out")
+    try:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "parity_report.json"), "w") as f:
+            json.dump({"exitstatus": int(exitstatus), "records": _PARITY_LOG}, f, indent=1)
+    except OSError:
+        pass
 
 
 @pytest.fixture(scope="session")

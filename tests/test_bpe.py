@@ -178,3 +178,22 @@ def test_gpu_trainer_matches_oracle_on_random_corpora():
         gt, gm = bpe.train_words_gpu(words, counts, nalpha, 1, vs, mf, ml)
         assert gm == merges, case
         assert gt == [t for t in toks[1 + nalpha:]], case
+
+
+@pytest.mark.gpu
+def test_gpu_trainer_counts_beyond_2_30():
+    """Pair counts are int64 on the device (two-sweep best pair): word counts near 2^31 push pair totals past 2^30
+    and 2^32, where the old packed 64-bit max (count << 34) refused the corpus; merges == the oracle's."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    rng = np.random.default_rng(12)
+    for case in range(4):
+        nalpha = 6
+        words = [rng.integers(0, nalpha, size=int(rng.integers(2, 20))).astype(np.int32) for _ in range(12)]
+        counts = rng.integers((1 << 31) - 1000, (1 << 31) - 1, size=len(words))
+        counts[case] = 3  # one rare word: its pairs lose every count tie
+        toks, merges = train_bpe([w + 1 for w in words], counts, nalpha, 1, 1 + nalpha + 30, 2, None)
+        gt, gm = bpe.train_words_gpu(words, counts, nalpha, 1, 1 + nalpha + 30, 2, None)
+        assert gm == merges, case
+        assert gt == [t for t in toks[1 + nalpha:]], case

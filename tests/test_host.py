@@ -125,12 +125,13 @@ def test_import_without_gpu_has_no_fallback():
 
 
 def test_bench_north_star_groups(tmp_path):
-    """bench.py's north-star breakdown: stage grouping, PMC lookup by bare symbol, HBM rate arithmetic."""
+    """bench.py's north-star breakdown: stage grouping, PMC lookup by stage (then by bare symbol), HBM rate
+    arithmetic, and a stage measured on another build's kernel flagged."""
     import sys
     sys.path.insert(0, ROOT)
     import bench
-    pmc = {"tag": "t", "kernels": {"mimi::resblock0_h16_kernel": {"traffic_bytes": 2.0e9},
-                                   "mimi::gemm_planes_kernel<1, 2>": {"traffic_bytes": 1.0e9}}}
+    pmc = {"tag": "t", "kernels": {"mimi::resblock0_h16_kernel": {"traffic_bytes": 2.0e9}},
+           "stages": {"down_s0": {"traffic_bytes": 1.0e9, "kernel": "mimi::gemm_planes_kernel<1, 3>"}}}
     p = tmp_path / "pmc.json"
     p.write_text(json.dumps(pmc))
     prof = {"res_s0": {"ms": 7.0, "flops": 1.4e12, "kernel": "mimi::resblock0_h16_kernel(mimi::ResArgs)",
@@ -141,5 +142,33 @@ def test_bench_north_star_groups(tmp_path):
     cs = g["conv_stack"]
     assert cs["stages"] == ["res_s0", "down_s0"] and cs["ms_per_step"] == 1.7
     assert cs["hbm_bytes_per_step"] == 3_000_000_000 and abs(cs["hbm_GBps"] - 3e9 / 1.7e-3 / 1e9) < 0.1
-    assert g["transformer"]["hbm_unmeasured_kernels"] == ["unknown"]
+    assert cs["hbm_measured_on_other_kernel"] == ["down_s0"]
+    assert g["transformer"]["hbm_unmeasured_stages"] == ["qkv"]
     assert "quantizer" not in g
+
+
+def test_stage_keyed_pmc_alignment(tmp_path):
+    """tools/summarize_profile.stage_bytes: counter rows after the spin marker walked against the launch sequence;
+    a stage's extra dispatches (RVQ levels, final) summed into it; bookkeeping kernels left out."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import summarize_profile as sp
+    seq = [["res_s0", "mimi::resblock0_h16_kernel"], ["down_s0", "mimi::gemm_planes_kernel<1, 2>"],
+           ["rvq", "mimi::rvq_level_h16_kernel<256, 4, 16>"]]
+    rows = [("void at::spin_kernel(long)", 9)]
+    for enc in range(2):
+        rows += [("mimi::resblock0_h16_kernel(mimi::ResArgs)", 10), ("void mimi::gemm_planes_kernel<1, 2>(mimi::GemmArgs)", 20),
+                 ("void mimi::rvq_level_h16_kernel<256, 4, 16>(mimi::RvqArgs, int)", 1),
+                 ("void mimi::rvq_level_h16_kernel<256, 4, 16>(mimi::RvqArgs, int)", 2),
+                 ("mimi::rvq_final_kernel(mimi::RvqArgs, int)", 3), ("mimi::amax_reduce_kernel(unsigned int*, int)", 99)]
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tmp_path / f"pmc_{counter}"
+        d.mkdir()
+        with open(d / "run_counter_collection.csv", "w") as f:
+            f.write("Dispatch_Id,Kernel_Name,Counter_Value\n")
+            for i, (k, v) in enumerate(rows):
+                f.write(f'{i},"{k}",{v}\n')
+    st = sp.stage_bytes(str(tmp_path), seq)
+    assert st["res_s0"]["write_bytes"] == 10 * 1024 and st["down_s0"]["fetch_bytes"] == 20 * 1024 * 2
+    assert st["rvq"]["write_bytes"] == 6 * 1024 and st["rvq"]["launches_WRITE_SIZE"] == 2
+    assert st["rvq"]["traffic_bytes"] == 6 * 1024 * 3

@@ -16,7 +16,7 @@
 //           pairs it forms ((L' , new), (new, sym R)) with L' = new when L is the partner of the previous
 //           occurrence -- the net of tokenizers' sequential change list
 //   relink  sym[p] = new, p -> R, q dead
-// and the best pair is a max over the table of (count << 34 | (MAXID - left) << 17 | (MAXID - right)).
+// and the best pair is the max count, then the smallest (left, right) among the pairs holding it (two sweeps).
 // HBM-bound integer work: one 4-B read per symbol per step for the mark scan, one table sweep for the max.
 #include <hip/hip_runtime.h>
 
@@ -98,18 +98,26 @@ __global__ void rehash_kernel(Table from, Table to) {
     }
 }
 
-// max over the table of count << 34 | (kMaxId - a) << 17 | (kMaxId - b)  (counts < 2^30, checked at create)
+// The best pair in two sweeps of the table, so counts are full int64 (no packing limit): best_count_kernel takes
+// the max count into best[0]; best_pair_kernel then takes, among the pairs holding that count, the max of
+// (kMaxId - a) << 17 | (kMaxId - b) = the smallest (a, b), into best[1] (the BpeTrainer order).
+template <bool PAIR>
 __global__ __launch_bounds__(256) void best_kernel(Table t, unsigned long long* best) {
     unsigned long long m = 0;
+    const unsigned long long want = PAIR ? best[0] : 0;
     for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i <= t.mask;
          i += (unsigned long long)gridDim.x * blockDim.x) {
         const unsigned long long k = t.keys[i];
         const long long v = (long long)t.vals[i];
         if (k != kEmpty && v > 0) {
-            const unsigned a = (unsigned)(k >> 32), b = (unsigned)k;
-            const unsigned long long packed =
-                ((unsigned long long)v << 34) | ((unsigned long long)(kMaxId - a) << kIdBits) | (kMaxId - b);
-            m = packed > m ? packed : m;
+            unsigned long long x;
+            if (PAIR) {
+                const unsigned a = (unsigned)(k >> 32), b = (unsigned)k;
+                x = (unsigned long long)v == want ? ((unsigned long long)(kMaxId - a) << kIdBits) | (kMaxId - b) : 0;
+            } else {
+                x = (unsigned long long)v;
+            }
+            m = x > m ? x : m;
         }
     }
 #pragma unroll
@@ -122,7 +130,7 @@ __global__ __launch_bounds__(256) void best_kernel(Table t, unsigned long long* 
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = red[w] > m ? red[w] : m;
-        if (m) atomicMax(best, m);
+        if (m) atomicMax(best + (PAIR ? 1 : 0), m);
     }
 }
 
@@ -229,7 +237,7 @@ struct mimi_bpe {
     unsigned* nstarts = nullptr;
     unsigned long long* best = nullptr;
     Table t{};
-    unsigned long long* host = nullptr;  // pinned: best, nkeys
+    unsigned long long* host = nullptr;  // pinned: best count, best pair, nkeys
     int grid = 1024;
 };
 
@@ -309,15 +317,14 @@ extern "C" int mimi_bpe_create(int device, const int32_t* symbols, int64_t n_sym
         return fail(MIMI_ERR_INVALID_ARGUMENT, "vocab_size %d must be in [%d, %u]", vocab_size, n_initial_tokens,
                     kMaxId);
     if (n_symbols >= (1ll << 31)) return fail(MIMI_ERR_UNSUPPORTED, "more than 2^31 symbols");
-    // host: links, per-symbol word counts, and the bound that keeps every pair count below 2^30
+    // host: links and per-symbol word counts (pair counts are int64 on the device: no corpus-size limit)
     std::vector<int> nxt(n_symbols), prv(n_symbols), wc(n_symbols);
-    long long total = 0;
     if (n_words > 0 && (word_offsets[0] != 0 || word_offsets[n_words] != n_symbols))
         return fail(MIMI_ERR_INVALID_ARGUMENT, "word offsets must run from 0 to n_symbols");
     for (int64_t w = 0; w < n_words; ++w) {
         const int64_t b0 = word_offsets[w], b1 = word_offsets[w + 1];
         if (b1 < b0) return fail(MIMI_ERR_INVALID_ARGUMENT, "word offsets must be non-decreasing");
-        if (word_counts[w] < 0 || word_counts[w] >= (1ll << 30))
+        if (word_counts[w] < 0 || word_counts[w] > 0x7fffffffll)
             return fail(MIMI_ERR_UNSUPPORTED, "word count %lld", (long long)word_counts[w]);
         for (int64_t p = b0; p < b1; ++p) {
             if (symbols[p] < 0 || symbols[p] >= n_initial_tokens)
@@ -326,8 +333,6 @@ extern "C" int mimi_bpe_create(int device, const int32_t* symbols, int64_t n_sym
             nxt[p] = p + 1 < b1 ? (int)(p + 1) : -1;
             wc[p] = (int)word_counts[w];
         }
-        if (b1 > b0) total += (long long)word_counts[w] * (b1 - b0 - 1);
-        if (total >= (1ll << 30)) return fail(MIMI_ERR_UNSUPPORTED, "corpus too large: pair counts reach 2^30");
     }
     std::unique_ptr<mimi_bpe> h(new mimi_bpe());
     mimi_bpe* H = h.get();
@@ -346,8 +351,8 @@ extern "C" int mimi_bpe_create(int device, const int32_t* symbols, int64_t n_sym
     BPE_TRY(hipMalloc(&H->flag, nb));
     BPE_TRY(hipMalloc(&H->len, (size_t)vocab_size * 4));
     BPE_TRY(hipMalloc(&H->nstarts, 4));
-    BPE_TRY(hipMalloc(&H->best, 8));
-    BPE_TRY(hipHostMalloc(&H->host, 16, hipHostMallocDefault));
+    BPE_TRY(hipMalloc(&H->best, 16));
+    BPE_TRY(hipHostMalloc(&H->host, 24, hipHostMallocDefault));
     if (n_symbols > 0) {
         BPE_TRY(hipMemcpy(H->sym, symbols, n_symbols * 4, hipMemcpyHostToDevice));
         BPE_TRY(hipMemcpy(H->nxt, nxt.data(), n_symbols * 4, hipMemcpyHostToDevice));
@@ -377,20 +382,22 @@ extern "C" int mimi_bpe_create(int device, const int32_t* symbols, int64_t n_sym
 extern "C" int mimi_bpe_best(mimi_bpe* h, int32_t* left, int32_t* right, int64_t* count) {
     if (!h || !left || !right || !count) return fail(MIMI_ERR_INVALID_ARGUMENT, "null argument");
     BPE_TRY(hipSetDevice(h->device));
-    BPE_TRY(hipMemsetAsync(h->best, 0, 8, h->s));
+    BPE_TRY(hipMemsetAsync(h->best, 0, 16, h->s));
     const unsigned long long slots = h->t.mask + 1;
     const unsigned grid = (unsigned)std::min<unsigned long long>((slots + 255) / 256, (unsigned long long)h->grid);
-    hipLaunchKernelGGL(best_kernel, dim3(grid), dim3(256), 0, h->s, h->t, h->best);
+    hipLaunchKernelGGL(best_kernel<false>, dim3(grid), dim3(256), 0, h->s, h->t, h->best);
     BPE_TRY(hipGetLastError());
-    BPE_TRY(hipMemcpyAsync(h->host, h->best, 8, hipMemcpyDeviceToHost, h->s));
-    BPE_TRY(hipMemcpyAsync(h->host + 1, h->t.nkeys, 8, hipMemcpyDeviceToHost, h->s));
+    hipLaunchKernelGGL(best_kernel<true>, dim3(grid), dim3(256), 0, h->s, h->t, h->best);
+    BPE_TRY(hipGetLastError());
+    BPE_TRY(hipMemcpyAsync(h->host, h->best, 16, hipMemcpyDeviceToHost, h->s));
+    BPE_TRY(hipMemcpyAsync(h->host + 2, h->t.nkeys, 8, hipMemcpyDeviceToHost, h->s));
     BPE_TRY(hipStreamSynchronize(h->s));
-    const unsigned long long m = h->host[0];
-    *count = (int64_t)(m >> 34);
-    *left = m ? (int32_t)(kMaxId - ((m >> kIdBits) & kMaxId)) : -1;
-    *right = m ? (int32_t)(kMaxId - (m & kMaxId)) : -1;
+    const unsigned long long c = h->host[0], m = h->host[1];
+    *count = (int64_t)c;
+    *left = c ? (int32_t)(kMaxId - ((m >> kIdBits) & kMaxId)) : -1;
+    *right = c ? (int32_t)(kMaxId - (m & kMaxId)) : -1;
     // keep the load factor under 1/2 (the merges' new pairs); a rehash also drops the merged (zero) pairs
-    if (2 * h->host[1] > slots) {
+    if (2 * h->host[2] > slots) {
         int rc = rehash(h, slots * 2);
         if (rc) return rc;
     }

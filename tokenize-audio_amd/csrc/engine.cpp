@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../include/mimi_hip.h"
+#include "host_io.h"
 #include "kernels.h"
 
 using namespace mimi;
@@ -264,7 +265,8 @@ struct mimi_engine {
     std::map<std::string, int> slot_of;
     std::vector<float> act_scale;
     bool calibrating = false;
-    bool uncalibrated_slot = false;  // an encode named a tensor the calibration did not see
+    bool calibrated = false;         // calibrate_scales has run (lazily, before the first f16x3 encode)
+    bool uncalibrated_slot = false;  // the current encode named a tensor the calibration did not see (reset per encode)
     unsigned* amax_dev = nullptr;   // [kMaxActSlots][AMAX_SLOT_WORDS] sub-slots, then [kMaxActSlots] reduced
     unsigned* amax_red = nullptr;
     unsigned* amax_host = nullptr;  // pinned
@@ -272,6 +274,7 @@ struct mimi_engine {
     // encodes enqueued by mimi_encode_async and not yet waited (see encode_async_locked)
     struct Pending {
         int64_t id = 0;  // ticket; 0 = free
+        bool claimed = false;  // a mimi_encode_wait is synchronising on it (outside the engine lock)
         hipEvent_t done = nullptr;
         unsigned* amax = nullptr;  // pinned [kMaxActSlots]: this encode's per-tensor maxima (f16x3)
         int nslots = 0;
@@ -293,6 +296,7 @@ struct mimi_engine {
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfStat> prof;
     std::vector<std::string> prof_order;
+    std::vector<std::string> last_seq;  // "stage|kernel" of the last profiled encode, in launch order
 
     // hipGraph replay of the f16x3 encode (see graph_encode): one captured graph per (batch, length, K), the
     // audio / codes pointers passed through io_dev
@@ -533,165 +537,24 @@ extern "C" int mimi_set_weight(mimi_engine* e, const char* name, const float* da
     return MIMI_OK;
 }
 
-// --- minimal safetensors reader (8-byte LE header length, JSON header, raw little-endian data) ---
-namespace {
-struct StEntry {
-    std::string dtype;
-    std::vector<int64_t> shape;
-    int64_t begin = 0, end = 0;
-};
-
-struct JsonCursor {
-    const std::string& s;
-    size_t i = 0;
-    explicit JsonCursor(const std::string& str) : s(str) {}
-    void ws() {
-        while (i < s.size() && (s[i] == ' ' || s[i] == '\n' || s[i] == '\t' || s[i] == '\r')) ++i;
-    }
-    bool eat(char c) {
-        ws();
-        if (i < s.size() && s[i] == c) {
-            ++i;
-            return true;
-        }
-        return false;
-    }
-    bool str(std::string& out) {
-        ws();
-        if (i >= s.size() || s[i] != '"') return false;
-        ++i;
-        out.clear();
-        while (i < s.size() && s[i] != '"') {
-            if (s[i] == '\\' && i + 1 < s.size()) ++i;
-            out.push_back(s[i++]);
-        }
-        if (i >= s.size()) return false;
-        ++i;
-        return true;
-    }
-    bool num(int64_t& v) {
-        ws();
-        size_t j = i;
-        if (j < s.size() && s[j] == '-') ++j;
-        while (j < s.size() && isdigit((unsigned char)s[j])) ++j;
-        if (j == i) return false;
-        v = std::stoll(s.substr(i, j - i));
-        i = j;
-        return true;
-    }
-    bool skip_value() {  // skip any JSON value (used for __metadata__)
-        ws();
-        if (i >= s.size()) return false;
-        if (s[i] == '"') {
-            std::string t;
-            return str(t);
-        }
-        if (s[i] == '{' || s[i] == '[') {
-            const char open = s[i], close = open == '{' ? '}' : ']';
-            int depth = 0;
-            bool in_str = false;
-            for (; i < s.size(); ++i) {
-                const char ch = s[i];
-                if (in_str) {
-                    if (ch == '\\') ++i;
-                    else if (ch == '"') in_str = false;
-                    continue;
-                }
-                if (ch == '"') in_str = true;
-                else if (ch == open) ++depth;
-                else if (ch == close && --depth == 0) {
-                    ++i;
-                    return true;
-                }
-            }
-            return false;
-        }
-        while (i < s.size() && s[i] != ',' && s[i] != '}' && s[i] != ']') ++i;
-        return true;
-    }
-    bool int_list(std::vector<int64_t>& v) {
-        v.clear();
-        if (!eat('[')) return false;
-        if (eat(']')) return true;
-        do {
-            int64_t x;
-            if (!num(x)) return false;
-            v.push_back(x);
-        } while (eat(','));
-        return eat(']');
-    }
-};
-
-bool parse_header(const std::string& hdr, std::map<std::string, StEntry>& out, std::string& err) {
-    JsonCursor c(hdr);
-    if (!c.eat('{')) return err = "header is not an object", false;
-    if (c.eat('}')) return true;
-    do {
-        std::string key;
-        if (!c.str(key) || !c.eat(':')) return err = "bad key", false;
-        if (key == "__metadata__") {
-            if (!c.skip_value()) return err = "bad metadata", false;
-            continue;
-        }
-        StEntry en;
-        if (!c.eat('{')) return err = "entry " + key + " is not an object", false;
-        if (!c.eat('}')) {
-            do {
-                std::string f;
-                if (!c.str(f) || !c.eat(':')) return err = "bad field in " + key, false;
-                if (f == "dtype") {
-                    if (!c.str(en.dtype)) return err = "bad dtype in " + key, false;
-                } else if (f == "shape") {
-                    if (!c.int_list(en.shape)) return err = "bad shape in " + key, false;
-                } else if (f == "data_offsets") {
-                    std::vector<int64_t> o;
-                    if (!c.int_list(o) || o.size() != 2) return err = "bad offsets in " + key, false;
-                    en.begin = o[0];
-                    en.end = o[1];
-                } else if (!c.skip_value()) {
-                    return err = "bad value in " + key, false;
-                }
-            } while (c.eat(','));
-            if (!c.eat('}')) return err = "unterminated entry " + key, false;
-        }
-        out[key] = en;
-    } while (c.eat(','));
-    return c.eat('}') ? true : (err = "unterminated header", false);
-}
-}  // namespace
-
+// Checkpoint files: safetensors.cpp (host-only, bounds-checked; built under ASan/UBSan by tools/asan).  A tensor
+// is read when the encode path needs it (the names build_expected lists, the quantizer's codebooks, weight-norm
+// factors of a conv); the decoder / upsample tensors of a full checkpoint are skipped unread.
 extern "C" int mimi_load_safetensors(mimi_engine* e, const char* path) {
     if (!e || !path) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null argument");
     if (e->finalized) return set_err(MIMI_ERR_STATE, "weights are frozen after mimi_finalize");
-    std::ifstream f(path, std::ios::binary);
-    if (!f) return set_err(MIMI_ERR_IO, "cannot open %s", path);
-    uint64_t hlen = 0;
-    f.read(reinterpret_cast<char*>(&hlen), 8);
-    if (!f || hlen == 0 || hlen > (1ull << 30)) return set_err(MIMI_ERR_IO, "%s: bad safetensors header", path);
-    std::string hdr(hlen, '\0');
-    f.read(&hdr[0], (std::streamsize)hlen);
-    if (!f) return set_err(MIMI_ERR_IO, "%s: truncated header", path);
-    std::map<std::string, StEntry> entries;
-    std::string perr;
-    if (!parse_header(hdr, entries, perr)) return set_err(MIMI_ERR_IO, "%s: %s", path, perr.c_str());
-    const int64_t data0 = 8 + (int64_t)hlen;
     std::lock_guard<std::mutex> lk(e->mu);
-    for (const auto& kv : entries) {
-        const std::string& name = kv.first;
-        const StEntry& en = kv.second;
-        const bool wanted = e->expected.count(name) || name.rfind("quantizer.", 0) == 0 ||
-                            name.find("weight_g") != std::string::npos || name.find("original0") != std::string::npos;
-        if (!wanted || name.rfind("decoder", 0) == 0) continue;
-        if (en.dtype != "F32") return set_err(MIMI_ERR_WEIGHTS, "%s: dtype %s (F32 required)", name.c_str(), en.dtype.c_str());
-        int64_t numel = 1;
-        for (int64_t d : en.shape) numel *= d;
-        if (en.end - en.begin != numel * 4) return set_err(MIMI_ERR_IO, "%s: size mismatch", name.c_str());
-        std::vector<float> buf(numel);
-        f.seekg(data0 + en.begin);
-        f.read(reinterpret_cast<char*>(buf.data()), numel * 4);
-        if (!f) return set_err(MIMI_ERR_IO, "%s: truncated data for %s", path, name.c_str());
-        e->host_w[name] = std::move(buf);
-    }
+    auto wanted = [&](const std::string& name) {
+        if (name.rfind("decoder", 0) == 0 || name.rfind("upsample", 0) == 0) return false;
+        return e->expected.count(name) > 0 || name.rfind("quantizer.", 0) == 0 ||
+               name.find("weight_g") != std::string::npos || name.find("weight_v") != std::string::npos ||
+               name.find("original0") != std::string::npos || name.find("original1") != std::string::npos;
+    };
+    std::map<std::string, std::vector<float>> got;
+    std::string err;
+    const int rc = st_load(path, wanted, got, err);
+    if (rc) return set_err(rc, "%s", err.c_str());
+    for (auto& kv : got) e->host_w[kv.first] = std::move(kv.second);
     return MIMI_OK;
 }
 
@@ -1027,8 +890,7 @@ extern "C" int mimi_finalize(mimi_engine* e) {
     }
     e->levels_available = L;
     e->host_w.clear();
-    if ((rc = calibrate_scales(e))) return rc;
-    e->finalized = true;
+    e->finalized = true;  // (the f16x3 activation scales are calibrated before the first f16x3 encode)
     return MIMI_OK;
 }
 
@@ -1288,9 +1150,9 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     r.codes = codes;
     r.codes_ref = e->capturing ? reinterpret_cast<int32_t* const*>(e->io_dev + 1) : nullptr;
     r.frames_per_item = frames_per_item;
-    LAUNCH_TRY(launch_rvq(r, s), "rvq");
-    rec.mark("rvq", 2.0 * frames * r.D * r.ncodes * K, (double)frames * (2 * r.D) * 4 + (double)frames * K * 4,
-             e->cb_h16 ? "mimi::rvq_level_h16_kernel<256>" : "mimi::rvq_level_kernel<256>");
+    const char* kname = "?";
+    LAUNCH_TRY(launch_rvq(r, s, &kname), "rvq");
+    rec.mark("rvq", 2.0 * frames * r.D * r.ncodes * K, (double)frames * (2 * r.D) * 4 + (double)frames * K * 4, kname);
     return MIMI_OK;
 }
 
@@ -1654,9 +1516,13 @@ static int f16_pass(mimi_engine* e, const float* audio, int B, int64_t L, int K,
     *overflow = false;
     HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));  // encodes enqueued on other streams use amax_dev too
     HIP_TRY(hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), s));
+    e->uncalibrated_slot = false;
     int rc = encode_pass(e, audio, B, L, K, codes, s, PREC_F16X3);
     if (rc) return rc;
-    if (e->uncalibrated_slot) return set_err(MIMI_ERR_STATE, "f16x3: an activation has no calibrated scale");
+    if (e->uncalibrated_slot) {
+        e->uncalibrated_slot = false;
+        return set_err(MIMI_ERR_STATE, "f16x3: an activation has no calibrated scale");
+    }
     int n = 0;
     if ((rc = read_amax(e, s, &n))) return rc;
     for (int i = 0; i < n; ++i) {
@@ -1728,6 +1594,8 @@ static int calibrate_scales(mimi_engine* e) {
         if (!changed) break;
     }
     e->calibrating = false;
+    e->uncalibrated_slot = false;
+    if (rc == MIMI_OK) e->calibrated = true;
     (void)hipStreamSynchronize(s);
     if (d_audio) (void)hipFree(d_audio);
     if (d_codes) (void)hipFree(d_codes);
@@ -1806,6 +1674,7 @@ static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int
         return nullptr;
     }
     e->capturing = true;
+    e->uncalibrated_slot = false;
     int rc = MIMI_OK;
     // (no maxima reset node: amax_reduce_kernel leaves every sub-slot at 0 as it reads it, so a replay starts
     // from the zeros the previous encode's fold left behind)
@@ -1817,6 +1686,7 @@ static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int
     hipGraphExec_t x = nullptr;
     if (rc || ec != hipSuccess || !g || e->uncalibrated_slot || hipGraphInstantiate(&x, g, nullptr, nullptr, 0) != hipSuccess) {
         (void)hipGetLastError();
+        e->uncalibrated_slot = false;
         if (g) (void)hipGraphDestroy(g);
         return nullptr;
     }
@@ -1897,6 +1767,7 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
     const bool h16 = prec == PREC_F16X3 && act_planes(e, plan_lengths(e->cfg, L), prec) == 2;
     int rc;
     int n = 0;
+    if (h16 && !e->calibrated && (rc = calibrate_scales(e))) return rc;
     if (h16) {
         bool replayed = false;
         if ((rc = graph_encode(e, audio, B, L, K, codes, s, &replayed))) return rc;
@@ -1904,8 +1775,12 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
         if (!replayed) {
             HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));  // the maxima buffers are part of the workspace
             HIP_TRY(hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), s));
+            e->uncalibrated_slot = false;
             if ((rc = encode_pass(e, audio, B, L, K, codes, s, PREC_F16X3))) return rc;
-            if (e->uncalibrated_slot) return set_err(MIMI_ERR_STATE, "f16x3: an activation has no calibrated scale");
+            if (e->uncalibrated_slot) {  // this encode only: the next one starts clean
+                e->uncalibrated_slot = false;
+                return set_err(MIMI_ERR_STATE, "f16x3: an activation has no calibrated scale");
+            }
             LAUNCH_TRY(launch_amax_reduce(e->amax_dev, n, e->amax_red, s), "amax_reduce");
         }
         HIP_TRY(hipMemcpyAsync(P->amax, e->amax_red, n * sizeof(unsigned), hipMemcpyDeviceToHost, s));
@@ -1922,28 +1797,51 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
     P->K = K;
     P->codes = codes;
     P->s = s;
+    P->claimed = false;
     P->id = e->next_ticket++;
     *ticket = P->id;
     return MIMI_OK;
 }
 
-static int encode_wait_locked(mimi_engine* e, int64_t ticket) {
-    mimi_engine::Pending* P = nullptr;
-    for (auto& q : e->pend)
-        if (ticket > 0 && q.id == ticket) P = &q;
-    if (!P) return set_err(MIMI_ERR_INVALID_ARGUMENT, "ticket %lld is not an encode in flight", (long long)ticket);
-    const mimi_engine::Pending q = *P;
-    P->id = 0;
-    HIP_TRY(hipEventSynchronize(q.done));
-    bool ovf = false;
-    if (q.h16) e->last_amax.assign(q.nslots, 0.0f);
-    for (int i = 0; q.h16 && i < q.nslots; ++i) {
-        float a;
-        std::memcpy(&a, &q.amax[i], 4);
-        e->last_amax[i] = a;
-        if (std::isfinite(a) && a * e->act_scale[i] >= kF16Overflow) ovf = true;
+// Waits for ticket's encode and runs its f16x3 overflow check.  The engine lock is NOT held while the host
+// synchronises on the encode's event (other threads keep enqueueing on the engine meanwhile): the slot is claimed
+// under the lock -- so it is neither reused nor waited twice -- and released, with the overflow check and any
+// fallback, under the lock again.
+static int encode_wait(mimi_engine* e, int64_t ticket) {
+    mimi_engine::Pending q;
+    {
+        std::lock_guard<std::mutex> lk(e->mu);
+        mimi_engine::Pending* P = nullptr;
+        for (auto& x : e->pend)
+            if (ticket > 0 && x.id == ticket && !x.claimed) P = &x;
+        if (!P) return set_err(MIMI_ERR_INVALID_ARGUMENT, "ticket %lld is not an encode in flight", (long long)ticket);
+        P->claimed = true;
+        q = *P;
     }
-    return ovf ? overflow_fallback(e, q.audio, q.B, q.L, q.K, q.codes, q.s) : MIMI_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    const hipError_t se = hipEventSynchronize(q.done);
+    std::lock_guard<std::mutex> lk(e->mu);
+    mimi_engine::Pending* P = nullptr;
+    for (auto& x : e->pend)
+        if (x.id == ticket) P = &x;
+    bool ovf = false;
+    if (q.h16 && se == hipSuccess) {
+        e->last_amax.assign(q.nslots, 0.0f);
+        for (int i = 0; i < q.nslots; ++i) {
+            float a;
+            std::memcpy(&a, &P->amax[i], 4);
+            e->last_amax[i] = a;
+            if (std::isfinite(a) && a * e->act_scale[i] >= kF16Overflow) ovf = true;
+        }
+    }
+    P->claimed = false;
+    P->id = 0;
+    if (se != hipSuccess)
+        return set_err(se == hipErrorOutOfMemory ? MIMI_ERR_OUT_OF_MEMORY : MIMI_ERR_HIP, "hipEventSynchronize: %s",
+                       hipGetErrorString(se));
+    if (!ovf) return MIMI_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    return overflow_fallback(e, q.audio, q.B, q.L, q.K, q.codes, q.s);
 }
 
 static int check_encode_args(mimi_engine* e, const float* audio, int32_t batch, int64_t length, int32_t* K,
@@ -1980,23 +1878,24 @@ extern "C" int mimi_encode_async(mimi_engine* e, const float* audio, int32_t bat
 
 extern "C" int mimi_encode_wait(mimi_engine* e, int64_t ticket) {
     if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
-    std::lock_guard<std::mutex> lk(e->mu);
-    HIP_TRY(hipSetDevice(e->device));
-    return encode_wait_locked(e, ticket);
+    return encode_wait(e, ticket);
 }
 
 extern "C" int mimi_encode(mimi_engine* e, const float* audio, int32_t batch, int64_t length, int32_t K,
                            int32_t* codes, void* stream) {
     int rc = check_encode_args(e, audio, batch, length, &K, codes);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(e->mu);
-    HIP_TRY(hipSetDevice(e->device));
-    (void)hipGetLastError();  // a failure left by an unrelated earlier call must not fail this encode's launches
     int64_t ticket = 0;
-    // NULL stream = the HIP null stream, as in every HIP API
-    if ((rc = encode_async_locked(e, audio, batch, length, K, codes, reinterpret_cast<hipStream_t>(stream), &ticket)))
-        return rc;
-    return encode_wait_locked(e, ticket);
+    {
+        std::lock_guard<std::mutex> lk(e->mu);
+        HIP_TRY(hipSetDevice(e->device));
+        (void)hipGetLastError();  // a failure left by an unrelated earlier call must not fail this encode's launches
+        // NULL stream = the HIP null stream, as in every HIP API
+        if ((rc = encode_async_locked(e, audio, batch, length, K, codes, reinterpret_cast<hipStream_t>(stream),
+                                      &ticket)))
+            return rc;
+    }
+    return encode_wait(e, ticket);
 }
 
 extern "C" int mimi_rvq_encode(mimi_engine* e, const float* emb, int64_t frames, int32_t K, int32_t* codes,
@@ -2102,6 +2001,16 @@ extern "C" int mimi_act_scales(mimi_engine* e, int32_t max_n, char* names, float
 
 extern "C" int mimi_get_precision(const mimi_engine* e) { return e ? e->precision : -1; }
 
+extern "C" int mimi_calibrate(mimi_engine* e) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    if (!e->finalized) return set_err(MIMI_ERR_STATE, "mimi_finalize has not been called");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (e->calibrated) return MIMI_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    (void)hipGetLastError();
+    return calibrate_scales(e);
+}
+
 extern "C" int64_t mimi_f16_reruns(const mimi_engine* e) { return e ? e->f16_reruns : -1; }
 
 extern "C" int mimi_set_profiling(mimi_engine* e, int enable) {
@@ -2114,12 +2023,16 @@ extern "C" int mimi_set_profiling(mimi_engine* e, int enable) {
 static int resolve_pending(mimi_engine* e) {
     HIP_TRY(hipSetDevice(e->device));
     hipEvent_t prev = nullptr;
+    std::vector<std::string> seq;
     for (auto& pe : e->pending) {
         HIP_TRY(hipEventSynchronize(pe.ev));
         if (pe.name.empty()) {
             prev = pe.ev;
+            if (!seq.empty()) e->last_seq = std::move(seq);
+            seq.clear();
             continue;
         }
+        seq.push_back(pe.name);
         float ms = 0;
         if (prev) HIP_TRY(hipEventElapsedTime(&ms, prev, pe.ev));
         if (!e->prof.count(pe.name)) e->prof_order.push_back(pe.name);
@@ -2130,8 +2043,27 @@ static int resolve_pending(mimi_engine* e) {
         st.launches += 1;
         prev = pe.ev;
     }
+    if (!seq.empty()) e->last_seq = std::move(seq);
     for (auto& pe : e->pending) e->event_pool.push_back(pe.ev);
     e->pending.clear();
+    return MIMI_OK;
+}
+
+extern "C" int mimi_profile_sequence(mimi_engine* e, int32_t max_stages, char* names, int32_t* n_stages) {
+    if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    int rc = resolve_pending(e);
+    if (rc) return rc;
+    int i = 0;
+    for (const auto& n : e->last_seq) {
+        if (i >= max_stages) break;
+        if (names) {
+            std::strncpy(names + 128 * i, n.c_str(), 127);
+            names[128 * i + 127] = 0;
+        }
+        ++i;
+    }
+    if (n_stages) *n_stages = i;
     return MIMI_OK;
 }
 

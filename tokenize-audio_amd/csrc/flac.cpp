@@ -233,14 +233,16 @@ bool read_residual(BitReader& br, int bs, int order, int64_t* out) {
     return true;
 }
 
-// s[i] += (sum_j coef[j] s[i-1-j]) >> shift, coefficient j applying to the sample j + 1 back
+// s[i] += (sum_j coef[j] s[i-1-j]) >> shift, coefficient j applying to the sample j + 1 back.  The products and
+// sums wrap in uint64 (two's complement, the same bits as int64 wherever a valid stream keeps them in range, and
+// defined behaviour on a corrupt one, whose garbage the frame CRC-16 then rejects; tools/asan runs this under UBSan)
 template <int ORDER>
 void lpc_restore(int64_t* s, int bs, const int64_t* coef, int shift) {
     for (int i = ORDER; i < bs; ++i) {
-        int64_t sum = 0;
+        uint64_t sum = 0;
 #pragma unroll
-        for (int j = 0; j < ORDER; ++j) sum += coef[j] * s[i - 1 - j];
-        s[i] += sum >> shift;
+        for (int j = 0; j < ORDER; ++j) sum += (uint64_t)coef[j] * (uint64_t)s[i - 1 - j];
+        s[i] = (int64_t)((uint64_t)s[i] + (uint64_t)((int64_t)sum >> shift));
     }
 }
 
@@ -272,15 +274,17 @@ bool read_subframe(BitReader& br, int bs, int bps, int64_t* s) {
         for (int i = 0; i < order; ++i) s[i] = br.sbits(b);
         if (!read_residual(br, bs, order, s)) return false;
         for (int i = order; i < bs; ++i) {
-            int64_t pred = 0;
+            uint64_t pred = 0;  // (wrapping: see lpc_restore)
+            const uint64_t a = (uint64_t)s[i - 1 < 0 ? 0 : i - 1], b2 = order >= 2 ? (uint64_t)s[i - 2] : 0,
+                           c = order >= 3 ? (uint64_t)s[i - 3] : 0, d = order >= 4 ? (uint64_t)s[i - 4] : 0;
             switch (order) {
-                case 1: pred = s[i - 1]; break;
-                case 2: pred = 2 * s[i - 1] - s[i - 2]; break;
-                case 3: pred = 3 * s[i - 1] - 3 * s[i - 2] + s[i - 3]; break;
-                case 4: pred = 4 * s[i - 1] - 6 * s[i - 2] + 4 * s[i - 3] - s[i - 4]; break;
+                case 1: pred = a; break;
+                case 2: pred = 2 * a - b2; break;
+                case 3: pred = 3 * a - 3 * b2 + c; break;
+                case 4: pred = 4 * a - 6 * b2 + 4 * c - d; break;
                 default: break;
             }
-            s[i] += pred;
+            s[i] = (int64_t)((uint64_t)s[i] + pred);
         }
     } else if (type >= 32) {  // LPC, order 1..32
         const int order = type - 31;

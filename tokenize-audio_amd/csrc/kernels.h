@@ -286,7 +286,7 @@ struct RvqArgs {
     int sem_split;          // (set by launch_rvq) semantic + first acoustic level in one launch
 };
 size_t rvq_work_bytes(long long frames);
-hipError_t launch_rvq(const RvqArgs& a, hipStream_t s);
+hipError_t launch_rvq(const RvqArgs& a, hipStream_t s, const char** kname = nullptr);  // kname: the level kernel's symbol
 
 // polyphase resampler (resample.hip): clips packed at in_off / out_off (device int64 arrays), one launch
 hipError_t launch_resample_poly(const float* x, const long long* in_off, const long long* in_len, int nclips,

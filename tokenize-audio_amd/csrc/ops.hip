@@ -862,50 +862,60 @@ hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int 
 
 // one workgroup per (item, edge, 64 output channels): thread (slice sl of 16, group g of 4 consecutive
 // channels) sums its C/16 terms with 16-B weight loads all in flight at once; the slices are added in a fixed
-// order, then the row and its planes are updated
+// order, then the row and its planes are updated.  T = 1 (F = 1, clips of <= 960 samples): both replicate terms
+// land on the one output row, so the edge-0 workgroup adds them both, left edge first (the edge-1 workgroup
+// exits) -- two workgroups updating one row would race and lose a term.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void ds_edge_fix_kernel(const float* __restrict__ x, const float* __restrict__ wfix,
                                                           float* __restrict__ out, void* __restrict__ outp,
                                                           long long pstride, float oscale, unsigned* __restrict__ oamax,
                                                           int T, int F, int C, int N) {
     const int b = blockIdx.x, edge = blockIdx.y;
-    if (edge == 1 && (T & 1) == 0) return;  // no right extra row
-    const int t = edge == 0 ? 0 : T - 1, f = edge == 0 ? 0 : F - 1;
+    const bool right = (T & 1) != 0;                 // a right "extra" row exists
+    if (edge == 1 && (!right || F == 1)) return;
+    const int last_edge = edge == 0 && right && F == 1 ? 1 : edge;
+    const int f = edge == 0 ? 0 : F - 1;
     const int g = threadIdx.x & 15, sl = threadIdx.x >> 4;
     const int n0 = blockIdx.z * 64;
     const int cs = C / 16, c0 = sl * cs;
-    const float* __restrict__ wc = wfix + (long long)edge * C * N + n0 + 4 * g;  // [edge][c][n]
-    const float* __restrict__ xr = x + ((long long)b * T + t) * C;
-    f32x4 a = {0.f, 0.f, 0.f, 0.f};
-    // 16 channels per round: all 20 loads issued before the first FMA (a plain loop let the compiler wait out
-    // each load's latency in turn: 13.8 us per launch at any batch); same FMA order as the plain loop
-    for (int c = c0; c < c0 + cs; c += 16) {
-        f32x4 w[16], xv[4];
+    __shared__ float part[16][64];
+    const long long o = ((long long)b * F + f) * N + n0 + (threadIdx.x & 63);
+    float v = threadIdx.x < 64 ? out[o] : 0.0f;
+    for (int e = edge; e <= last_edge; ++e) {
+        const int t = e == 0 ? 0 : T - 1;
+        const float* __restrict__ wc = wfix + (long long)e * C * N + n0 + 4 * g;  // [edge][c][n]
+        const float* __restrict__ xr = x + ((long long)b * T + t) * C;
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        // 16 channels per round: all 20 loads issued before the first FMA (a plain loop let the compiler wait out
+        // each load's latency in turn: 13.8 us per launch at any batch); same FMA order as the plain loop
+        for (int c = c0; c < c0 + cs; c += 16) {
+            f32x4 w[16], xv[4];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = *reinterpret_cast<const f32x4*>(wc + (long long)(c + i) * N);
+            for (int i = 0; i < 16; ++i) w[i] = *reinterpret_cast<const f32x4*>(wc + (long long)(c + i) * N);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) xv[i] = *reinterpret_cast<const f32x4*>(xr + c + 4 * i);
+            for (int i = 0; i < 4; ++i) xv[i] = *reinterpret_cast<const f32x4*>(xr + c + 4 * i);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float x1 = xv[i >> 2][i & 3];
-            a.x = __builtin_fmaf(w[i].x, x1, a.x);
-            a.y = __builtin_fmaf(w[i].y, x1, a.y);
-            a.z = __builtin_fmaf(w[i].z, x1, a.z);
-            a.w = __builtin_fmaf(w[i].w, x1, a.w);
+            for (int i = 0; i < 16; ++i) {
+                const float x1 = xv[i >> 2][i & 3];
+                a.x = __builtin_fmaf(w[i].x, x1, a.x);
+                a.y = __builtin_fmaf(w[i].y, x1, a.y);
+                a.z = __builtin_fmaf(w[i].z, x1, a.z);
+                a.w = __builtin_fmaf(w[i].w, x1, a.w);
+            }
+        }
+        if (e != edge) __syncthreads();  // wave 0 has read the previous edge's partials
+        part[sl][4 * g] = a.x;
+        part[sl][4 * g + 1] = a.y;
+        part[sl][4 * g + 2] = a.z;
+        part[sl][4 * g + 3] = a.w;
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            float sum = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) sum += part[q][threadIdx.x];
+            v = v + sum;
         }
     }
-    __shared__ float part[16][64];
-    part[sl][4 * g] = a.x;
-    part[sl][4 * g + 1] = a.y;
-    part[sl][4 * g + 2] = a.z;
-    part[sl][4 * g + 3] = a.w;
-    __syncthreads();
     if (threadIdx.x >= 64) return;  // (wave-uniform: wave 0 finishes)
-    const int lane = threadIdx.x;
-    float sum = 0.0f;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) sum += part[q][lane];
-    const long long o = ((long long)b * F + f) * N + n0 + lane;
-    const float v = out[o] + sum;
     out[o] = v;
     float mx = 0.0f;
     if (outp) store_act(nullptr, outp, pstride, 2, o, v, oscale, &mx);
@@ -1473,7 +1483,9 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
     }
 }
 
-hipError_t launch_rvq(const RvqArgs& args, hipStream_t s) {
+hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
+    const char* kn_dummy = nullptr;
+    if (!kname) kname = &kn_dummy;
     if (args.D != 256 || args.ncodes != 2048 || !args.work) return hipErrorInvalidValue;
     RvqArgs a = args;
     a.sem_split = (a.nsem == 1 && a.levels > 1 && a.cb_h16 && a.cb_unscale && a.cb_emax) ? 1 : 0;
@@ -1486,6 +1498,7 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s) {
         const dim3 grid((unsigned)((a.frames + 31) / 32), 2048 / RVQ_CS);
         const bool small = grid.x * grid.y < 256;
         const bool split = a.sem_split != 0;  // levels 0 and 1 in one launch (rvq_sem_split)
+        *kname = small ? "mimi::rvq_level_h16_kernel<256, 16, 32>" : "mimi::rvq_level_h16_kernel<256, 4, 16>";
         for (int L = 0; L < a.levels; L += (split && L == 0) ? 2 : 1) {
             const dim3 g(grid.x, grid.y, (split && L == 0) ? 2 : 1);
             if (small)
@@ -1501,6 +1514,7 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s) {
     // small batches (fewer 64-frame workgroups than CUs, B < 16 x 10 s): 32-frame tiles
     const bool small = (a.frames + RVQ_FT - 1) / RVQ_FT * (2048 / RVQ_CS) < 256;
     const int ft = small ? 32 : RVQ_FT;
+    *kname = small ? "mimi::rvq_level_kernel<256, 32>" : "mimi::rvq_level_kernel<256, 64>";
     const dim3 grid((unsigned)((a.frames + ft - 1) / ft), 2048 / RVQ_CS);
     for (int L = 0; L < a.levels; ++L) {
         if (small)

@@ -24,10 +24,10 @@ STATUS_NAMES = {
 # every symbol include/mimi_hip.h declares (tests check the library exports exactly these)
 EXPORTED_SYMBOLS = (
     "mimi_config_default", "mimi_create", "mimi_set_weight", "mimi_load_safetensors", "mimi_finalize",
-    "mimi_encode", "mimi_encode_async", "mimi_encode_wait", "mimi_rvq_encode", "mimi_set_precision", "mimi_get_precision", "mimi_f16_reruns", "mimi_set_graphs", "mimi_graph_replays", "mimi_act_scales", "mimi_encoded_length",
+    "mimi_encode", "mimi_encode_async", "mimi_encode_wait", "mimi_rvq_encode", "mimi_set_precision", "mimi_get_precision", "mimi_calibrate", "mimi_f16_reruns", "mimi_set_graphs", "mimi_graph_replays", "mimi_act_scales", "mimi_encoded_length",
     "mimi_encoded_length_cfg",
     "mimi_workspace_bytes", "mimi_destroy", "mimi_last_error", "mimi_set_profiling", "mimi_profile_read",
-    "mimi_profile_reset", "mimi_set_taps", "mimi_get_tap", "mimi_resample_poly",
+    "mimi_profile_reset", "mimi_profile_sequence", "mimi_set_taps", "mimi_get_tap", "mimi_resample_poly",
     "mimi_bpe_create", "mimi_bpe_best", "mimi_bpe_merge", "mimi_bpe_destroy", "mimi_flac_info", "mimi_flac_decode",
 )
 RESAMPLE_MAX_TAPS = 8192  # MIMI_RESAMPLE_MAX_TAPS
@@ -86,6 +86,7 @@ def _declare(lib):
         "mimi_rvq_encode": (c.c_int, [vp, vp, c.c_int64, c.c_int32, vp, vp]),
         "mimi_set_precision": (c.c_int, [vp, c.c_int32]),
         "mimi_get_precision": (c.c_int, [vp]),
+        "mimi_calibrate": (c.c_int, [vp]),
         "mimi_f16_reruns": (c.c_int64, [vp]),
         "mimi_set_graphs": (c.c_int, [vp, c.c_int32]),
         "mimi_graph_replays": (c.c_int64, [vp]),
@@ -100,6 +101,7 @@ def _declare(lib):
         "mimi_profile_read": (c.c_int, [vp, c.c_int32, c.c_char_p, c.POINTER(c.c_double), c.POINTER(c.c_int64),
                                         c.POINTER(c.c_double), c.POINTER(c.c_int32)]),
         "mimi_profile_reset": (c.c_int, [vp]),
+        "mimi_profile_sequence": (c.c_int, [vp, c.c_int32, c.c_char_p, c.POINTER(c.c_int32)]),
         "mimi_set_taps": (c.c_int, [vp, c.c_int]),
         "mimi_get_tap": (c.c_int, [vp, c.c_char_p, vp, c.c_int64, c.POINTER(c.c_int64), c.POINTER(c.c_int64)]),
         "mimi_bpe_create": (c.c_int, [c.c_int, vp, c.c_int64, vp, vp, c.c_int64, c.c_int32, c.c_int32, c.c_int32,

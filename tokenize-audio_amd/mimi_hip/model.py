@@ -62,7 +62,11 @@ def _resolve_device(device) -> torch.device:
 
 
 def resolve_checkpoint(name_or_path: str) -> str:
-    """Map ``"kyutai/mimi"`` (a Hub name; no network here) or a local directory/file to a local path."""
+    """Map ``"kyutai/mimi"`` (a Hub name; no network here) or a local directory/file to a local path.
+
+    Order: an existing path; ``$MIMI_HIP_CHECKPOINT``; the huggingface_hub cache (``$HF_HUB_CACHE``, else
+    ``$HF_HOME/hub``, else ``~/.cache/huggingface/hub``), ``models--<org>--<name>/snapshots/<rev>`` with ``<rev>``
+    from ``refs/main`` when present (the snapshot ``from_pretrained`` would load offline), else the newest."""
     if os.path.exists(name_or_path):
         return name_or_path
     env = os.environ.get("MIMI_HIP_CHECKPOINT")
@@ -70,7 +74,14 @@ def resolve_checkpoint(name_or_path: str) -> str:
         return env
     hub = os.environ.get("HF_HUB_CACHE") or os.path.join(
         os.environ.get("HF_HOME", os.path.expanduser("~/.cache/huggingface")), "hub")
-    snaps = sorted(glob.glob(os.path.join(hub, "models--" + name_or_path.replace("/", "--"), "snapshots", "*")))
+    repo = os.path.join(hub, "models--" + name_or_path.replace("/", "--"))
+    ref = os.path.join(repo, "refs", "main")
+    if os.path.exists(ref):
+        with open(ref) as f:
+            snap = os.path.join(repo, "snapshots", f.read().strip())
+        if os.path.isdir(snap):
+            return snap
+    snaps = sorted(glob.glob(os.path.join(repo, "snapshots", "*")), key=os.path.getmtime)
     if snaps:
         return snaps[-1]
     raise FileNotFoundError(
@@ -184,12 +195,10 @@ class MimiHipModel:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def encode(self, input_values: torch.Tensor, padding_mask: Optional[torch.Tensor] = None,
-               num_quantizers: Optional[int] = None, encoder_past_key_values=None, padding_cache=None,
-               use_streaming: Optional[bool] = None, return_dict: Optional[bool] = None):
-        if use_streaming:
-            raise NotImplementedError("streaming encode (padding cache / KV cache) is not on the batch path")
-        K = self.config.num_quantizers if num_quantizers is None else int(num_quantizers)
+    def _check_k(self, K: int) -> int:
+        """The reference's num_quantizers checks (TF/modeling_mimi.py:1335-1340); the C side would replace
+        K <= 0 by config.num_quantizers, so a caller's 0 must not reach it with an output sized for 0 levels."""
+        K = int(K)
         if K > self.config.num_quantizers:
             raise ValueError(
                 f"The number of quantizers (i.e codebooks) asked should be lower than the total number of "
@@ -198,6 +207,28 @@ class MimiHipModel:
             raise ValueError(
                 f"The number of quantizers (i.e codebooks) asked should be higher than the number of semantic "
                 f"quantizers {self.config.num_semantic_quantizers}, but is currently {K}.")
+        return K
+
+    def _device_audio(self, audio: torch.Tensor) -> torch.Tensor:
+        """device f32 [B, L], contiguous (the C ABI reads audio.data_ptr() as such)."""
+        if audio.dim() != 2:
+            raise ValueError(f"audio must be [batch, length], got {tuple(audio.shape)}")
+        return audio.to(device=self.device, dtype=torch.float32).contiguous()
+
+    def _out(self, B: int, K: int, T: int, out: Optional[torch.Tensor]) -> torch.Tensor:
+        if out is None:
+            return torch.empty((B, K, T), dtype=torch.int32, device=self.device)
+        if (tuple(out.shape) != (B, K, T) or out.dtype != torch.int32 or out.device != self.device
+                or not out.is_contiguous()):
+            raise ValueError(f"out must be a contiguous int32 [{B}, {K}, {T}] tensor on {self.device}")
+        return out
+
+    def encode(self, input_values: torch.Tensor, padding_mask: Optional[torch.Tensor] = None,
+               num_quantizers: Optional[int] = None, encoder_past_key_values=None, padding_cache=None,
+               use_streaming: Optional[bool] = None, return_dict: Optional[bool] = None):
+        if use_streaming:
+            raise NotImplementedError("streaming encode (padding cache / KV cache) is not on the batch path")
+        K = self._check_k(self.config.num_quantizers if num_quantizers is None else num_quantizers)
         if not torch.is_tensor(input_values):
             input_values = torch.as_tensor(np.asarray(input_values))
         if input_values.dim() != 3:
@@ -212,9 +243,10 @@ class MimiHipModel:
         if B == 0 or L == 0:
             return MimiEncoderOutput(codes.long())
         x = input_values.to(device=self.device, dtype=torch.float32).reshape(B, L).contiguous()
-        with self._lock:
-            _lib.check(self._lib.mimi_encode(self._h, ctypes.c_void_p(x.data_ptr()), B, L, K,
-                                             ctypes.c_void_p(codes.data_ptr()), self._stream()))
+        # (no Python lock: the engine serialises enqueues itself and waits outside its lock, so threads sharing
+        # one engine overlap -- the YODAS2 thread pool, yodas2-mimi/process_shard.py:691-717)
+        _lib.check(self._lib.mimi_encode(self._h, ctypes.c_void_p(x.data_ptr()), B, L, K,
+                                         ctypes.c_void_p(codes.data_ptr()), self._stream()))
         out = codes.long()
         if return_dict is False:
             return (out, None, None)
@@ -223,13 +255,12 @@ class MimiHipModel:
     def encode_int32(self, audio: torch.Tensor, num_quantizers: int, out: Optional[torch.Tensor] = None
                      ) -> torch.Tensor:
         """Lean path for the bench / shard driver: device f32 [B, L] in, device int32 [B, K, T] out."""
+        K = self._check_k(num_quantizers)
+        audio = self._device_audio(audio)
         B, L = audio.shape
-        T = encoded_length(L, self.config)
-        if out is None:
-            out = torch.empty((B, num_quantizers, T), dtype=torch.int32, device=self.device)
-        with self._lock:
-            _lib.check(self._lib.mimi_encode(self._h, ctypes.c_void_p(audio.data_ptr()), B, L, num_quantizers,
-                                             ctypes.c_void_p(out.data_ptr()), self._stream()))
+        out = self._out(B, K, encoded_length(L, self.config), out)
+        _lib.check(self._lib.mimi_encode(self._h, ctypes.c_void_p(audio.data_ptr()), B, L, K,
+                                         ctypes.c_void_p(out.data_ptr()), self._stream()))
         return out
 
     def encode_async(self, audio: torch.Tensor, num_quantizers: int, out: Optional[torch.Tensor] = None
@@ -237,14 +268,13 @@ class MimiHipModel:
         """Enqueue an encode of device f32 [B, L] on the current stream and return without waiting
         (``mimi_encode_async``); ``ticket.wait()`` returns the int32 [B, K, T] codes once they are final (the
         f16x3 overflow check runs there).  The ticket keeps ``audio`` alive until then."""
+        K = self._check_k(num_quantizers)
+        audio = self._device_audio(audio)
         B, L = audio.shape
-        T = encoded_length(L, self.config)
-        if out is None:
-            out = torch.empty((B, num_quantizers, T), dtype=torch.int32, device=self.device)
+        out = self._out(B, K, encoded_length(L, self.config), out)
         t = ctypes.c_int64()
-        with self._lock:
-            _lib.check(self._lib.mimi_encode_async(self._h, ctypes.c_void_p(audio.data_ptr()), B, L, num_quantizers,
-                                                   ctypes.c_void_p(out.data_ptr()), self._stream(), ctypes.byref(t)))
+        _lib.check(self._lib.mimi_encode_async(self._h, ctypes.c_void_p(audio.data_ptr()), B, L, K,
+                                               ctypes.c_void_p(out.data_ptr()), self._stream(), ctypes.byref(t)))
         return EncodeTicket(self, t.value, out, audio)
 
     def quantize(self, embedding: torch.Tensor, num_quantizers: int) -> torch.Tensor:
@@ -267,6 +297,10 @@ class MimiHipModel:
     def precision(self) -> str:
         v = self._lib.mimi_get_precision(self._h)
         return {i: k for k, i in _lib.PRECISIONS.items()}[v]
+
+    def calibrate(self):
+        """Run the f16x3 activation-scale calibration now (otherwise it runs inside the first f16x3 encode)."""
+        _lib.check(self._lib.mimi_calibrate(self._h))
 
     @property
     def f16_reruns(self) -> int:
@@ -318,6 +352,19 @@ class MimiHipModel:
             while key in out:  # one stage run by two kernel symbols (e.g. the last layer's fc2): "fc2#2"
                 key, j = f"{stage}#{j}", j + 1
             out[key] = dict(kernel=kernel, ms=ms[i], launches=launches[i], flops=fb[2 * i], bytes=fb[2 * i + 1])
+        return out
+
+    def profile_sequence(self):
+        """[(stage, kernel symbol)] of the last profiled encode in launch order (mimi_profile_sequence)."""
+        n = 512
+        names = ctypes.create_string_buffer(128 * n)
+        cnt = ctypes.c_int32()
+        _lib.check(self._lib.mimi_profile_sequence(self._h, n, names, ctypes.byref(cnt)))
+        out = []
+        for i in range(cnt.value):
+            nm = names.raw[128 * i:128 * (i + 1)].split(b"\0", 1)[0].decode()
+            stage, _, kernel = nm.partition("|")
+            out.append((stage, kernel))
         return out
 
     def set_taps(self, enable: bool = True):

@@ -12,7 +12,7 @@ IFS=';' read -ra GROUPS_ <<< "$PASSES"
 for G in "${GROUPS_[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc ${G//,/ } --kernel-trace -d "$OUT/p$i" -o run --output-format csv -- \
-    python3 "$R/bench.py" --steps 2 --warmup 1 --cpu-baseline-seconds 0 --no-profile ${BENCH_ARGS:-} \
+    python3 "$R/bench.py" --steps 2 --warmup 1 --cpu-baseline-seconds 0 --no-profile --pmc-pass ${BENCH_ARGS:-} \
     > "$OUT/p$i.log" 2>&1 || { echo "pass $i ($G) failed rc=$?"; tail -20 "$OUT/p$i.log"; exit 1; }
   echo "pass $i ok: $G"
 done

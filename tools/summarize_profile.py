@@ -6,6 +6,13 @@ Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats summary
 profiles/<tag>_pmc_summary.json (per-kernel mean FETCH_SIZE / WRITE_SIZE per launch from the two separate
 --pmc passes, with the gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md §HBM applied) and
 profiles/pmc_summary.json (the latest, read by bench.py to fill roofline.traffic).
+
+PMC bytes are keyed by STAGE (bench.py's stage names: res_s0, down_s1, qkv, rvq, ...), not only by kernel symbol, so a
+retuned template does not drop out of the lookup: the bench writes the engine's per-encode launch sequence
+(`--dump-sequence`, mimi_profile_sequence) and the counter rows after the spin marker are walked against it -- a row
+whose kernel is the next stage's named kernel opens that stage, any other row (a stage's further dispatches: RVQ
+levels, the downsample's edge fix) belongs to the open stage; the engine's own bookkeeping kernels (amax fold,
+set_io) and torch's are kept out.
 """
 import collections
 import csv
@@ -15,6 +22,53 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _norm(k):
+    return k.replace("void ", "", 1).split("(")[0].strip().replace("mimi::", "")
+
+
+OTHER = ("amax_reduce", "set_io", "spin_kernel", "at::", "elementwise", "vectorized", "Memcpy", "memset")
+
+
+def stage_bytes(src, seq):
+    """Per-stage mean FETCH / WRITE bytes per launch, from the counter rows aligned to the launch sequence."""
+    names = [(st, _norm(k)) for st, k in seq]
+    per = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        p = os.path.join(src, f"pmc_{counter}", "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        rows = list(csv.DictReader(open(p)))
+        if "Dispatch_Id" in rows[0]:
+            rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        mk = [i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]]
+        rows = rows[mk[0] + 1:] if mk else rows
+        j, cur, acc = 0, None, collections.defaultdict(float)
+        launches = collections.Counter()
+        for r in rows:
+            k = _norm(r["Kernel_Name"])
+            if any(o in r["Kernel_Name"] for o in OTHER):
+                continue
+            if k == names[j][1]:
+                cur = names[j]
+                launches[cur[0]] += 1
+                j = (j + 1) % len(names)
+            if cur is None:
+                continue
+            acc[cur[0]] += float(r["Counter_Value"])
+        for st, tot in acc.items():
+            d = per.setdefault(st, {"kernel": "mimi::" + dict(names)[st] if st in dict(names) else None})
+            kb = tot / max(1, launches[st])  # per stage launch (a stage's extra dispatches summed into it)
+            if counter == "FETCH_SIZE":
+                d["fetch_bytes"] = kb * 1024 * 2.0
+            else:
+                d["write_bytes"] = kb * 1024
+            d["launches_" + counter] = launches[st]
+    for d in per.values():
+        if "fetch_bytes" in d and "write_bytes" in d:
+            d["traffic_bytes"] = d["fetch_bytes"] + d["write_bytes"]
+    return per
 
 
 def main(tag):
@@ -56,6 +110,11 @@ def main(tag):
     for d in out["kernels"].values():
         if "fetch_bytes" in d and "write_bytes" in d:
             d["traffic_bytes"] = d["fetch_bytes"] + d["write_bytes"]
+    seqp = os.path.join(src, "stage_sequence.json")
+    if os.path.exists(seqp):
+        with open(seqp) as f:
+            seq = json.load(f)
+        out["stages"] = stage_bytes(src, seq)
     # the dominant kernel's steady-state launches in the kernel trace (the bench's own timed steps: the last
     # `launches` of that kernel; calibration / warm-up launches excluded) next to the bench's HIP-event figure
     if os.path.exists(bj):
