@@ -546,7 +546,9 @@ extern "C" int mimi_load_safetensors(mimi_engine* e, const char* path) {
     std::lock_guard<std::mutex> lk(e->mu);
     auto wanted = [&](const std::string& name) {
         if (name.rfind("decoder", 0) == 0 || name.rfind("upsample", 0) == 0) return false;
-        return e->expected.count(name) > 0 || name.rfind("quantizer.", 0) == 0 ||
+        const bool quant = name.rfind("quantizer.", 0) == 0 &&  // input_proj + codebooks (not output_proj)
+                           (name.find(".codebook.") != std::string::npos || name.find("input_proj") != std::string::npos);
+        return e->expected.count(name) > 0 || quant ||
                name.find("weight_g") != std::string::npos || name.find("weight_v") != std::string::npos ||
                name.find("original0") != std::string::npos || name.find("original1") != std::string::npos;
     };

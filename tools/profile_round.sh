@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 BENCH="$R/bench.py"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
   python3 "$BENCH" --steps ${STEPS:-10} --warmup 3 --cpu-baseline-seconds 0 --json-out "$OUT/bench_under_trace.json" \
-  --dump-sequence "$OUT/stage_sequence.json" \
+  --dump-sequence "$OUT/stage_sequence.json" --pmc-pass \
   > "$OUT/trace.log" 2>&1 || { echo "trace failed rc=$?"; tail -20 "$OUT/trace.log"; exit 1; }
 echo "trace ok"
 if [ "${PMC:-1}" = 1 ]; then
