@@ -83,9 +83,7 @@ def parse():
                     help="wall budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: this process's CPU affinity, capped by OMP_NUM_THREADS)")
-    ap.add_argument("--concurrency", type=int, default=0,
-                    help="mls workload: engines encoding different utterances at once through "
-                         "MimiEncoder.encode_audio_chunks (0 = 4)")
+    ap.add_argument("--concurrency", type=int, default=0, help="(ignored: per-utterance encodes run as ragged batches)")
     ap.add_argument("--bpe", action="store_true",
                     help="mls workload: after the timed encodes, train codec-BPE (GPU merge loop) over the emitted "
                          "codes on rank 0, timed separately (configs[4])")
@@ -326,8 +324,7 @@ class Workload:
             self.desc = (f"LibriTTS-R-style batch encode (configs[{1 if B <= 32 else 2}]): batch={B} x "
                          f"{args.seconds:g} s @ 24 kHz resident in HBM, K={K} codebooks, 1 encode per step per GPU")
             return
-        conc = (args.concurrency or 4) if self.kind == "mls" else 1
-        enc = MimiEncoder(device=dev, model=model, num_quantizers=K, concurrency=conc)
+        enc = MimiEncoder(device=dev, model=model, num_quantizers=K)
         lo, hi = (1.5, 20.0) if self.kind == "yodas2" else (10.0, 20.0)
         n_steps = args.warmup + args.steps
         # the whole shard's utterance list; this rank takes i % world == rank (sharding.py), in batches of B
@@ -340,28 +337,42 @@ class Workload:
         self.i = 0
 
         if self.kind == "yodas2":
-            def step():
-                enc.encode_audio_batch(self.clips[self.i], 24000)
-                self.i += 1
+            def run(first, count):  # the steps' batches through the pipelined iterator (host staging overlapped)
+                for _ in enc.encode_batches(self.clips[first:first + count], 24000):
+                    pass
             self.desc = (f"YODAS2-style shard (configs[3]): batches of {B} mixed-length clips U[{lo:g}, {hi:g}] s "
-                         f"from host memory through MimiEncoder.encode_audio_batch (pad to longest, H2D, encode, "
-                         f"D2H, trim), K={K}, utterance round-robin over {world} GPU(s)")
+                         f"from host memory through MimiEncoder.encode_batches (= encode_audio_batch per batch: "
+                         f"pad-to-longest codes, run as a ragged encode at min(Lmax, 1920 ceil(L/1920)) per item; host "
+                         f"staging, H2D, encode, D2H, trim -- the next batch staged under the current encode), K={K}, "
+                         f"utterance round-robin over {world} GPU(s)")
         else:
             self.emitted = []  # codes of the timed steps, for --bpe
 
-            def step():
-                out = enc.encode_audio_chunks(self.clips[self.i], 24000)
-                if self.i >= args.warmup:
+            def run(first, count):  # every utterance of the steps, each encoded alone (ragged batches of 32)
+                out = enc.encode_audio_chunks([a for c in self.clips[first:first + count] for a in c], 24000)
+                if first >= args.warmup:
                     self.emitted.extend(out)
-                self.i += 1
             self.desc = (f"MLS-style stream (configs[4], encode part): {B} utterances U[{lo:g}, {hi:g}] s per step, "
-                         f"each encoded alone at its own length (encode_audio_chunk semantics, batch 1, H2D + D2H "
-                         f"included) through MimiEncoder.encode_audio_chunks with {conc} engine(s) at once, K={K}, "
-                         f"utterance round-robin over {world} GPU(s)" +
+                         f"each encoded alone at its own length (encode_audio_chunk semantics, bit for bit; H2D + D2H "
+                         f"included) through MimiEncoder.encode_audio_chunks = ragged batches of 32 by length, "
+                         f"pipelined, K={K}, utterance round-robin over {world} GPU(s)" +
                          ("; then codec-BPE training over the timed steps' codes on rank 0 (`bpe`, `pipeline_value`)"
                           if args.bpe else ""))
+        self.run = run
+
+        def step():
+            run(self.i, 1)
+            self.i += 1
         self.step = step
         self._np = np
+
+    def run_steps(self, first, count):
+        """count steps starting at step index first (host-resident workloads pipeline across them)"""
+        if self.kind == "batch":
+            for _ in range(count):
+                self.step()
+        else:
+            self.run(first, count)
 
     def timed_seconds(self, first, count):
         if self.kind == "batch":
@@ -455,8 +466,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        wl.step()
+    wl.run_steps(0, args.warmup)
     torch.cuda.synchronize()
     profile = not args.no_profile and wl.kind == "batch"
     # small batches are launch-bound and replay hipGraphs (engine.cpp graph_encode), which per-stage events
@@ -468,8 +478,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        wl.step()
+    wl.run_steps(args.warmup, args.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
@@ -485,8 +494,7 @@ def main():
     if profile_separately:
         model.profile_reset()
         model.set_profiling(True)
-        for _ in range(args.steps):
-            wl.step()
+        wl.run_steps(args.warmup, args.steps)
         torch.cuda.synchronize()
     if profile:
         model.set_profiling(False)

@@ -111,6 +111,27 @@ int mimi_encode_async(mimi_engine* e, const float* dev_audio, int32_t batch, int
 int mimi_encode_wait(mimi_engine* e, int64_t ticket);
 
 /*
+ * Ragged batch: item b's samples are dev_audio[b][0 .. lengths[b]) (rows max_length apart; samples past lengths[b]
+ * are never read), lengths a HOST int64 array, 1 <= lengths[b] <= max_length.  Each item is encoded exactly as
+ * mimi_encode(dev_audio[b], 1, lengths[b], ...) would encode it alone -- its codes, frames [0,
+ * mimi_encoded_length(lengths[b])) of dev_codes[b], are bit for bit those -- while the batch runs as one pass
+ * whose kernels skip every item's rows past its own length.  Frames past an item's own are unspecified.
+ * dev_codes: device int32 [batch][num_quantizers][mimi_encoded_length(max_length)].
+ *   - per-utterance callers (batch-1 semantics: mls-en-mimi-pretrain/process_shard.py:302-307,
+ *     librispeech-mimi/process_librispeech_dev-test.py:136-141) pass each utterance's length;
+ *   - pad-to-longest callers (EncodecFeatureExtractor padding, emilia-mimi/process_shard.py:113-139) pass
+ *     min(max_length, 1920 ceil(L_b / 1920)) over the zero-padded batch: every frame the caller keeps,
+ *     ceil(L_b / 1920), depends only on samples below that length (all convs causal, no extra padding at a
+ *     multiple of 1920), so the kept frames are the padded batch's -- without the padding's compute.
+ * In f16x3 the overflow check applies per batch; a fallback re-encodes each item alone at its length.
+ */
+int mimi_encode_ragged(mimi_engine* e, const float* dev_audio, const int64_t* lengths, int32_t batch,
+                       int64_t max_length, int32_t num_quantizers, int32_t* dev_codes, void* stream);
+int mimi_encode_ragged_async(mimi_engine* e, const float* dev_audio, const int64_t* lengths, int32_t batch,
+                             int64_t max_length, int32_t num_quantizers, int32_t* dev_codes, void* stream,
+                             int64_t* ticket);
+
+/*
  * The quantizer alone: dev_embedding is the pre-quantizer embedding, device f32 [frames][hidden_size]
  * (frame-major, i.e. the reference's [B, 512, T] transposed to [B*T, 512]).  dev_codes: int32
  * [num_quantizers][frames].

@@ -160,7 +160,23 @@ def test_pre_quantizer_embedding_and_audit(engine, golden, tag, length, seed_ind
     assert frac >= EXACT_MIN, frac
 
 
-def _audit_padded_batch(engine, outs, refs, x_padded, state_dict, parity_log=None, name="padded"):
+def our_padded_embedding(engine, x_padded, lengths, ragged):
+    """Our pre-quantizer embedding of a padded batch [B, 1, Lmax] as the wrapper computed it: the literal padded
+    encode, or (ragged) the ragged encode at the wrapper's per-item lengths E_i (mimi_hip/encoder.py)."""
+    from mimi_hip.encoder import padded_batch_lengths
+    engine.set_taps(True)
+    try:
+        if ragged:
+            engine.encode_ragged(torch.from_numpy(x_padded[:, 0]).cuda(), padded_batch_lengths(lengths), 32)
+        else:
+            engine.encode(torch.from_numpy(x_padded).cuda())
+        return engine.get_tap("downsample").transpose(0, 2, 1)
+    finally:
+        engine.set_taps(False)
+
+
+def _audit_padded_batch(engine, outs, refs, x_padded, state_dict, parity_log=None, name="padded", lengths=None,
+                        ragged=True):
     """Our wrapper outputs vs the reference wrapper's on a padded batch: exact, or every flip explained by the
     measured pre-quantizer error on that padded batch (our embedding from the taps, the oracle's on the same
     padded input; audit.perturbation_near_tie)."""
@@ -172,12 +188,7 @@ def _audit_padded_batch(engine, outs, refs, x_padded, state_dict, parity_log=Non
         if np.array_equal(o, ref):
             continue
         if emb is None:
-            engine.set_taps(True)
-            try:
-                engine.encode(torch.from_numpy(x_padded).cuda())
-                emb = engine.get_tap("downsample").transpose(0, 2, 1)
-            finally:
-                engine.set_taps(False)
+            emb = our_padded_embedding(engine, x_padded, lengths, ragged)
             taps = {}
             mimi_ref.encode(torch.from_numpy(x_padded), state_dict, taps=taps)
             emb_ref = taps["pre_quantizer"].numpy()
@@ -201,7 +212,8 @@ def test_batch_wrapper_matches_reference_wrapper(engine, golden, state_dict, par
     x = np.zeros((len(audio), 1, max(meta["batch_lengths"])), np.float32)
     for i, a in enumerate(audio):
         x[i, 0, :len(a)] = a
-    _audit_padded_batch(engine, outs, refs, x, state_dict, parity_log, "reference_wrapper_b5")
+    _audit_padded_batch(engine, outs, refs, x, state_dict, parity_log, "reference_wrapper_b5",
+                        lengths=meta["batch_lengths"])
     assert enc.encode_audio_batch([], 24000) == []
     # one item: the wrapper delegates to encode_audio_chunk (no trim), as the reference does
     s = enc.encode_audio_batch([audio[2]], 24000)[0]
@@ -230,18 +242,20 @@ def test_encode_audio_chunks_equals_per_utterance_calls(engine, golden):
     assert enc.encode_audio_chunks([], 24000) == []
 
 
-def test_padded_batch_b32_vs_reference_wrapper(engine, state_dict, parity_log):
+@pytest.mark.parametrize("ragged", [True, False])
+def test_padded_batch_b32_vs_reference_wrapper(engine, state_dict, parity_log, ragged):
     """B = 32 mixed lengths U[1.5, 20] s (17 items > 10.24 s: window-250 attention path; items 3 and 7 at -40 /
     -60 dB) through our MimiEncoder vs the reference's own MimiEncoder.encode_audio_batch
     (tests/golden/make_golden_batch.py): >= EXACT_MIN of all codes exact, and every flip explained by the measured
-    pre-quantizer error on that padded batch (the oracle's embedding of the same padded input)."""
+    pre-quantizer error on that padded batch (the oracle's embedding of the same padded input).  Both forms of the
+    padded batch: the ragged encode at E_i (the wrapper's default) and the literal padded encode."""
     from mimi_hip.encoder import MimiEncoder
     with open(os.path.join(GOLDEN_DIR, "golden_batch_meta.json")) as f:
         meta = json.load(f)
     audio = [synthetic.speech_like(L, meta["audio_seed"], meta["audio_index0"] + i) *
              np.float32(meta["quiet_gain"].get(str(i), 1.0)) for i, L in enumerate(meta["lengths"])]
     assert synthetic.audio_sha256(audio) == meta["audio_sha256"]
-    enc = MimiEncoder(device="cuda:0", model=engine)
+    enc = MimiEncoder(device="cuda:0", model=engine, ragged=ragged)
     outs = enc.encode_audio_batch(audio, 24000)
     with np.load(os.path.join(GOLDEN_DIR, "golden_batch.npz"), allow_pickle=False) as z:
         refs = [z[f"item{i}"].astype(np.int64) for i in range(len(outs))]
@@ -257,12 +271,7 @@ def test_padded_batch_b32_vs_reference_wrapper(engine, state_dict, parity_log):
         xp = np.zeros((len(audio), 1, Lmax), np.float32)
         for i, a in enumerate(audio):
             xp[i, 0, :len(a)] = a
-        engine.set_taps(True)
-        try:
-            engine.encode(torch.from_numpy(xp).cuda())
-            emb = engine.get_tap("downsample").transpose(0, 2, 1)
-        finally:
-            engine.set_taps(False)
+        emb = our_padded_embedding(engine, xp, meta["lengths"], ragged)
         taps = {}
         mimi_ref.encode(torch.from_numpy(xp), state_dict, taps=taps)
         emb_ref = taps["pre_quantizer"].numpy()
@@ -274,7 +283,7 @@ def test_padded_batch_b32_vs_reference_wrapper(engine, state_dict, parity_log):
             bad += [(i,) + x for x in b]
             flips += fl
             thr = max(thr, t)
-    rec = record(parity_log, "padded_batch_b32", allc, allr, flips, thr,
+    rec = record(parity_log, f"padded_batch_b32[{'ragged' if ragged else 'literal'}]", allc, allr, flips, thr,
                  item_exact_min=float(min((o == r).mean() for o, r in zip(outs, refs))))
     assert not bad, bad[:5]
     assert rec["exact"] >= EXACT_MIN, rec

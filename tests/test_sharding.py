@@ -41,14 +41,38 @@ class _FakeEncoder:
         return [np.array([len(a), lmax, int(a[0] * 1000)], dtype=np.int64) for a in batch]
 
 
-def _worker(rank, world, port, audio, q):
+class _FakePipelinedEncoder(_FakeEncoder):
+    """As _FakeEncoder, with the pipelined batch iterator: pulls batch i + 1 before yielding batch i's codes."""
+
+    def encode_batches(self, batches, sr):
+        prev = None
+        for b in batches:
+            b = list(b)
+            if prev is not None:
+                yield self.encode_audio_batch(prev, sr)
+            prev = b
+        if prev is not None:
+            yield self.encode_audio_batch(prev, sr)
+
+
+def _worker(rank, world, port, audio, q, lazy=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        enc = sharding.DistributedMimiEncoder(encoder=_FakeEncoder(), batch_size=2)
-        out = enc.encode_all(audio)
+        if lazy:  # each rank loads only its own utterances, through the pipelined iterator
+            touched = []
+
+            def load(i):
+                touched.append(i)
+                return audio[i]
+            enc = sharding.DistributedMimiEncoder(encoder=_FakePipelinedEncoder(), batch_size=2)
+            out = enc.encode_all(n_items=len(audio), loader=load)
+            assert sorted(touched) == sharding.shard_indices(len(audio), world, rank), touched
+        else:
+            enc = sharding.DistributedMimiEncoder(encoder=_FakeEncoder(), batch_size=2)
+            out = enc.encode_all(audio)
         if rank == 0:
             q.put([o.tolist() for o in out])
     finally:
@@ -63,13 +87,14 @@ def _free_port():
     return p
 
 
-def test_gloo_world2_matches_single_process_per_rank_batches():
+@pytest.mark.parametrize("lazy", [False, True])
+def test_gloo_world2_matches_single_process_per_rank_batches(lazy):
     rng = np.random.RandomState(0)
     audio = [rng.rand(int(n)).astype(np.float32) + 0.01 for n in rng.randint(5, 50, size=9)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, audio, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, audio, q, lazy)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)

@@ -284,6 +284,10 @@ struct mimi_engine {
         int64_t L = 0;
         int32_t* codes = nullptr;
         hipStream_t s = nullptr;
+        bool ragged = false;          // a ragged batch (lens: the items' lengths, for the overflow fallback)
+        std::vector<int64_t> lens;
+        int* rg_pinned = nullptr;     // pinned image of its RaggedTable (read by the encode's async upload)
+        size_t rg_cap = 0;
     };
     static constexpr int kMaxPending = 16;
     Pending pend[kMaxPending];
@@ -905,6 +909,40 @@ struct Workspace {
     float *dsout, *proj;
     float* rvq;  // rvq_work_bytes(frames)
     float *xe, *h;  // planes path, unfused residual blocks: ELU(x) planes, hidden planes
+    int* rg;        // ragged batches: the per-item length table (RaggedTable)
+};
+
+// Ragged batches (mimi_encode_ragged): item b is encoded exactly as it would be alone at its own length L_b --
+// every kernel reads only its item's valid rows (the rest read as zero: the item's own extra padding) and
+// computes / stores / max-reduces only its valid rows.  The per-item lengths of every stage live in one small
+// device table, stage-major: T[0..4][B] (conv0 / down-conv outputs), T25[B], F[B] (12.5 Hz frames), then the
+// fused blocks' tile prefixes st0[B + 1], st1[B + 1] (32-step tiles over T[0] / T[1]).
+struct RaggedTable {
+    enum { NST = 7 };
+    int B = 0;
+    std::vector<StagePlan> plan;  // per item
+    std::vector<int64_t> len;     // samples per item
+    int minT25 = 0, maxT25 = 0;
+    static size_t ints(int B) { return (size_t)NST * B + 2 * ((size_t)B + 1); }
+    void fill(int* h) const {  // the device image (host side)
+        for (int b = 0; b < B; ++b) {
+            for (int st = 0; st < 5; ++st) h[st * B + b] = (int)plan[b].T[st];
+            h[5 * B + b] = (int)plan[b].frames25;
+            h[6 * B + b] = (int)plan[b].frames12;
+        }
+        unsigned* s0 = reinterpret_cast<unsigned*>(h + NST * B);
+        unsigned* s1 = s0 + B + 1;
+        s0[0] = s1[0] = 0;
+        for (int b = 0; b < B; ++b) {
+            s0[b + 1] = s0[b] + (unsigned)((plan[b].T[0] + 31) / 32);
+            s1[b + 1] = s1[b] + (unsigned)((plan[b].T[1] + 31) / 32);
+        }
+    }
+    double rows(int st) const {  // valid rows of stage st (0..4: T, 5: T25, 6: F) summed over the items
+        double r = 0;
+        for (const auto& p : plan) r += st < 5 ? (double)p.T[st] : st == 5 ? (double)p.frames25 : (double)p.frames12;
+        return r;
+    }
 };
 
 // Planes of the split-bf16 path: activations consumed only by GEMMs (resblock outputs, the last down conv's
@@ -924,7 +962,7 @@ static int act_planes(const mimi_engine* e, const StagePlan& p, int prec) {
     return ns;
 }
 
-static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspace* w, int prec) {
+static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspace* w, int prec, bool ragged = false) {
     const mimi_config& c = e->cfg;
     const int ns = act_planes(e, p, prec);
     // a plane-format buffer of n values takes ns * n bf16 = ns * n / 2 floats
@@ -951,15 +989,18 @@ static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspa
                             (size_t)p.frames12 * 2 * c.vq_hidden_dim * B,
                             rvq_work_bytes((long long)p.frames12 * B) / sizeof(float),
                             act(xemax * B),
-                            act(xemax / 2 * B)};
+                            act(xemax / 2 * B),
+                            ragged ? RaggedTable::ints(B) : 0};
     size_t off = 0;
+    float* rgp = nullptr;
     float** ptrs[] = {&w->x, &w->y, &w->t0, &w->t1, &w->qkv, &w->att, &w->ff, &w->dsout, &w->proj, &w->rvq,
-                      &w->xe, &w->h};
+                      &w->xe, &w->h, &rgp};
     char* base = reinterpret_cast<char*>(e->ws);
     for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); ++i) {
         if (w) *ptrs[i] = reinterpret_cast<float*>(base + off);
         off += ((sizes[i] * sizeof(float) + 255) / 256) * 256;
     }
+    if (w) w->rg = reinterpret_cast<int*>(rgp);
     return off;
 }
 
@@ -1134,8 +1175,9 @@ static GemmArgs linear_args(const float* in, int64_t rows, int K, const float* W
     } while (0)
 
 static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int32_t* codes, int frames_per_item,
-                   void* work, hipStream_t s, Recorder& rec) {
+                   void* work, hipStream_t s, Recorder& rec, const int* flen = nullptr, double valid_share = 1.0) {
     RvqArgs r{};
+    r.flen = flen;
     r.work = work;
     r.proj = proj;
     r.frames = frames;
@@ -1154,19 +1196,20 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     r.frames_per_item = frames_per_item;
     const char* kname = "?";
     LAUNCH_TRY(launch_rvq(r, s, &kname), "rvq");
-    rec.mark("rvq", 2.0 * frames * r.D * r.ncodes * K, (double)frames * (2 * r.D) * 4 + (double)frames * K * 4, kname);
+    rec.mark("rvq", 2.0 * frames * valid_share * r.D * r.ncodes * K,
+             (double)frames * (2 * r.D) * 4 + (double)frames * K * 4, kname);
     return MIMI_OK;
 }
 
 // One pass of the whole encode at precision prec.
 static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s,
-                       int prec) {
+                       int prec, const RaggedTable* rg = nullptr, const int* rg_pinned = nullptr) {
     const mimi_config& c = e->cfg;
     const StagePlan p = plan_lengths(c, L);
     Workspace w{};
-    int rc = ensure_ws(e, ws_layout(e, B, p, nullptr, prec), s);
+    int rc = ensure_ws(e, ws_layout(e, B, p, nullptr, prec, rg != nullptr), s);
     if (rc) return rc;
-    ws_layout(e, B, p, &w, prec);
+    ws_layout(e, B, p, &w, prec, rg != nullptr);
     if ((rc = ensure_rope(e, p.frames25))) return rc;
     const int ns = act_planes(e, p, prec);  // 0: fp32 activations; 2/3: plane-format GEMM inputs
     // fp16 planes: each plane-format tensor takes the next activation-scale slot (launch order)
@@ -1208,6 +1251,21 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     Recorder rec{e, s};
     const char* kname = "?";
     if (!e->capturing) HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));  // (a replay waits outside the graph)
+    // ragged batches: the length table (pinned host image, alive until the encode is waited) -> workspace
+    const int* dT[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    const int *dT25 = nullptr, *dF = nullptr;
+    const unsigned *dst0 = nullptr, *dst1 = nullptr;
+    if (rg) {
+        if (!rg_pinned || rg->B != B || !w.rg) return set_err(MIMI_ERR_STATE, "ragged encode without its length table");
+        HIP_TRY(hipMemcpyAsync(w.rg, rg_pinned, RaggedTable::ints(B) * sizeof(int), hipMemcpyHostToDevice, s));
+        for (int st = 0; st < 5; ++st) dT[st] = w.rg + st * B;
+        dT25 = w.rg + 5 * B;
+        dF = w.rg + 6 * B;
+        dst0 = reinterpret_cast<const unsigned*>(w.rg + RaggedTable::NST * B);
+        dst1 = dst0 + B + 1;
+    }
+    // (profile bookkeeping) a GEMM's algorithmic FLOPs over the items' valid rows
+    auto rows_of = [&](int st, double uniform) { return rg ? rg->rows(st) : uniform; };
     rec.begin();
     auto gemm_flops = [](const GemmArgs& a) { return 2.0 * a.batch * (double)a.M * a.N * a.K; };
     auto gemm_bytes = [](const GemmArgs& a, bool res) {
@@ -1247,6 +1305,10 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             }
             ra.T = T;
             ra.batch = B;
+            if (rg) {
+                ra.ilen = dT[si];
+                ra.istart = si == 0 ? dst0 : dst1;
+            }
             ra.w3 = e->res3[si].w;
             ra.b3 = e->res3[si].b;
             ra.w1 = e->res1[si].w;
@@ -1288,11 +1350,13 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                 ra.xamax = xa.amax;
                 ra.hamax = ha.amax;
             }
+            if (rg && !(h16 && (si == 0 || si == 1))) return set_err(MIMI_ERR_UNSUPPORTED, "ragged: fp16 blocks only");
             LAUNCH_TRY(launch_resblock(C, ra, s, &kname), "resblock");
             snprintf(nm, sizeof nm, "res_s%d", si);
             const double H = C / c.compress;
-            const double fl = 2.0 * B * T * (3.0 * C * H + H * C) + (si == 0 ? 2.0 * B * T * C * c.kernel_size : 0.0);
-            const double by = (double)B * T * 4 * (si == 0 ? 1 + C : 2 * C) + (3.0 * C * H + H * C) * 4;
+            const double BT = rows_of(si, (double)B * T);
+            const double fl = 2.0 * BT * (3.0 * C * H + H * C) + (si == 0 ? 2.0 * BT * C * c.kernel_size : 0.0);
+            const double by = BT * 4 * (si == 0 ? 1 + C : 2 * C) + (3.0 * C * H + H * C) * 4;
             rec.mark(nm, fl, by, kname);
         } else {
             // two plane GEMMs: h = ELU(b3 + W3 (*) ELU(x)) from the ELU(x) planes the down conv wrote, then
@@ -1303,22 +1367,24 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             use_h(a3, e->res3[si].wh, e->res3[si].wscale, xeact);
             a3.Cp = w.h;
             a3.c_pstride = (long long)B * T * Hh;
+            if (rg) a3.a_rows = a3.m_rows = dT[si];
             hact = new_act(nmf("h%d", si));
             out_act(a3, hact);
             LAUNCH_TRY(launch_gemm(ROLE_RES3P, a3, s, &kname, prec), "res3");
             snprintf(nm, sizeof nm, "res3_s%d", si);
-            rec.mark(nm, gemm_flops(a3), gemm_bytes(a3, false), kname);
+            rec.mark(nm, gemm_flops(a3) * rows_of(si, (double)B * T) / ((double)B * T), gemm_bytes(a3, false), kname);
             GemmArgs a1 = conv_args(e->res1[si], nullptr, T, nullptr, T, B);
             planes_in(a1, w.h, (long long)B * T * Hh);
             use_h(a1, e->res1[si].wh, e->res1[si].wscale, hact);
             a1.R = w.x;
             a1.Cp = w.y;
             a1.c_pstride = (long long)B * T * C;
+            if (rg) a1.a_rows = a1.m_rows = dT[si];
             yact = new_act(nmf("y%d", si));
             out_act(a1, yact);
             LAUNCH_TRY(launch_gemm(ROLE_RES1P, a1, s, &kname, prec), "res1");
             snprintf(nm, sizeof nm, "res1_s%d", si);
-            rec.mark(nm, gemm_flops(a1), gemm_bytes(a1, true), kname);
+            rec.mark(nm, gemm_flops(a1) * rows_of(si, (double)B * T) / ((double)B * T), gemm_bytes(a1, true), kname);
         }
         snprintf(nm, sizeof nm, "res%d_elu", si);
         if ((rc = save_tap_planes(e, nm, w.y, ns, B, T, C, s, yact.scale))) return rc;
@@ -1343,9 +1409,14 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                 out_act(ad, xeact);
             }
         }
+        if (rg) {
+            ad.a_rows = dT[si];
+            ad.m_rows = dT[si + 1];
+        }
         LAUNCH_TRY(launch_gemm(role, ad, s, &kname, prec), "down");
         snprintf(nm, sizeof nm, "down_s%d", si);
-        rec.mark(nm, gemm_flops(ad), gemm_bytes(ad, false), kname);
+        rec.mark(nm, gemm_flops(ad) * rows_of(si + 1, (double)B * p.T[si + 1]) / ((double)B * p.T[si + 1]),
+                 gemm_bytes(ad, false), kname);
         snprintf(nm, sizeof nm, last ? "down%d_elu" : "down%d", si);
         if ((rc = save_tap_planes(e, nm, w.x, last ? ns : 0, B, p.T[si + 1], 2 * C, s, last ? xact.scale : 0.0f)))
             return rc;
@@ -1356,8 +1427,13 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     GemmArgs af = conv_args(e->final_conv, w.x, p.T[c.num_ratios], w.t0, T, B);
     if (ns) planes_in(af, w.x, (long long)B * p.T[c.num_ratios] * C);
     use_h(af, e->final_conv.wh, e->final_conv.wscale, xact);
+    if (rg) {
+        af.a_rows = dT[c.num_ratios];
+        af.m_rows = dT25;
+    }
     LAUNCH_TRY(launch_gemm(ROLE_FINAL, af, s, &kname, prec), "final");
-    rec.mark("final", gemm_flops(af), gemm_bytes(af, false), kname);
+    const double rT25 = rows_of(5, (double)B * p.frames25) / ((double)B * p.frames25);  // ragged share of the rows
+    rec.mark("final", gemm_flops(af) * rT25, gemm_bytes(af, false), kname);
     if ((rc = save_tap(e, "encoder", w.t0, B, T, Hd, s))) return rc;
 
     // ---- transformer (x in t0) ----
@@ -1367,14 +1443,33 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     const bool ds_planes = h16 && e->ds_fix && e->inproj_h && c.downsample_kernel == 4 && c.downsample_stride == 2;
     Act dsin, dsouta;
     double att_flops = 0;
-    for (int64_t i = 0; i < T; ++i) att_flops += 4.0 * Dh * std::min<int64_t>(i + 1, c.sliding_window);
-    att_flops *= (double)B * H;
+    auto att_fl = [&](int64_t Tn) {
+        double f = 0;
+        for (int64_t i = 0; i < Tn; ++i) f += 4.0 * Dh * std::min<int64_t>(i + 1, c.sliding_window);
+        return f * H;
+    };
+    if (rg) {
+        for (const auto& pb : rg->plan) att_flops += att_fl(pb.frames25);
+    } else {
+        att_flops = att_fl(T) * B;
+    }
+    // ragged: the row-local transformer GEMMs run per item (batch B, M = T rows each, the valid ones per item) --
+    // the same instruction sequence per output as the flattened [B x T] form
+    auto per_item = [&](GemmArgs& a, int64_t Mi, int Kd, int Nd, const int* valid) {
+        if (!rg) return;
+        a.batch = B;
+        a.M = (int)Mi;
+        a.a_bstride = Mi * Kd;
+        a.c_bstride = Mi * Nd;
+        a.a_len = Mi * Kd;
+        a.a_rows = a.m_rows = valid;
+    };
     for (int l = 0; l < c.num_hidden_layers; ++l) {
         const DevXfmr& x = e->xf[l];
         const long long nact = rows * Hd;
         const Act t1a = new_act(nmf("xf%d.ln1", l));
         LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1a.scale,
-                                    t1a.amax),
+                                    t1a.amax, rg ? dT25 : nullptr, (int)T),
                    "ln1");
         rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
         GemmArgs aq = linear_args(w.t1, T, Hd, x.wqkv, 3 * H * Dh, w.qkv);
@@ -1387,15 +1482,17 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         aq.rope_cols = 2 * H * Dh;
         if (ns) planes_in(aq, w.t1, nact);
         use_h(aq, x.wqkv_h, x.wqkv_hs, t1a);
+        if (rg) aq.a_rows = aq.m_rows = dT25;
         LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, prec), "qkv");
-        rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
+        rec.mark("qkv", gemm_flops(aq) * rT25, gemm_bytes(aq, false), kname);
         if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, B, T, 3 * H * Dh, s))) return rc;
         const Act atta = new_act(nmf("xf%d.att", l));
         // fp16-plane attention in f16x3 mode (also for the no-plane long clips: the same arithmetic as their
         // prefixes); true fp32 in f32 mode and the bf16 modes
         const bool ah16 = prec == PREC_F16X3;
         LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh), s,
-                                    w.att, nact, ns, atta.scale, atta.amax, ah16),
+                                    w.att, nact, ns, atta.scale, atta.amax, ah16, rg ? dT25 : nullptr,
+                                    rg ? rg->maxT25 : 0, rg ? rg->minT25 : 0),
                    "attention");
         rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4,
                  ah16 ? (T <= 256 ? "mimi::attention_t256_h16_kernel" : "mimi::attention_band_h16_kernel")
@@ -1407,12 +1504,13 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         ao.scale = x.ls1;
         if (ns) planes_in(ao, w.att, nact);
         use_h(ao, x.wo_h, x.wo_hs, atta);
+        per_item(ao, T, H * Dh, Hd, dT25);
         LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
-        rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
+        rec.mark("o_proj", gemm_flops(ao) * rT25, gemm_bytes(ao, true), kname);
         if ((rc = save_tap(e, nmf("oproj%d", l).c_str(), w.t0, B, T, Hd, s))) return rc;
         const Act t1b = new_act(nmf("xf%d.ln2", l));
         LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1b.scale,
-                                    t1b.amax),
+                                    t1b.amax, rg ? dT25 : nullptr, (int)T),
                    "ln2");
         rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
         GemmArgs a1 = linear_args(w.t1, rows, Hd, x.w1, c.intermediate_size, w.ff);
@@ -1427,8 +1525,9 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             ffa = new_act(nmf("xf%d.ff", l));
             out_act(a1, ffa);
         }
+        per_item(a1, T, Hd, c.intermediate_size, dT25);
         LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, prec), "fc1");
-        rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
+        rec.mark("fc1", gemm_flops(a1) * rT25, gemm_bytes(a1, false), kname);
         if ((rc = save_tap_planes(e, nmf("ff%d", l).c_str(), w.ff, ns, B, T, c.intermediate_size, s, ffa.scale)))
             return rc;
         GemmArgs a2 = linear_args(w.ff, rows, c.intermediate_size, x.w2, Hd, w.t0);
@@ -1443,8 +1542,9 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             dsin = new_act("ds.in");
             out_act(a2, dsin);
         }
+        per_item(a2, T, c.intermediate_size, Hd, dT25);
         LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname, prec), "fc2");
-        rec.mark("fc2", gemm_flops(a2), gemm_bytes(a2, true), kname);
+        rec.mark("fc2", gemm_flops(a2) * rT25, gemm_bytes(a2, true), kname);
         snprintf(nm, sizeof nm, "xfmr%d", l);
         if ((rc = save_tap(e, nm, w.t0, B, T, Hd, s))) return rc;
     }
@@ -1460,12 +1560,18 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         dsouta = new_act("ds.out");
         out_act(ad, dsouta);
     }
+    if (rg) {
+        if (!ds_planes) return set_err(MIMI_ERR_UNSUPPORTED, "ragged: planes downsample only");
+        ad.a_rows = dT25;
+        ad.m_rows = dF;
+    }
     LAUNCH_TRY(launch_gemm(ROLE_DOWNSAMPLE, ad, s, &kname, prec), "downsample");
     if (ds_planes)
         LAUNCH_TRY(launch_ds_edge_fix(w.t0, e->ds_fix, w.dsout, w.att, ad.c_pstride, dsouta.scale, dsouta.amax, B,
-                                      (int)T, (int)T2, Hd, Hd, s),
+                                      (int)T, (int)T2, Hd, Hd, s, rg ? dT25 : nullptr, rg ? dF : nullptr),
                    "downsample edges");
-    rec.mark("downsample", gemm_flops(ad), gemm_bytes(ad, false), kname);
+    const double rF = rows_of(6, (double)B * T2) / ((double)B * T2);
+    rec.mark("downsample", gemm_flops(ad) * rF, gemm_bytes(ad, false), kname);
     if ((rc = save_tap(e, "downsample", w.dsout, B, T2, Hd, s))) return rc;
     const int Dq = c.vq_hidden_dim;
     GemmArgs ap = linear_args(w.dsout, (int64_t)B * T2, Hd, e->inproj, 2 * Dq, w.proj);
@@ -1473,10 +1579,11 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         planes_in(ap, w.att, (long long)B * T2 * Hd);
         use_h(ap, e->inproj_h, e->inproj_hs, dsouta);
     }
+    per_item(ap, T2, Hd, 2 * Dq, dF);
     LAUNCH_TRY(launch_gemm(ROLE_INPROJ, ap, s, &kname, ds_planes ? PREC_F16X3 : PREC_F32), "input_proj");
-    rec.mark("input_proj", gemm_flops(ap), gemm_bytes(ap, false), kname);
+    rec.mark("input_proj", gemm_flops(ap) * rF, gemm_bytes(ap, false), kname);
     if ((rc = save_tap(e, "proj", w.proj, B, T2, 2 * Dq, s))) return rc;
-    if ((rc = run_rvq(e, w.proj, (int64_t)B * T2, K, codes, (int)T2, w.rvq, s, rec))) return rc;
+    if ((rc = run_rvq(e, w.proj, (int64_t)B * T2, K, codes, (int)T2, w.rvq, s, rec, rg ? dF : nullptr, rF))) return rc;
     if (!e->capturing) HIP_TRY(hipEventRecord(e->ws_free, s));
     return MIMI_OK;
 }
@@ -1637,6 +1744,43 @@ static int overflow_fallback(mimi_engine* e, const float* audio, int B, int64_t 
     return MIMI_OK;
 }
 
+// Ragged batch, item by item (each alone at its own length: the definition of the ragged result): the f16x3
+// overflow fallback of a ragged encode, and the whole ragged encode where the batched form does not apply
+// (precision modes other than f16x3, clips too long for the plane buffers).  Item b's codes go to
+// codes[b][k][0 .. F_b) of the [B][K][Fmax] output.  Synchronises s.
+static int ragged_item_by_item(mimi_engine* e, const float* audio, int B, int64_t L, const int64_t* lens, int K,
+                               int32_t* codes, hipStream_t s, int prec) {
+    const int64_t Fmax = plan_lengths(e->cfg, L).frames12;
+    const size_t per = (size_t)K * Fmax;
+    if (e->item_codes_cap < per) {
+        HIP_TRY(hipStreamSynchronize(s));
+        if (e->item_codes) HIP_TRY(hipFree(e->item_codes));
+        e->item_codes = nullptr;
+        e->item_codes_cap = 0;
+        HIP_TRY(hipMalloc(&e->item_codes, per * sizeof(int32_t)));
+        e->item_codes_cap = per;
+    }
+    int rc;
+    for (int b = 0; b < B; ++b) {
+        const float* ab = audio + (int64_t)b * L;
+        const int64_t Fb = plan_lengths(e->cfg, lens[b]).frames12;
+        if (prec == PREC_F16X3 && act_planes(e, plan_lengths(e->cfg, lens[b]), prec) == 2) {
+            bool ovf = false;
+            if ((rc = f16_pass(e, ab, 1, lens[b], K, e->item_codes, s, &ovf))) return rc;
+            if (ovf) {
+                ++e->f16_reruns;
+                if ((rc = encode_pass(e, ab, 1, lens[b], K, e->item_codes, s, PREC_BF16X6))) return rc;
+            }
+        } else if ((rc = encode_pass(e, ab, 1, lens[b], K, e->item_codes, s, prec))) {
+            return rc;
+        }
+        HIP_TRY(hipMemcpy2DAsync(codes + (int64_t)b * K * Fmax, Fmax * sizeof(int32_t), e->item_codes,
+                                 Fb * sizeof(int32_t), Fb * sizeof(int32_t), K, hipMemcpyDeviceToDevice, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return MIMI_OK;
+}
+
 // ---- hipGraph replay (f16x3).  A small batch is launch-bound: ~80 kernels per encode, each a few
 // microseconds of GPU time.  The second encode of a (batch, length, K) shape captures the whole pass -- the
 // maxima reset, every kernel, the maxima fold -- into a graph on a private stream; later encodes of that shape
@@ -1754,7 +1898,7 @@ static int graph_encode(mimi_engine* e, const float* audio, int B, int64_t L, in
 // Enqueues one encode on s and returns its ticket without waiting.  In f16x3 the per-tensor maxima are folded
 // and copied to this ticket's pinned slot behind the encode; mimi_encode_wait checks them.
 static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes,
-                               hipStream_t s, int64_t* ticket) {
+                               hipStream_t s, int64_t* ticket, const int64_t* lengths = nullptr) {
     mimi_engine::Pending* P = nullptr;
     for (auto& q : e->pend)
         if (q.id == 0) {
@@ -1770,15 +1914,57 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
     int rc;
     int n = 0;
     if (h16 && !e->calibrated && (rc = calibrate_scales(e))) return rc;
+    RaggedTable rt;
+    if (lengths) {
+        const mimi_config& c = e->cfg;
+        const bool batched = h16 && e->res0_h16 && e->res1_h16 && e->ds_fix && e->inproj_h &&
+                             c.downsample_kernel == 4 && c.downsample_stride == 2 && c.num_ratios >= 2;
+        if (!batched) {  // item by item, synchronously (the ticket's event is then already complete)
+            if ((rc = ragged_item_by_item(e, audio, B, L, lengths, K, codes, s, prec))) return rc;
+            HIP_TRY(hipEventRecord(P->done, s));
+            P->nslots = 0;
+            P->h16 = false;
+            P->ragged = false;
+            P->audio = audio;
+            P->B = B;
+            P->L = L;
+            P->K = K;
+            P->codes = codes;
+            P->s = s;
+            P->claimed = false;
+            P->id = e->next_ticket++;
+            *ticket = P->id;
+            return MIMI_OK;
+        }
+        rt.B = B;
+        rt.len.assign(lengths, lengths + B);
+        rt.plan.resize(B);
+        for (int b = 0; b < B; ++b) rt.plan[b] = plan_lengths(c, lengths[b]);
+        rt.minT25 = rt.maxT25 = (int)rt.plan[0].frames25;
+        for (const auto& pb : rt.plan) {
+            rt.minT25 = std::min<int>(rt.minT25, (int)pb.frames25);
+            rt.maxT25 = std::max<int>(rt.maxT25, (int)pb.frames25);
+        }
+        const size_t need = RaggedTable::ints(B) * sizeof(int);
+        if (P->rg_cap < need) {
+            if (P->rg_pinned) HIP_TRY(hipHostFree(P->rg_pinned));
+            P->rg_pinned = nullptr;
+            P->rg_cap = 0;
+            HIP_TRY(hipHostMalloc(&P->rg_pinned, need, hipHostMallocDefault));
+            P->rg_cap = need;
+        }
+        rt.fill(P->rg_pinned);
+    }
     if (h16) {
         bool replayed = false;
-        if ((rc = graph_encode(e, audio, B, L, K, codes, s, &replayed))) return rc;
+        if (!lengths && (rc = graph_encode(e, audio, B, L, K, codes, s, &replayed))) return rc;
         n = (int)e->slot_of.size();
         if (!replayed) {
             HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));  // the maxima buffers are part of the workspace
             HIP_TRY(hipMemsetAsync(e->amax_dev, 0, (size_t)kMaxActSlots * AMAX_SLOT_WORDS * sizeof(unsigned), s));
             e->uncalibrated_slot = false;
-            if ((rc = encode_pass(e, audio, B, L, K, codes, s, PREC_F16X3))) return rc;
+            if ((rc = encode_pass(e, audio, B, L, K, codes, s, PREC_F16X3, lengths ? &rt : nullptr, P->rg_pinned)))
+                return rc;
             if (e->uncalibrated_slot) {  // this encode only: the next one starts clean
                 e->uncalibrated_slot = false;
                 return set_err(MIMI_ERR_STATE, "f16x3: an activation has no calibrated scale");
@@ -1799,6 +1985,8 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
     P->K = K;
     P->codes = codes;
     P->s = s;
+    P->ragged = lengths != nullptr;
+    if (lengths) P->lens.assign(lengths, lengths + B);
     P->claimed = false;
     P->id = e->next_ticket++;
     *ticket = P->id;
@@ -1843,6 +2031,10 @@ static int encode_wait(mimi_engine* e, int64_t ticket) {
                        hipGetErrorString(se));
     if (!ovf) return MIMI_OK;
     HIP_TRY(hipSetDevice(e->device));
+    if (q.ragged) {  // each item alone at its own length (the ragged result's definition), bf16x6 if it overflows
+        ++e->f16_reruns;
+        return ragged_item_by_item(e, q.audio, q.B, q.L, q.lens.data(), q.K, q.codes, q.s, PREC_F16X3);
+    }
     return overflow_fallback(e, q.audio, q.B, q.L, q.K, q.codes, q.s);
 }
 
@@ -1876,6 +2068,36 @@ extern "C" int mimi_encode_async(mimi_engine* e, const float* audio, int32_t bat
     HIP_TRY(hipSetDevice(e->device));
     (void)hipGetLastError();  // a failure left by an unrelated earlier call must not fail this encode's launches
     return encode_async_locked(e, audio, batch, length, K, codes, reinterpret_cast<hipStream_t>(stream), ticket);
+}
+
+static int check_ragged(mimi_engine* e, const int64_t* lengths, int32_t batch, int64_t max_length) {
+    if (!lengths) return set_err(MIMI_ERR_INVALID_ARGUMENT, "lengths is NULL");
+    for (int b = 0; b < batch; ++b)
+        if (lengths[b] < 1 || lengths[b] > max_length)
+            return set_err(MIMI_ERR_INVALID_ARGUMENT, "lengths[%d] = %lld outside [1, %lld]", b, (long long)lengths[b],
+                           (long long)max_length);
+    (void)e;
+    return MIMI_OK;
+}
+
+extern "C" int mimi_encode_ragged_async(mimi_engine* e, const float* audio, const int64_t* lengths, int32_t batch,
+                                        int64_t max_length, int32_t K, int32_t* codes, void* stream, int64_t* ticket) {
+    int rc = check_encode_args(e, audio, batch, max_length, &K, codes);
+    if (rc || (rc = check_ragged(e, lengths, batch, max_length))) return rc;
+    if (!ticket) return set_err(MIMI_ERR_INVALID_ARGUMENT, "ticket is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    (void)hipGetLastError();
+    return encode_async_locked(e, audio, batch, max_length, K, codes, reinterpret_cast<hipStream_t>(stream), ticket,
+                               lengths);
+}
+
+extern "C" int mimi_encode_ragged(mimi_engine* e, const float* audio, const int64_t* lengths, int32_t batch,
+                                  int64_t max_length, int32_t K, int32_t* codes, void* stream) {
+    int64_t ticket = 0;
+    const int rc = mimi_encode_ragged_async(e, audio, lengths, batch, max_length, K, codes, stream, &ticket);
+    if (rc) return rc;
+    return encode_wait(e, ticket);
 }
 
 extern "C" int mimi_encode_wait(mimi_engine* e, int64_t ticket) {
@@ -1948,6 +2170,7 @@ extern "C" void mimi_destroy(mimi_engine* e) {
     for (auto& q : e->pend) {
         if (q.done) (void)hipEventDestroy(q.done);
         if (q.amax) (void)hipHostFree(q.amax);
+        if (q.rg_pinned) (void)hipHostFree(q.rg_pinned);
     }
     drop_graphs(e);
     if (e->io_dev) (void)hipFree(e->io_dev);

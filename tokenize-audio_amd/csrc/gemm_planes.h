@@ -160,6 +160,18 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     const int ntiles = MT * NTn * p.batch;
     float omx = 0.0f;  // max|planes value| (fp16 planes: the engine's range check), over this workgroup's tiles
     const int KT = K / BK / NB;
+    // ragged batches: a tile whose first row lies past its item's valid rows does nothing (no loads, MFMAs or
+    // stores); loaders and compute waves skip the same tiles, so they keep meeting at the same barriers
+    auto next_tile = [&](int t) {
+        if (p.m_rows) {
+            for (; t < ntiles; t += (int)gridDim.x) {
+                const int lg = xcd_remap(t, ntiles), rest = lg / NTn;
+                if ((rest % MT) * BM < p.m_rows[rest / MT]) break;
+            }
+        }
+        return t;
+    };
+    auto a_len_of = [&](int b) { return p.a_rows ? (long long)p.a_rows[b] * p.a_cin : p.a_len; };
 
     if constexpr (LW > 0) {
         // Warp-specialised: the loading waves run their own tile loop, meeting the compute waves at the same
@@ -187,7 +199,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                     const __bf16* __restrict__ Abase = reinterpret_cast<const __bf16*>(p.Ap) + (long long)b * p.a_bstride;
 #pragma unroll
                     for (int pl = 0; pl < NS; ++pl)
-                        arsrc[pl] = make_rsrc(Abase + (long long)pl * p.a_pstride, p.a_len * 2);
+                        arsrc[pl] = make_rsrc(Abase + (long long)pl * p.a_pstride, a_len_of(b) * 2);
                     a_lane = (int)((p.a_off + (long long)(m0 + prow) * p.a_rs + c * 8) * 2);
                     b_lane = ((n0 + prow) * K + c * 8) * 2;
                     ko.init(p, PAIR);
@@ -222,8 +234,9 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                     for (int s2 = 0; s2 < STAGES - KG; ++s2)
                         if (s2 < KT) issue_w(s2);
                 };
-                if ((int)blockIdx.x < ntiles) prologue(blockIdx.x);
-                for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+                const int first = next_tile((int)blockIdx.x);
+                if (first < ntiles) prologue(first);
+                for (int tile = first; tile < ntiles;) {
                     for (int kt = 0; kt < KT; kt += KG) {
                         const int ng = min(KG, KT - kt);
                         wait_stages<PW, STAGES - 2 * KG>(min(KT, kt + STAGES - KG) - (kt + ng));
@@ -235,13 +248,14 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                         }
                     }
                     __syncthreads();  // the compute waves' epilogue starts (the ring is free)
-                    const int next = tile + (int)gridDim.x;
+                    const int next = next_tile(tile + (int)gridDim.x);
                     if (PF && next < ntiles) prologue(next);  // lands in slots [0, STAGES - KG) under the epilogue
                     if (FL & FL_PERSIST) {
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                         __builtin_amdgcn_s_barrier();
                     }
                     if (!PF && next < ntiles) prologue(next);
+                    tile = next;
                 }
             };
             static_assert(LW <= 8, "loader waves");
@@ -259,7 +273,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         }
     }
 
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (int tile = next_tile((int)blockIdx.x); tile < ntiles; tile = next_tile(tile + (int)gridDim.x)) {
     const int logical = xcd_remap(tile, ntiles);
     const int nt = logical % NTn;
     const int rest = logical / NTn;
@@ -272,7 +286,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     const __bf16* __restrict__ Abase = reinterpret_cast<const __bf16*>(p.Ap) + (long long)b * p.a_bstride;
     __amdgpu_buffer_rsrc_t arsrc[NS];
 #pragma unroll
-    for (int pl = 0; pl < NS; ++pl) arsrc[pl] = make_rsrc(Abase + (long long)pl * p.a_pstride, p.a_len * 2);
+    for (int pl = 0; pl < NS; ++pl) arsrc[pl] = make_rsrc(Abase + (long long)pl * p.a_pstride, a_len_of(b) * 2);
     // per piece slot q of this wave: piece j = ldw + q * NLD (wave-uniform), its LDS destination within a stage
     // (elements) and this lane's source: a byte offset into A plane pl (may be negative or past the end: the
     // buffer range check loads 0 -- the causal padding) or an element offset into the weight planes.
@@ -446,6 +460,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     const int rbase = m0 + wm * RW;
     const int cbase = n0 + wn * CW + (lane & (MF - 1));
     const float us = F16 ? p.unscale : 1.0f;  // 1 / (activation scale x weight scale): exact power of two
+    const int Mb = p.m_rows ? min(M, p.m_rows[b]) : M;  // this item's valid output rows
 #pragma unroll
     for (int jh = 0; jh < JH; ++jh) {
 #pragma unroll
@@ -463,7 +478,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
             for (int r = 0; r < NACC; ++r) {
                 const int lrow = MF == 32 ? i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel : i * 16 + 4 * hsel + r;
                 const int row = rbase + lrow;
-                const bool ok = row < M && col < N;
+                const bool ok = row < Mb && col < N;
                 float v = F16 ? acc[i][j][r] * us : acc[i][j][r];
                 if (EPI == EPI_BIAS || EPI == EPI_BIAS_OUT) {
                     v = v + bias;
@@ -507,7 +522,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc);
         f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc + 4);
         const int row = m0 + wm * RW + lr, col = n0 + wn * CW + jh * CWC + lc;
-        if (row >= M || col >= N) continue;  // N % 8 == 0: a lane's 8 columns are all in or all out
+        if (row >= Mb || col >= N) continue;  // N % 8 == 0: a lane's 8 columns are all in or all out
         const long long off = (long long)row * p.ldc + col;
         if (EPI == EPI_BIAS_RES_ELU || EPI == EPI_SCALE_RES) {
             const f32x4 r0 = *reinterpret_cast<const f32x4*>(Rb + off);

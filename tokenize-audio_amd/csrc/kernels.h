@@ -164,6 +164,11 @@ struct GemmArgs {
     float unscale;
     float out_scale;
     unsigned* out_amax;
+    // ragged batches (mimi_encode_ragged): per-item valid rows of the A input (rows past a_rows[b] read as 0, the
+    // item's own extra padding: a_len = a_rows[b] * a_cin) and of the output (tiles from m_rows[b] on are skipped,
+    // rows past it are neither stored nor in max|out|); null = every item has M rows / a_len elements
+    const int* a_rows;
+    const int* m_rows;
 };
 
 // Launch the GEMM for a given conv/linear role (the role picks tile shape and template flags).
@@ -222,6 +227,10 @@ struct ResArgs {
     float ascale, xscale, hscale;     // audio (conv0 input), ELU(x) (conv3 input), ELU(h) (conv1 input)
     float unscale0, unscale1, unscale2;
     unsigned *aamax, *xamax, *hamax;
+    // ragged batches (fp16 blocks): item b has ilen[b] steps (T is then the row stride); istart[b] = the item's first
+    // 32-step tile in the concatenation of every item's tiles (istart[batch] = their count); null = uniform T
+    const int* ilen;
+    const unsigned* istart;
 };
 hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** kname);
 
@@ -235,22 +244,28 @@ hipError_t launch_conv0(const float* x, long long L, int batch, const float* w /
                         const float* b, float* y, int cout, int ksize, hipStream_t s);
 
 // LayerNorm over the last dim (C = 512) of rows; output fp32 (yns == 0) or yns bf16 planes.
+// row_len (ragged batches): row r belongs to item r / row_T at step r % row_T and is skipped past row_len[item]
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* y, long long rows,
                             int C, float eps, hipStream_t s, void* yp = nullptr, long long y_pstride = 0,
-                            int yns = 0, float yscale = 0.0f, unsigned* yamax = nullptr);
+                            int yns = 0, float yscale = 0.0f, unsigned* yamax = nullptr, const int* row_len = nullptr,
+                            int row_T = 0);
 
 // Sliding-window causal attention on the fused qkv tensor [B][T][3*H*D] (q, k already rotated);
 // output [B][T][H*D].  h16: the fp16-plane kernels (PREC_F16X3; T <= 256 needs fp16-plane output), else fp32.
+// tlen (ragged batches, h16 only): item b has tlen[b] frames (T is the row stride); each item runs the kernel it
+// would run alone (tlen[b] <= 256: attention_t256_h16_kernel, else the banded one)
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window,
                             float scale, hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
-                            unsigned* oamax, bool h16);
+                            unsigned* oamax, bool h16, const int* tlen = nullptr, int max_tlen = 0, int min_tlen = 0);
 
 // Replicate-padding fix of the downsample conv (k = 4, s = 2) run as a zero-padded planes GEMM: per item,
 // out[0] += (W_0 + W_1) . x[0] (the 2 left pad rows replicate x[0]) and, when T is odd (one right "extra" pad
 // row), out[F-1] += W_3 . x[T-1]; the fixed rows are re-written as fp32 and as fp16 planes of out * oscale.
 // wfix: fp32 [2][C][N] (W_0 + W_1, W_3, input channel major); x: fp32 [B][T][C]; out: fp32 [B][F][N].
+// tlen / flen (ragged batches): per-item T and F (T, F are then the row strides)
 hipError_t launch_ds_edge_fix(const float* x, const float* wfix, float* out, void* outp, long long out_pstride,
-                              float oscale, unsigned* oamax, int B, int T, int F, int C, int N, hipStream_t s);
+                              float oscale, unsigned* oamax, int B, int T, int F, int C, int N, hipStream_t s,
+                              const int* tlen = nullptr, const int* flen = nullptr);
 
 // the banded fp16-plane attention at any T (tools/attn_check.hip compares it with the T <= 256 kernel)
 hipError_t launch_attention_band(const float* qkv, int batch, int T, int H, int window, float scale,
@@ -284,6 +299,8 @@ struct RvqArgs {
     int frames_per_item;    // T (for [b][level][t] output); 0 -> [level][frame]
     void* work;             // rvq_work_bytes(frames): residual ping-pong + per-slice partial argmins
     int sem_split;          // (set by launch_rvq) semantic + first acoustic level in one launch
+    const int* flen;        // ragged batches: item b's valid frames (frame f of item f / frames_per_item); the
+                            // others read a zero projection and their codes are unspecified.  null: all valid
 };
 size_t rvq_work_bytes(long long frames);
 hipError_t launch_rvq(const RvqArgs& a, hipStream_t s, const char** kname = nullptr);  // kname: the level kernel's symbol

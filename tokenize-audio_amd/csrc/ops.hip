@@ -76,7 +76,8 @@ __global__ __launch_bounds__(512) void layernorm_kernel(const float* __restrict_
                                                         const float* __restrict__ bta, float* __restrict__ y,
                                                         long long rows, float eps, __bf16* __restrict__ yp,
                                                         long long pstride, int yns, float yscale,
-                                                        unsigned* __restrict__ yamax) {
+                                                        unsigned* __restrict__ yamax, const int* __restrict__ row_len,
+                                                        int row_T) {
     constexpr int PER = C / 64;  // floats per lane
     static_assert(PER % 4 == 0, "C multiple of 256");
     const int lane = threadIdx.x & 63;
@@ -105,6 +106,7 @@ __global__ __launch_bounds__(512) void layernorm_kernel(const float* __restrict_
     for (int rr = 0; rr < RPW; ++rr) {
     const long long row = row0 + rr;
     if (row >= rows) break;
+    if (row_len && row % row_T >= row_len[row / row_T]) continue;  // ragged: past the item's frames
     float (&v)[PER] = vr[rr];
     float s = 0.f;
 #pragma unroll
@@ -163,12 +165,13 @@ __global__ __launch_bounds__(512) void layernorm_kernel(const float* __restrict_
 
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* y, long long rows, int C,
                             float eps, hipStream_t s, void* yp, long long y_pstride, int yns, float yscale,
-                            unsigned* yamax) {
+                            unsigned* yamax, const int* row_len, int row_T) {
+    if (row_len && row_T <= 0) return hipErrorInvalidValue;
     if (C != 512 || (yns != 0 && !yp) || (yscale > 0.0f && yns != 2)) return hipErrorInvalidValue;
     constexpr int RPW = 2;  // 16 rows per workgroup
     hipLaunchKernelGGL((layernorm_kernel<512, RPW>), dim3((unsigned)((rows + 8 * RPW - 1) / (8 * RPW))), dim3(512), 0, s,
                        x, g, b, y,
-                       rows, eps, reinterpret_cast<__bf16*>(yp), y_pstride, yns, yscale, yamax);
+                       rows, eps, reinterpret_cast<__bf16*>(yp), y_pstride, yns, yscale, yamax, row_len, row_T);
     return hipGetLastError();
 }
 
@@ -529,10 +532,11 @@ __device__ __forceinline__ int vt_key_pos(int r) {
     return (r & ~15) + 8 * ((k >> 2) & 1) + (k & 3) + 4 * ((k >> 3) & 1);
 }
 
-__global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __restrict__ qkv, int T, int H,
+__global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __restrict__ qkv, int Ts, int H,
                                                                  int window, float scale, void* __restrict__ outp,
                                                                  long long pstride, float oscale,
-                                                                 unsigned* __restrict__ oamax) {
+                                                                 unsigned* __restrict__ oamax,
+                                                                 const int* __restrict__ tlen) {
     constexpr int D = 64, TM = 256, LDO = D + 1;
     constexpr int KLD = 72, KPL = TM * KLD;  // K planes: [256][72 halves]
     constexpr int VLD = 264, VPL = D * VLD;  // V^T planes: [64][264 halves]
@@ -541,11 +545,15 @@ __global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __
     _Float16* Ks = lds;
     _Float16* Vt = lds + 2 * KPL;
     const int h = blockIdx.x, b = blockIdx.y;
+    // Ts: the row stride; T: this item's frames (ragged batches: its own, and items over 256 frames run the banded
+    // kernel instead -- what they would run alone)
+    const int T = tlen ? tlen[b] : Ts;
+    if (T > TM) return;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hf = lane >> 5, col = lane & 31;
     const long long ld = 3LL * H * D;
-    const float* base = qkv + (long long)b * T * ld;
+    const float* base = qkv + (long long)b * Ts * ld;
     // K / V rows 0 .. 255 (zeros past T) -> registers, head max |K|, |V|
     constexpr int PER = TM * (D / 4) / 512;  // 8
     f32x4 kv[PER], vv[PER];
@@ -661,7 +669,7 @@ __global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __
     for (int qq = 0; qq < 32; ++qq) {
         const int q = qw + qq;
         if (q < T)
-            store_act(nullptr, outp, pstride, 2, ((long long)b * T + q) * (H * D) + h * D + lane, ow[qq * LDO + lane],
+            store_act(nullptr, outp, pstride, 2, ((long long)b * Ts + q) * (H * D) + h * D + lane, ow[qq * LDO + lane],
                       oscale, &mx);
     }
     amax_commit(oamax, mx);
@@ -676,9 +684,10 @@ __global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __
 // ratio (exact: powers of two, folded into the online-softmax correction) and later smaller-valued chunks put the
 // ratio on P instead (P s <= 2^14).  Every scale depends on this item's own q/k/v only.
 __global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __restrict__ qkv, float* __restrict__ out,
-                                                                 int T, int H, int window, float scale,
+                                                                 int Ts, int H, int window, float scale,
                                                                  void* __restrict__ outp, long long pstride, int outns,
-                                                                 float oscale, unsigned* __restrict__ oamax) {
+                                                                 float oscale, unsigned* __restrict__ oamax,
+                                                                 const int* __restrict__ tlen) {
     constexpr int D = 64, KC = 32, LDO = D + 1;
     constexpr int KLD = 72, KPL = KC * KLD;  // K planes: [32 keys][72 halves] (conflict-free b128 fragment reads)
     constexpr int VLD = 40, VPL = D * VLD;   // V^T planes: [64 dims][40 halves]
@@ -689,12 +698,15 @@ __global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __
     _Float16* Ks = lds;
     _Float16* Vt = lds + 2 * KPL;
     const int b = blockIdx.z, h = blockIdx.y;
+    // Ts: the row stride; T: this item's frames (ragged batches: items of <= 256 frames run the T <= 256 kernel)
+    const int T = tlen ? tlen[b] : Ts;
+    const int q0 = blockIdx.x * 128;
+    if (tlen && (T <= 256 || q0 >= T)) return;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hf = lane >> 5, col = lane & 31;
     const long long ld = 3LL * H * D;
-    const float* base = qkv + (long long)b * T * ld;
-    const int q0 = blockIdx.x * 128;
+    const float* base = qkv + (long long)b * Ts * ld;
     const int qw = q0 + 32 * wave, qi = qw + col;
     const int kstart = max(0, q0 - window + 1) & ~31;
     const int kend = min(T - 1, q0 + 127);        // the workgroup's last key
@@ -820,7 +832,7 @@ __global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __
     for (int qq = 0; qq < 32; ++qq) {
         const int q = qw + qq;
         if (q < T)
-            store_act(out, outp, pstride, outns, ((long long)b * T + q) * (H * D) + h * D + lane,
+            store_act(out, outp, pstride, outns, ((long long)b * Ts + q) * (H * D) + h * D + lane,
                       ow[qq * LDO + lane], oscale, &mx);
     }
     amax_commit(oamax, mx);
@@ -829,24 +841,37 @@ __global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __
 hipError_t launch_attention_band(const float* qkv, int batch, int T, int H, int window, float scale,
                                  hipStream_t s, void* outp, long long out_pstride, float oscale, unsigned* oamax) {
     hipLaunchKernelGGL(attention_band_h16_kernel, dim3((T + 127) / 128, H, batch), dim3(256), 0, s, qkv, nullptr, T, H,
-                       window, scale, outp, out_pstride, 2, oscale, oamax);
+                       window, scale, outp, out_pstride, 2, oscale, oamax, nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window, float scale,
                             hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
-                            unsigned* oamax, bool h16) {
+                            unsigned* oamax, bool h16, const int* tlen, int max_tlen, int min_tlen) {
     if (D != 64 || (outns != 0 && !outp) || (outns == 0 && !out) || (oscale > 0.0f && outns != 2)) return hipErrorInvalidValue;
+    if (tlen) {  // ragged batch: each item the kernel it would run alone (each exits on the other's items)
+        if (!h16 || !(oscale > 0.0f && outns == 2) || max_tlen > T || min_tlen < 1) return hipErrorInvalidValue;
+        if (min_tlen <= 256) {
+            hipLaunchKernelGGL(attention_t256_h16_kernel, dim3(H, batch), dim3(512), 0, s, qkv, T, H, window, scale,
+                               outp, out_pstride, oscale, oamax, tlen);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        if (max_tlen > 256)
+            hipLaunchKernelGGL(attention_band_h16_kernel, dim3((max_tlen + 127) / 128, H, batch), dim3(256), 0, s, qkv,
+                               out, T, H, window, scale, outp, out_pstride, outns, oscale, oamax, tlen);
+        return hipGetLastError();
+    }
     // (the banded kernel at T <= 256 measured slower at B = 1 and B = 32: profiles/r2d_ab_attention_band.log)
     if (h16 && T <= 256) {  // fp16-plane output (the engine's plane path at these lengths)
         if (!(oscale > 0.0f && outns == 2)) return hipErrorInvalidValue;
         hipLaunchKernelGGL(attention_t256_h16_kernel, dim3(H, batch), dim3(512), 0, s, qkv, T, H, window, scale, outp,
-                           out_pstride, oscale, oamax);
+                           out_pstride, oscale, oamax, nullptr);
         return hipGetLastError();
     }
     if (h16) {  // T > 256: fp16-plane output, or fp32 for clips too long for the plane buffers
         hipLaunchKernelGGL(attention_band_h16_kernel, dim3((T + 127) / 128, H, batch), dim3(256), 0, s, qkv, out, T, H,
-                           window, scale, outp, out_pstride, outns, oscale, oamax);
+                           window, scale, outp, out_pstride, outns, oscale, oamax, nullptr);
         return hipGetLastError();
     }
     if (T <= 256) {
@@ -868,8 +893,10 @@ hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void ds_edge_fix_kernel(const float* __restrict__ x, const float* __restrict__ wfix,
                                                           float* __restrict__ out, void* __restrict__ outp,
                                                           long long pstride, float oscale, unsigned* __restrict__ oamax,
-                                                          int T, int F, int C, int N) {
+                                                          int Ts, int Fs, int C, int N, const int* __restrict__ tlen,
+                                                          const int* __restrict__ flen) {
     const int b = blockIdx.x, edge = blockIdx.y;
+    const int T = tlen ? tlen[b] : Ts, F = flen ? flen[b] : Fs;  // (Ts, Fs: the row strides)
     const bool right = (T & 1) != 0;                 // a right "extra" row exists
     if (edge == 1 && (!right || F == 1)) return;
     const int last_edge = edge == 0 && right && F == 1 ? 1 : edge;
@@ -878,12 +905,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     const int n0 = blockIdx.z * 64;
     const int cs = C / 16, c0 = sl * cs;
     __shared__ float part[16][64];
-    const long long o = ((long long)b * F + f) * N + n0 + (threadIdx.x & 63);
+    const long long o = ((long long)b * Fs + f) * N + n0 + (threadIdx.x & 63);
     float v = threadIdx.x < 64 ? out[o] : 0.0f;
     for (int e = edge; e <= last_edge; ++e) {
         const int t = e == 0 ? 0 : T - 1;
         const float* __restrict__ wc = wfix + (long long)e * C * N + n0 + 4 * g;  // [edge][c][n]
-        const float* __restrict__ xr = x + ((long long)b * T + t) * C;
+        const float* __restrict__ xr = x + ((long long)b * Ts + t) * C;
         f32x4 a = {0.f, 0.f, 0.f, 0.f};
         // 16 channels per round: all 20 loads issued before the first FMA (a plain loop let the compiler wait out
         // each load's latency in turn: 13.8 us per launch at any batch); same FMA order as the plain loop
@@ -922,10 +949,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     if (outp) amax_commit(oamax, mx);
 }
 hipError_t launch_ds_edge_fix(const float* x, const float* wfix, float* out, void* outp, long long out_pstride,
-                              float oscale, unsigned* oamax, int B, int T, int F, int C, int N, hipStream_t s) {
-    if (B <= 0 || T <= 0 || F <= 0 || N % 64 || C % 256 || (outp && !(oscale > 0.0f))) return hipErrorInvalidValue;
+                              float oscale, unsigned* oamax, int B, int T, int F, int C, int N, hipStream_t s,
+                              const int* tlen, const int* flen) {
+    if (B <= 0 || T <= 0 || F <= 0 || N % 64 || C % 256 || (outp && !(oscale > 0.0f)) || (!tlen != !flen))
+        return hipErrorInvalidValue;
     hipLaunchKernelGGL(ds_edge_fix_kernel, dim3(B, 2, N / 64), dim3(256), 0, s, x, wfix, out, outp, out_pstride,
-                       oscale, oamax, T, F, C, N);
+                       oscale, oamax, T, F, C, N, tlen, flen);
     return hipGetLastError();
 }
 
@@ -1056,6 +1085,14 @@ __device__ __forceinline__ RvqWork rvq_work(const RvqArgs& p, int nsl) {
     return r;
 }
 
+// frame f holds data: inside the frames and, for a ragged batch, inside its item's valid frames
+__device__ __forceinline__ bool rvq_valid(const RvqArgs& p, long long f) {
+    if (f >= p.frames) return false;
+    if (!p.flen) return true;
+    const long long bb = f / p.frames_per_item;
+    return f - bb * p.frames_per_item < p.flen[bb];
+}
+
 __device__ __forceinline__ void rvq_store_code(const RvqArgs& p, int level, long long f, int ix) {
     int32_t* codes = io_pointer(p.codes_ref, p.codes);
     if (p.frames_per_item > 0) {
@@ -1130,7 +1167,7 @@ __global__ __launch_bounds__(512) void rvq_level_kernel(RvqArgs p, int L) {
         const int i = idx / (D / 4), k = (idx % (D / 4)) * 4;
         const long long f = f0 + i;
         f32x4 r = {0.f, 0.f, 0.f, 0.f};
-        if (f < p.frames) {
+        if (rvq_valid(p, f)) {
             if (fresh) {
                 r = *reinterpret_cast<const f32x4*>(p.proj + f * (2 * D) + coff + k);
             } else {
@@ -1304,7 +1341,7 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
         const int i = idx / (D / 4), k = (idx % (D / 4)) * 4;
         const long long f = f0 + i;
         f32x4 r = {0.f, 0.f, 0.f, 0.f};
-        if (f < p.frames) {
+        if (rvq_valid(p, f)) {
             if (fresh) {
                 r = *reinterpret_cast<const f32x4*>(p.proj + f * (2 * D) + coff + k);
             } else {

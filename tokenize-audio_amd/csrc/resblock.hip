@@ -572,6 +572,32 @@ __device__ __forceinline__ void elu_s4(const float (&z)[4], float s, float (&t)[
     }
 }
 
+// The persistent fp16 blocks' walk over 32-step tiles: the items' tiles concatenated (uniform: tpi per item;
+// ragged: item b's ceil(ilen[b] / 32) tiles from istart[b]), a wave / workgroup taking a contiguous range of them.
+struct TileWalk {
+    const ResArgs& p;
+    unsigned tpi;
+    unsigned b = 0;
+    long long t0 = 0;
+    __device__ TileWalk(const ResArgs& pa, unsigned tiles_per_item, unsigned g) : p(pa), tpi(tiles_per_item) {
+        if (p.istart) {
+            while (b + 1 < (unsigned)p.batch && p.istart[b + 1] <= g) ++b;
+            t0 = (long long)(g - p.istart[b]) * 32;
+        } else {
+            b = g / tpi;
+            t0 = (long long)(g - b * tpi) * 32;
+        }
+    }
+    __device__ long long len(unsigned bb) const { return p.ilen ? (long long)p.ilen[bb] : p.T; }
+    __device__ void next() {
+        t0 += 32;
+        if (t0 >= len(b)) {
+            ++b;
+            t0 = 0;
+        }
+    }
+};
+
 __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
     using namespace r0h;
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
@@ -596,23 +622,25 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
     _Float16* hb = slab + 2 * SLD;  // h plane p, row j at hb + p * SPL + j * SLD (after GEMM1)
     float* aud = reinterpret_cast<float*>(slab + 2 * SPL);
 
-    const long long T = p.T;
+    const long long T = p.T;  // row stride of the audio / y (and every item's length unless ragged)
     const float* __restrict__ audio = io_pointer(p.audio_ref, p.audio);
     const unsigned tpi = (unsigned)((T + 31) >> 5);  // tiles per item (host checks B x tpi < 2^32)
-    const unsigned long long NT = (unsigned long long)tpi * p.batch;
+    const unsigned long long NT = p.istart ? p.istart[p.batch] : (unsigned long long)tpi * p.batch;
     const unsigned long long W = (unsigned long long)gridDim.x * NW;
     const unsigned long long wid = (unsigned long long)blockIdx.x * NW + wave;
     const unsigned g0 = (unsigned)(wid * NT / W), g1 = (unsigned)((wid + 1) * NT / W);
+    // tile g -> (item, first step): items' tiles concatenated (ragged: istart), walked in order from g0
+    TileWalk tw(p, tpi, g0);
     const int j = lane & 31, hh = lane >> 5;
     const float sa = p.ascale, sx = p.xscale, sh = p.hscale, sy = p.yscale;
     const float u0 = p.unscale0, u1 = p.unscale1, u2 = p.unscale2;
     float mxa = 0.0f, mxx = 0.0f, mxh = 0.0f, mxy = 0.0f;  // max |audio|, then max |scaled operand|
 
-    // lane's audio-window value of tile gg: audio[t0 - 8 + lane] (lanes < AUD; zero outside [0, T))
-    auto aload = [&](unsigned gg) {
-        const unsigned bb = gg / tpi;
-        const long long pos = (long long)(gg - bb * tpi) * 32 - 8 + lane;
-        return (lane < AUD && pos >= 0 && pos < T) ? audio[(long long)bb * T + pos] : 0.0f;
+    // lane's audio-window value of tile (item bb, step t0): audio[t0 - 8 + lane] (lanes < AUD; zero outside the
+    // item's [0, T_b))
+    auto aload = [&](unsigned bb, long long t0) {
+        const long long pos = t0 - 8 + lane;
+        return (lane < AUD && pos >= 0 && pos < tw.len(bb)) ? audio[(long long)bb * T + pos] : 0.0f;
     };
     // x0^T for the tile's 32 steps (lane column j = step t0 + j) from its audio window value av, + b0
     auto conv0 = [&](float av, f32x16 (&x0)[2]) {
@@ -666,19 +694,21 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
     // 2 slab rows per plane: lane -> (plane, row, 4 halves)
     const int cpl = lane >> 5, crow = (lane >> 4) & 1, cc = (lane & 15) * 4;
 
-    float anext = g0 < g1 ? aload(g0) : 0.0f;
+    float anext = g0 < g1 ? aload(tw.b, tw.t0) : 0.0f;
     for (unsigned g = g0; g < g1; ++g) {
-        const unsigned b = g / tpi;
-        const long long t0 = (long long)(g - b * tpi) * 32;
+        const unsigned b = tw.b;
+        const long long t0 = tw.t0;
+        const long long Tb = tw.len(b);
         if (t0 == 0) {  // causal zero padding of ELU(x0) before t = 0
             *reinterpret_cast<uint2*>(slab + cpl * SPL + crow * SLD + cc) = make_uint2(0u, 0u);
         } else if (g == g0) {  // range start inside an item: halo rows from the preceding tile's conv0
             f32x16 xp[2];
-            conv0(aload(g - 1), xp);
+            conv0(aload(b, t0 - 32), xp);
             slab_put(xp, -30);
         }
         const float acur = anext;
-        if (g + 1 < g1) anext = aload(g + 1);  // the next tile's audio flies under this tile
+        tw.next();
+        if (g + 1 < g1) anext = aload(tw.b, tw.t0);  // the next tile's audio flies under this tile
         f32x16 x0[2];
         conv0(acur, x0);
         slab_put(x0, 2);
@@ -761,7 +791,7 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
                 *reinterpret_cast<uint2*>(hb + o) = hi;
                 *reinterpret_cast<uint2*>(hb + SPL + o) = lo;
             }
-        if (t0 + j < T) mxy = fmaxf(mxy, tmy);  // steps past the end are not stored, not in max|y|
+        if (t0 + j < Tb) mxy = fmaxf(mxy, tmy);  // steps past the end are not stored, not in max|y|
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         {
             const int sr = lane >> 3, sc = (lane & 7) * 8;
@@ -771,7 +801,7 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
                 for (int it = 0; it < 4; ++it) {
                     const int r = it * 8 + sr;
                     const uint4 v = *reinterpret_cast<const uint4*>(hb + pl * SPL + r * SLD + sc);
-                    if (t0 + r < T)
+                    if (t0 + r < Tb)
                         *reinterpret_cast<uint4*>(reinterpret_cast<_Float16*>(p.yp) + pl * p.y_pstride +
                                                   ((long long)b * T + t0 + r) * 64 + sc) = v;
                 }
@@ -843,11 +873,13 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
     }
     const f16x8* wf = reinterpret_cast<const f16x8*>(lds);
 
-    const long long T = p.T;
+    const long long T = p.T;  // row stride of x / y (and every item's length unless ragged)
     const unsigned tpi = (unsigned)((T + BM - 1) / BM);  // blocks per item (host checks B x tpi < 2^32)
-    const unsigned long long NB = (unsigned long long)tpi * p.batch;
+    const unsigned long long NB = p.istart ? p.istart[p.batch] : (unsigned long long)tpi * p.batch;
     const unsigned g0 = (unsigned)((unsigned long long)blockIdx.x * NB / gridDim.x);
     const unsigned g1 = (unsigned)((unsigned long long)(blockIdx.x + 1) * NB / gridDim.x);
+    static_assert(BM == 32, "TileWalk steps 32");
+    TileWalk tw(p, tpi, g0);
     const int li = lane & 15, lq = lane >> 4;
     const int n = wave & 1, mp = wave >> 1;  // N-tile (16 steps), M-tile pair
     const int t = 16 * n + li;                // this lane's step inside a block (E layout)
@@ -855,11 +887,11 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
     const float u1 = p.unscale1, u2 = p.unscale2;
     float mxx = 0.0f, mxh = 0.0f, mxy = 0.0f;
 
-    // x of block g, step t, channels 16(2mp + i) + 4lq .. +3 (zero past T)
-    auto xload = [&](unsigned g, long long off, f32x4 (&xv)[2]) {
-        const unsigned b = g / tpi;
-        const long long row = (long long)(g - b * tpi) * BM + off;
-        const bool ok = row >= 0 && row < T;
+    // x of the block at (item b, step t0), step t0 + off, channels 16(2mp + i) + 4lq .. +3 (zero outside the item's
+    // [0, T_b))
+    auto xload = [&](unsigned b, long long t0b, long long off, f32x4 (&xv)[2]) {
+        const long long row = t0b + off;
+        const bool ok = row >= 0 && row < tw.len(b);
         const float* xr = p.x + ((long long)b * T + (ok ? row : 0)) * C + 4 * lq;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -888,20 +920,22 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
 
     uint2 hhi[2], hlo[2];  // lanes with t >= 30: the halo planes for the next block
     f32x4 xn[2];
-    if (g0 < g1) xload(g0, t, xn);
+    if (g0 < g1) xload(tw.b, tw.t0, t, xn);
     __syncthreads();  // weights and biases resident
     for (unsigned g = g0; g < g1; ++g) {
-        const unsigned b = g / tpi;
-        const long long t0 = (long long)(g - b * tpi) * BM;
+        const unsigned b = tw.b;
+        const long long t0 = tw.t0;
+        const long long Tb = tw.len(b);
         f32x4 xc[2] = {xn[0], xn[1]};
-        if (g + 1 < g1) xload(g + 1, t, xn);  // flies under this block
+        tw.next();
+        if (g + 1 < g1) xload(tw.b, tw.t0, t, xn);  // flies under this block
         // ---- slab: halo rows 0, 1 (lanes t = 30, 31), rows 2 + t
         if (t >= BM - 2) {
             if (t0 == 0) {
                 hhi[0] = hhi[1] = hlo[0] = hlo[1] = make_uint2(0u, 0u);
             } else if (g == g0) {
                 f32x4 xh[2];
-                xload(g, t - BM, xh);  // steps t0 - 2, t0 - 1
+                xload(b, t0, t - BM, xh);  // steps t0 - 2, t0 - 1
                 xsplit(xh, hhi, hlo);
             }
             slab_row_put(t - (BM - 2), hhi, hlo);
@@ -981,7 +1015,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
                 *reinterpret_cast<uint2*>(slab + o) = hi;
                 *reinterpret_cast<uint2*>(slab + SPL + o) = lo;
             }
-            if (t0 + t < T) mxy = fmaxf(mxy, tmy);  // steps past the end are not stored, not in max|y|
+            if (t0 + t < Tb) mxy = fmaxf(mxy, tmy);  // steps past the end are not stored, not in max|y|
         }
         lds_barrier();  // B3: staging complete
         {  // 2 planes x 32 rows x 16 chunks of 16 B = 1024 chunks, 2 per thread
@@ -990,7 +1024,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
                 const int idx = tid + k * NW * 64;
                 const int pl = idx >> 9, r = (idx >> 4) & 31, c = (idx & 15) * 8;
                 const uint4 v = *reinterpret_cast<const uint4*>(slab + pl * SPL + (2 + r) * SLD + c);
-                if (t0 + r < T)
+                if (t0 + r < Tb)
                     *reinterpret_cast<uint4*>(reinterpret_cast<_Float16*>(p.yp) + pl * p.y_pstride +
                                               ((long long)b * T + t0 + r) * C + c) = v;
             }

@@ -10,42 +10,106 @@ in ``libritts-r-mimi/process_libritts_r.py:33-105``, ``yodas2-mimi/process_shard
   single item; otherwise pad-to-longest, ONE encode, trim item i to ``int(ceil(L_i / (sr / 12.5)))``
   frames                                                                                        ``:88-140``
 
+How a padded batch is encoded: item i keeps frames [0, ceil(L_i / 1920)), and every one of them depends only on
+the item's samples below E_i = min(Lmax, 1920 ceil(L_i / 1920)) (every conv is causal, and a length that is a
+multiple of 1920 needs no extra padding at any stage), which are its own samples followed by the batch's zero
+padding.  So the batch runs as ONE ragged encode (``mimi_encode_ragged``) with item i at length E_i: the codes the
+caller keeps are the padded batch's, and the compute the padding would cost is skipped (U[1.5, 20] s YODAS2
+batches: about 45 % of a pad-to-longest encode).  ``ragged=False`` runs the literal padded encode instead.
+
 Added for the per-utterance callers (MLS ``mls-en-mimi-pretrain/process_shard.py:268-307`` and LibriSpeech call
 ``encode_audio_chunk`` once per utterance): ``encode_audio_chunks(list, sr)`` returns exactly
-``[encode_audio_chunk(a, sr) for a in list]`` -- each item encoded alone at its own length, batch 1 -- but runs
-``concurrency`` engines (same weights and calibration, so the same codes) on their own streams from as many host
-threads, so several batch-1 encodes fill the GPU at once.  A driver keeps its per-utterance loop semantics by
-encoding a window of upcoming utterances per call.
+``[encode_audio_chunk(a, sr) for a in list]`` -- each item encoded alone at its own length, bit for bit -- as
+ragged batches of several utterances at once.
 
-The inputs and outputs are the reference's; the data path is leaner.  The reference runs the feature
-extractor and moves ``input_values`` and the int64 ``padding_mask`` (8 B per sample) to the device, although
-the model ignores the mask (``TF/modeling_mimi.py:1244, :1247``).  Here the items are copied straight into a
-zeroed device batch (the same values as the extractor's right padding with 0.0, after its float32 cast), no
-mask is built or moved, and the int32 codes come back to the host before the int64 widening.
+And for shard drivers that can hand over their batches ahead of time (the YODAS2 sub-shard loop,
+``yodas2-mimi/process_shard.py:494-525``): ``encode_batches(batches, sr)`` yields ``encode_audio_batch(b, sr)`` for
+each batch in order, pipelined -- the next batch's host copy into pinned memory and its host->device copy (on a
+copy stream) run while the GPU encodes the current one, and results come back as soon as they are final.
 
 A shard script switches by replacing its ``class MimiEncoder`` with ``from mimi_hip import MimiEncoder``.
 """
 from __future__ import annotations
 
 import logging
-import threading
-from concurrent.futures import ThreadPoolExecutor
-from typing import List, Optional
+import math
+from typing import Iterable, Iterator, List, Optional, Sequence
 
 import numpy as np
 import torch
 
+from .config import encoded_length
 from .feature_extraction import MimiFeatureExtractor
 from .model import MimiHipModel
 
 logger = logging.getLogger(__name__)
+
+FRAME = 1920  # samples per 12.5 Hz frame at 24 kHz (MimiConfig.frame_size)
+
+
+def padded_batch_lengths(lengths: Sequence[int]) -> List[int]:
+    """Per-item encode lengths that reproduce a pad-to-longest batch's kept frames (module docstring)."""
+    lmax = max(lengths)
+    return [min(lmax, FRAME * math.ceil(n / FRAME)) for n in lengths]
+
+
+class _Pipeline:
+    """Double-buffered ragged encodes: pinned host staging -> device on a copy stream -> encode on a compute stream.
+    Slot k's buffers are reused by the (k + depth)-th submit, after the result of the k-th was collected (its
+    encode finished reading them)."""
+
+    def __init__(self, model: MimiHipModel, K: int, depth: int = 2):
+        self.model, self.K, self.depth = model, K, depth
+        self.dev = model.device
+        self.copy = torch.cuda.Stream(device=self.dev)
+        self.comp = torch.cuda.Stream(device=self.dev)
+        self.slots = [dict(pin=None, din=None, out=None) for _ in range(depth)]
+        self.n = 0
+
+    def _buf(self, slot, key, numel, dtype, pinned):
+        b = slot[key]
+        if b is None or b.numel() < numel:
+            b = (torch.empty(numel, dtype=dtype, pin_memory=True) if pinned
+                 else torch.empty(numel, dtype=dtype, device=self.dev))
+            slot[key] = b
+        return b
+
+    def submit(self, arrays: List[np.ndarray], enc_lens: List[int], keep: List[int]):
+        B, L = len(arrays), max(enc_lens)
+        slot = self.slots[self.n % self.depth]
+        self.n += 1
+        pin = self._buf(slot, "pin", B * L, torch.float32, True)[:B * L].view(B, L)
+        pn = pin.numpy()
+        for i, a in enumerate(arrays):  # the item's samples, then zeros up to its encode length (never past it)
+            n = a.shape[0]
+            pn[i, :n] = a
+            if enc_lens[i] > n:
+                pn[i, n:enc_lens[i]] = 0.0
+        din = self._buf(slot, "din", B * L, torch.float32, False)[:B * L].view(B, L)
+        T = encoded_length(L, self.model.config)
+        out = self._buf(slot, "out", B * self.K * T, torch.int32, False)[:B * self.K * T].view(B, self.K, T)
+        with torch.cuda.stream(self.copy):
+            din.copy_(pin, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.copy)
+        self.comp.wait_event(ev)
+        with torch.cuda.stream(self.comp):
+            ticket = self.model.encode_ragged_async(din, enc_lens, self.K, out=out)
+        return ticket, keep
+
+    @staticmethod
+    def collect(handle) -> List[np.ndarray]:
+        ticket, keep = handle
+        codes = ticket.wait().cpu().numpy()  # final once waited (the f16x3 overflow check runs there)
+        return [codes[i, :, :t].astype(np.int64) for i, t in enumerate(keep)]
 
 
 class MimiEncoder:
     """Wrapper for Mimi model encoding (HIP engine)."""
 
     def __init__(self, model_id: str = "kyutai/mimi", device: str = "cuda", model: Optional[MimiHipModel] = None,
-                 num_quantizers: Optional[int] = None, concurrency: int = 1):
+                 num_quantizers: Optional[int] = None, concurrency: int = 1, ragged: bool = True,
+                 chunk_batch: int = 32):
         logger.info(f"Loading Mimi model: {model_id}")
         self.device = device
         self.feature_extractor = MimiFeatureExtractor.from_pretrained(model_id)
@@ -56,10 +120,15 @@ class MimiEncoder:
         # first K levels do not depend on the later ones (split RVQ, TF/modeling_mimi.py:1060-1066), so a
         # caller that only keeps K may set num_quantizers=K for the same result with less work.
         self.num_quantizers = num_quantizers
-        self.concurrency = max(1, int(concurrency))
-        self._lanes = None  # [(engine, stream)] built on the first encode_audio_chunks call
-        self._lanes_lock = threading.Lock()
+        self.concurrency = max(1, int(concurrency))  # (kept for API compatibility; ragged batches replace it)
+        self.ragged = bool(ragged) and hasattr(self.model, "encode_ragged_async")
+        self.chunk_batch = max(1, int(chunk_batch))
+        self._pipe = None
         logger.info("Mimi model loaded successfully")
+
+    @property
+    def _K(self) -> int:
+        return self.num_quantizers or self.model.config.num_quantizers
 
     def _check(self, arrays, sample_rate):
         # the feature extractor's checks and float32 cast (ENC/feature_extraction_encodec.py:130-150)
@@ -93,13 +162,26 @@ class MimiEncoder:
         for i, a in enumerate(arrays):
             if a.shape[0]:
                 x[i, :a.shape[0]].copy_(torch.from_numpy(a))
-        K = self.num_quantizers or self.model.config.num_quantizers
-        return self.model.encode_async(x, K).wait().cpu().numpy()
+        return self.model.encode_async(x, self._K).wait().cpu().numpy()
+
+    def _pipeline(self) -> _Pipeline:
+        if self._pipe is None:
+            self._pipe = _Pipeline(self.model, self._K)
+        return self._pipe
 
     def encode_audio_chunk(self, audio_array: np.ndarray, sample_rate: int = 24000) -> np.ndarray:
         with torch.no_grad():
             (a,) = self._check([audio_array], sample_rate)
             return self._encode_padded([a])[0].astype(np.int64)
+
+    def _batch_plan(self, items: List[np.ndarray], sample_rate: int):
+        if any(a.shape[0] == 0 for a in items):
+            raise ValueError("empty audio")
+        samples_per_frame = sample_rate / 12.5
+        # item i keeps the frames its own samples produce, int(ceil(L_i / samples_per_frame)), of the padded
+        # batch's codes (the reference's trim)
+        keep = [int(np.ceil(len(a) / samples_per_frame)) for a in items]
+        return padded_batch_lengths([len(a) for a in items]), keep
 
     def encode_audio_batch(self, audio_arrays: List[np.ndarray], sample_rate: int = 24000) -> List[np.ndarray]:
         if len(audio_arrays) == 0:
@@ -108,47 +190,63 @@ class MimiEncoder:
             return [self.encode_audio_chunk(audio_arrays[0], sample_rate)]
         with torch.no_grad():
             items = self._check(audio_arrays, sample_rate)
+            if self.ragged:
+                enc_lens, keep = self._batch_plan(items, sample_rate)
+                pipe = self._pipeline()
+                return pipe.collect(pipe.submit(items, enc_lens, keep))
             codes = self._encode_padded(items)
             samples_per_frame = sample_rate / 12.5
-            # item i keeps the frames its own samples produce, int(ceil(L_i / samples_per_frame)), of the padded
-            # batch's codes (the reference's trim)
             return [codes[i, :, :int(np.ceil(len(a) / samples_per_frame))].astype(np.int64)
                     for i, a in enumerate(items)]
 
-    def _get_lanes(self):
-        with self._lanes_lock:
-            if self._lanes is None:
-                engines = [self.model] + [self.model.clone() for _ in range(self.concurrency - 1)]
-                self._lanes = [(e, torch.cuda.Stream(device=e.device)) for e in engines]
-            return self._lanes
+    def encode_batches(self, batches: Iterable[Sequence[np.ndarray]], sample_rate: int = 24000
+                       ) -> Iterator[List[np.ndarray]]:
+        """Yields ``encode_audio_batch(batch, sample_rate)`` for each batch, in order (the same codes), with the next
+        batch's host staging and host->device copy overlapping the current batch's encode."""
+        if not self.ragged:
+            for b in batches:
+                yield self.encode_audio_batch(list(b), sample_rate)
+            return
+        pipe = self._pipeline()
+        pending = None  # (handle, or the finished result of a 0/1-item batch)
+        with torch.no_grad():
+            for b in batches:
+                b = list(b)
+                if len(b) <= 1:
+                    cur = ("done", [self.encode_audio_chunk(b[0], sample_rate)] if b else [])
+                else:
+                    items = self._check(b, sample_rate)
+                    enc_lens, keep = self._batch_plan(items, sample_rate)
+                    cur = ("run", pipe.submit(items, enc_lens, keep))
+                if pending is not None:
+                    yield pending[1] if pending[0] == "done" else pipe.collect(pending[1])
+                pending = cur
+            if pending is not None:
+                yield pending[1] if pending[0] == "done" else pipe.collect(pending[1])
 
     def encode_audio_chunks(self, audio_arrays: List[np.ndarray], sample_rate: int = 24000) -> List[np.ndarray]:
-        """``[self.encode_audio_chunk(a, sample_rate) for a in audio_arrays]``, with ``concurrency`` engines
-        encoding different items at once (item i on lane i mod concurrency, in order within a lane)."""
-        if not hasattr(self.model, "encode_async") or self.concurrency == 1 or len(audio_arrays) <= 1:
+        """``[self.encode_audio_chunk(a, sample_rate) for a in audio_arrays]``, bit for bit: each utterance encoded
+        alone at its own length, as ragged batches of up to ``chunk_batch`` utterances (grouped by length),
+        pipelined."""
+        if not self.ragged or len(audio_arrays) <= 1:
             return [self.encode_audio_chunk(a, sample_rate) for a in audio_arrays]
         items = self._check(audio_arrays, sample_rate)
         if any(a.shape[0] == 0 for a in items):
             raise ValueError("empty audio")
-        lanes = self._get_lanes()
-        K = self.num_quantizers or self.model.config.num_quantizers
+        order = sorted(range(len(items)), key=lambda i: items[i].shape[0])
+        groups = [order[i:i + self.chunk_batch] for i in range(0, len(order), self.chunk_batch)]
         out: List[Optional[np.ndarray]] = [None] * len(items)
-
-        def run(k):  # lane k: its items in order, the next one enqueued before the previous one is waited for
-            engine, stream = lanes[k]
-            pending = None
-            with torch.no_grad(), torch.cuda.stream(stream):
-                for i in list(range(k, len(items), len(lanes))) + [None]:
-                    ticket = None
-                    if i is not None:
-                        x = torch.from_numpy(items[i]).to(engine.device, non_blocking=False).reshape(1, -1)
-                        ticket = (i, engine.encode_async(x, K))
-                    if pending is not None:
-                        j, t = pending
-                        out[j] = t.wait()[0].cpu().numpy().astype(np.int64)
-                    pending = ticket
-
-        n = min(len(lanes), len(items))
-        with ThreadPoolExecutor(n) as ex:
-            list(ex.map(run, range(n)))
+        pipe = self._pipeline()
+        pending = None
+        with torch.no_grad():
+            for g in groups + [None]:
+                cur = None
+                if g is not None:
+                    lens = [items[i].shape[0] for i in g]
+                    cur = (g, pipe.submit([items[i] for i in g], lens,
+                                          [encoded_length(n, self.model.config) for n in lens]))
+                if pending is not None:
+                    for i, c in zip(pending[0], pipe.collect(pending[1])):
+                        out[i] = c
+                pending = cur
         return out

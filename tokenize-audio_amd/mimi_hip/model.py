@@ -277,6 +277,30 @@ class MimiHipModel:
                                                ctypes.c_void_p(out.data_ptr()), self._stream(), ctypes.byref(t)))
         return EncodeTicket(self, t.value, out, audio)
 
+    def encode_ragged_async(self, audio: torch.Tensor, lengths, num_quantizers: int,
+                            out: Optional[torch.Tensor] = None) -> "EncodeTicket":
+        """Ragged batch (``mimi_encode_ragged_async``): item b = ``audio[b, :lengths[b]]`` of a device f32 [B, Lmax]
+        tensor, encoded exactly as it would be alone at its own length (bit for bit), in one pass that skips every
+        item's rows past its length.  ``ticket.wait()`` returns int32 [B, K, T(Lmax)]; item b's codes are
+        ``[:, :encoded_length(lengths[b])]`` (the frames past are unspecified)."""
+        K = self._check_k(num_quantizers)
+        audio = self._device_audio(audio)
+        B, L = audio.shape
+        lens = np.ascontiguousarray(np.asarray(lengths, dtype=np.int64).reshape(-1))
+        if lens.shape != (B,) or (B and (int(lens.min()) < 1 or int(lens.max()) > L)):
+            raise ValueError(f"lengths must be {B} values in [1, {L}]")
+        out = self._out(B, K, encoded_length(L, self.config), out)
+        t = ctypes.c_int64()
+        _lib.check(self._lib.mimi_encode_ragged_async(self._h, ctypes.c_void_p(audio.data_ptr()),
+                                                      ctypes.c_void_p(lens.ctypes.data), B, L, K,
+                                                      ctypes.c_void_p(out.data_ptr()), self._stream(),
+                                                      ctypes.byref(t)))
+        return EncodeTicket(self, t.value, out, audio)
+
+    def encode_ragged(self, audio: torch.Tensor, lengths, num_quantizers: int,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return self.encode_ragged_async(audio, lengths, num_quantizers, out).wait()
+
     def quantize(self, embedding: torch.Tensor, num_quantizers: int) -> torch.Tensor:
         """Quantizer alone on a pre-quantizer embedding [B, 512, T] -> int64 codes [B, K, T]."""
         B, C, T = embedding.shape

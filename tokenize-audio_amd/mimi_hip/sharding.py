@@ -7,7 +7,10 @@ node this driver does the same thing with one process per GPU launched by ``torc
 * batching: each rank forms batches from ITS utterances in original order (``make_batches``), so a padded
   batch has exactly the composition the reference wrapper would give those utterances, which is what the
   pad-to-longest tail-frame semantics depend on (``emilia-mimi/process_shard.py:88-140``);
-* encode: the drop-in ``MimiEncoder`` of this package on the rank's GPU -- no collective on the data path;
+* encode: the drop-in ``MimiEncoder`` of this package on the rank's GPU -- no collective on the data path; its
+  ``encode_batches`` pipeline is used when present (the next batch is loaded, staged and copied to the GPU while
+  the current one encodes), and a rank only ever reads its own utterances (``audio`` may be a lazy sequence, or
+  ``loader(i)`` loads utterance i on demand);
 * merge: codes are gathered to rank 0 on the host (``torch.distributed.gather_object``; ~400 B per
   audio-second) and put back in original index order.
 """
@@ -34,16 +37,36 @@ def make_batches(indices: Sequence[int], batch_size: int) -> List[List[int]]:
     return [idx[i:i + batch_size] for i in range(0, len(idx), batch_size)]
 
 
-def encode_shard(encode_batch: Callable[[List[np.ndarray]], List[np.ndarray]], audio: Sequence[np.ndarray],
-                 world: int, rank: int, batch_size: int) -> dict:
-    """Encode this rank's utterances; returns {index: codes}."""
+def encode_shard(encode_batch: Callable[[List[np.ndarray]], List[np.ndarray]], audio, world: int, rank: int,
+                 batch_size: int, encode_batches: Optional[Callable] = None) -> dict:
+    """Encode this rank's utterances; returns {index: codes}.  ``audio[i]`` is only read for this rank's indices,
+    one batch at a time (lazily, when ``encode_batches`` -- a pipelined batch iterator -- asks for it)."""
     out = {}
-    for batch in make_batches(shard_indices(len(audio), world, rank), batch_size):
-        codes = encode_batch([audio[i] for i in batch])
+    batches = make_batches(shard_indices(len(audio), world, rank), batch_size)
+    if encode_batches is not None:
+        results = encode_batches([audio[i] for i in b] for b in batches)
+    else:
+        results = (encode_batch([audio[i] for i in b]) for b in batches)
+    for batch, codes in zip(batches, results):
         if len(codes) != len(batch):
             raise RuntimeError("encoder returned a different number of items than it was given")
         out.update(zip(batch, codes))
     return out
+
+
+class LazyAudio:
+    """A sequence of ``n`` utterances loaded on demand by ``loader(i)`` (a rank touches only its own indices)."""
+
+    def __init__(self, n: int, loader: Callable[[int], np.ndarray]):
+        self.n, self.loader = n, loader
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        if not 0 <= i < self.n:
+            raise IndexError(i)
+        return self.loader(i)
 
 
 def merge_shards(parts: Sequence[dict], n_items: int) -> List[np.ndarray]:
@@ -81,9 +104,18 @@ class DistributedMimiEncoder:
             encoder = MimiEncoder(model_id, device=f"cuda:{local}", num_quantizers=num_quantizers)
         self.encoder = encoder
 
-    def encode_all(self, audio: Sequence[np.ndarray]) -> Optional[List[np.ndarray]]:
+    def encode_all(self, audio: Optional[Sequence[np.ndarray]] = None, n_items: Optional[int] = None,
+                   loader: Optional[Callable[[int], np.ndarray]] = None) -> Optional[List[np.ndarray]]:
+        """Encode the shard (``audio``, or ``n_items`` utterances loaded by ``loader(i)``); the merged codes on rank
+        0, None elsewhere."""
+        if audio is None:
+            if loader is None or n_items is None:
+                raise ValueError("pass audio, or n_items and loader")
+            audio = LazyAudio(n_items, loader)
+        eb = getattr(self.encoder, "encode_batches", None)
         part = encode_shard(lambda b: self.encoder.encode_audio_batch(b, self.sample_rate), audio, self.world,
-                            self.rank, self.batch_size)
+                            self.rank, self.batch_size,
+                            encode_batches=(lambda it: eb(it, self.sample_rate)) if eb else None)
         if self.dist is None:
             return merge_shards([part], len(audio))
         parts = [None] * self.world if self.rank == 0 else None
