@@ -468,10 +468,11 @@ def main():
 
     wl.run_steps(0, args.warmup)
     torch.cuda.synchronize()
-    profile = not args.no_profile and wl.kind == "batch"
+    profile = not args.no_profile
     # small batches are launch-bound and replay hipGraphs (engine.cpp graph_encode), which per-stage events
-    # would switch off: their timed region runs without events and the stage profile comes from a separate pass
-    profile_separately = profile and args.batch <= 4
+    # would switch off: their timed region runs without events and the stage profile comes from a separate pass;
+    # so do the host-fed workloads (their device time per step, beside the wall time, shows what the host costs)
+    profile_separately = profile and (args.batch <= 4 or wl.kind != "batch")
     if profile and not profile_separately:
         model.profile_reset()
         model.set_profiling(True)
@@ -494,8 +495,11 @@ def main():
     if profile_separately:
         model.profile_reset()
         model.set_profiling(True)
+        n_emitted = len(getattr(wl, "emitted", []))
         wl.run_steps(args.warmup, args.steps)
         torch.cuda.synchronize()
+        if hasattr(wl, "emitted"):
+            del wl.emitted[n_emitted:]  # (the profiled pass re-encodes the timed steps: keep their codes once)
     if profile:
         model.set_profiling(False)
         prof = model.profile_read()

@@ -64,6 +64,12 @@ static hipError_t run_split(const GemmArgs& a, hipStream_t s) {
 template <int BM, int BN, int WM, int WN, int NS, int ST, int EPI, int OUTP, int TAG, int LW = 0, int BK = 32, int MF = 32,
           int FL = 0, bool F16 = false>
 static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
+    if constexpr (F16 && !(FL & FL_RAGGED)) {  // ragged batch: the same tile with per-item rows (gemm_planes.h)
+        if (a.m_rows || a.a_rows) {
+            if (!a.m_rows || !a.a_rows) return hipErrorInvalidValue;
+            return run_planes<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL | FL_RAGGED, F16>(a, s);
+        }
+    }
     static char name[160];
     if (!name[0])
         snprintf(name, sizeof(name), "mimi::gemm_planes_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %s>", BM,

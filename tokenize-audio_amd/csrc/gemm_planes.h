@@ -87,7 +87,9 @@ __device__ __forceinline__ int chunk_swz(int row) {
 //           FL_PF -- (with FL_PERSIST and loader waves) the loaders issue the next tile's first ring stages while
 //           the compute waves run this tile's epilogue (the staging moves past those slots, in more passes if
 //           needed).
-enum : int { FL_PRIO = 2, FL_PAIR = 4, FL_PERSIST = 8, FL_KG2 = 16, FL_KG4 = 32, FL_PF = 256 };
+//           FL_RAGGED -- per-item valid rows (GemmArgs a_rows / m_rows: ragged batches); a separate instantiation so
+//           the uniform batches' kernels carry none of its bookkeeping (it cost them 2-7 % when it was run-time)
+enum : int { FL_PRIO = 2, FL_PAIR = 4, FL_PERSIST = 8, FL_KG2 = 16, FL_KG4 = 32, FL_PF = 256, FL_RAGGED = 512 };
 // tuning diagnostics (tools/gemm_bench.hip only; results are garbage): no DMA refills after the prologue / no MFMAs
 enum : int { FL_DIAG_NODMA = 64, FL_DIAG_NOMMA = 128 };
 
@@ -157,21 +159,37 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     const int wn = compute ? wave % WN : 0;
     const int M = p.M, N = p.N, K = p.K;
     const int MT = (M + BM - 1) / BM, NTn = (N + BN - 1) / BN;
-    const int ntiles = MT * NTn * p.batch;
+    // ragged batches (FL_RAGGED): the tile space is only the items' valid M tiles (item b: ceil(m_rows[b] / BM),
+    // items concatenated) x the N tiles, so the XCD-contiguous blocks of xcd_remap and the persistent round-robin
+    // share VALID work evenly (a skip of invalid tiles would leave whole XCDs idle beside long items)
+    constexpr bool RG = (FL & FL_RAGGED) != 0;
+    int ntiles = MT * NTn * p.batch;
+    if constexpr (RG) {
+        int v = 0;
+        for (int bb = 0; bb < p.batch; ++bb) v += (p.m_rows[bb] + BM - 1) / BM;
+        ntiles = v * NTn;
+    }
     float omx = 0.0f;  // max|planes value| (fp16 planes: the engine's range check), over this workgroup's tiles
     const int KT = K / BK / NB;
-    // ragged batches: a tile whose first row lies past its item's valid rows does nothing (no loads, MFMAs or
-    // stores); loaders and compute waves skip the same tiles, so they keep meeting at the same barriers
-    auto next_tile = [&](int t) {
-        if (p.m_rows) {
-            for (; t < ntiles; t += (int)gridDim.x) {
-                const int lg = xcd_remap(t, ntiles), rest = lg / NTn;
-                if ((rest % MT) * BM < p.m_rows[rest / MT]) break;
+    // tile -> (item, M tile, N tile)
+    auto decode = [&](int tile, int& b, int& mt, int& nt) {
+        const int logical = xcd_remap(tile, ntiles);
+        nt = logical % NTn;
+        int rest = logical / NTn;
+        if constexpr (RG) {
+            b = 0;
+            for (; b < p.batch - 1; ++b) {
+                const int nb = (p.m_rows[b] + BM - 1) / BM;
+                if (rest < nb) break;
+                rest -= nb;
             }
+            mt = rest;
+        } else {
+            mt = rest % MT;
+            b = rest / MT;
         }
-        return t;
     };
-    auto a_len_of = [&](int b) { return p.a_rows ? (long long)p.a_rows[b] * p.a_cin : p.a_len; };
+    auto a_len_of = [&](int b) { return RG ? (long long)p.a_rows[b] * p.a_cin : p.a_len; };
 
     if constexpr (LW > 0) {
         // Warp-specialised: the loading waves run their own tile loop, meeting the compute waves at the same
@@ -193,9 +211,9 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                 int a_lane = 0, b_lane = 0, kimg = 0;
                 KOrderT<BK> ko;  // K steps are issued in order: the cursor follows the issues
                 auto setup = [&](int tile) {  // this wave's sources for `tile`, K cursor at its first step
-                    const int logical = xcd_remap(tile, ntiles);
-                    const int nt = logical % NTn, rest = logical / NTn;
-                    const int m0 = (rest % MT) * BM, n0 = nt * BN, b = rest / MT;
+                    int b, mt, nt;
+                    decode(tile, b, mt, nt);
+                    const int m0 = mt * BM, n0 = nt * BN;
                     const __bf16* __restrict__ Abase = reinterpret_cast<const __bf16*>(p.Ap) + (long long)b * p.a_bstride;
 #pragma unroll
                     for (int pl = 0; pl < NS; ++pl)
@@ -234,7 +252,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                     for (int s2 = 0; s2 < STAGES - KG; ++s2)
                         if (s2 < KT) issue_w(s2);
                 };
-                const int first = next_tile((int)blockIdx.x);
+                const int first = (int)blockIdx.x;
                 if (first < ntiles) prologue(first);
                 for (int tile = first; tile < ntiles;) {
                     for (int kt = 0; kt < KT; kt += KG) {
@@ -248,7 +266,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                         }
                     }
                     __syncthreads();  // the compute waves' epilogue starts (the ring is free)
-                    const int next = next_tile(tile + (int)gridDim.x);
+                    const int next = tile + (int)gridDim.x;
                     if (PF && next < ntiles) prologue(next);  // lands in slots [0, STAGES - KG) under the epilogue
                     if (FL & FL_PERSIST) {
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -273,12 +291,9 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         }
     }
 
-    for (int tile = next_tile((int)blockIdx.x); tile < ntiles; tile = next_tile(tile + (int)gridDim.x)) {
-    const int logical = xcd_remap(tile, ntiles);
-    const int nt = logical % NTn;
-    const int rest = logical / NTn;
-    const int mt = rest % MT;
-    const int b = rest / MT;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int b, mt, nt;
+    decode(tile, b, mt, nt);
     const int m0 = mt * BM, n0 = nt * BN;
 
     // ---- DMA sources for this lane (RPP rows x CPR chunks per piece; lane -> row lane/CPR, chunk lane%CPR)
@@ -460,7 +475,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     const int rbase = m0 + wm * RW;
     const int cbase = n0 + wn * CW + (lane & (MF - 1));
     const float us = F16 ? p.unscale : 1.0f;  // 1 / (activation scale x weight scale): exact power of two
-    const int Mb = p.m_rows ? min(M, p.m_rows[b]) : M;  // this item's valid output rows
+    const int Mb = RG ? min(M, p.m_rows[b]) : M;  // this item's valid output rows
 #pragma unroll
     for (int jh = 0; jh < JH; ++jh) {
 #pragma unroll

@@ -1294,9 +1294,14 @@ constexpr int RVQ_CAND = 2048;
 // 32 frames per workgroup (64-frame tiles, which halve the per-CU codebook stream, were slower: 1 workgroup per CU,
 // profiles/r2d_rvq_ft64.log).  PF: codebook k-steps in flight per wave (4: two workgroups per CU; 16 = all of them, for small batches whose few
 // workgroups wait on L2 / Infinity-Cache latency); EX: float4 of a code row in flight per exact re-score round
-template <int D, int PF = 4, int EX = 16>
+template <int D, int PF = 4, int EX = 16, bool RG = false>
 // (HIP's second launch bound is waves per SIMD: 4 = two 8-wave workgroups per CU, i.e. <= 128 VGPRs)
 __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(RvqArgs p, int L0) {
+    // RG (a ragged batch: p.flen): a workgroup none of whose frames is valid has nothing to do -- no later level
+    // reads what it would write (only valid frames' residuals and partial argmins are ever read)
+    if constexpr (RG) {
+        if (!__syncthreads_or((int)threadIdx.x < 32 && rvq_valid(p, (long long)blockIdx.x * 32 + threadIdx.x))) return;
+    }
     const int L = L0 + (int)blockIdx.z;  // (grid.z = 2: the semantic and first acoustic levels together)
     constexpr int FT = 32;
     constexpr int LDH = D / 2 + 4;
@@ -1535,13 +1540,20 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
         const dim3 grid((unsigned)((a.frames + 31) / 32), 2048 / RVQ_CS);
         const bool small = grid.x * grid.y < 256;
         const bool split = a.sem_split != 0;  // levels 0 and 1 in one launch (rvq_sem_split)
-        *kname = small ? "mimi::rvq_level_h16_kernel<256, 16, 32>" : "mimi::rvq_level_h16_kernel<256, 4, 16>";
+        *kname = a.flen ? (small ? "mimi::rvq_level_h16_kernel<256, 16, 32, true>" : "mimi::rvq_level_h16_kernel<256, 4, 16, true>")
+                        : (small ? "mimi::rvq_level_h16_kernel<256, 16, 32, false>" : "mimi::rvq_level_h16_kernel<256, 4, 16, false>");
         for (int L = 0; L < a.levels; L += (split && L == 0) ? 2 : 1) {
             const dim3 g(grid.x, grid.y, (split && L == 0) ? 2 : 1);
-            if (small)
+            if (a.flen) {  // ragged: workgroups of invalid frames exit (rvq_level_h16_kernel<..., RG>)
+                if (small)
+                    hipLaunchKernelGGL((rvq_level_h16_kernel<256, 16, 32, true>), g, dim3(512), 0, s, a, L);
+                else
+                    hipLaunchKernelGGL((rvq_level_h16_kernel<256, 4, 16, true>), g, dim3(512), 0, s, a, L);
+            } else if (small) {
                 hipLaunchKernelGGL((rvq_level_h16_kernel<256, 16, 32>), g, dim3(512), 0, s, a, L);
-            else
+            } else {
                 hipLaunchKernelGGL((rvq_level_h16_kernel<256>), g, dim3(512), 0, s, a, L);
+            }
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
