@@ -92,6 +92,8 @@ def parse():
     ap.add_argument("--no-f32-mode", action="store_true", help="skip the fp32-MFMA comparison run")
     ap.add_argument("--precision", default=None, help="GEMM precision mode (default: the engine's)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--stage0-fused", type=int, default=None,
+                    help="kernel variant A/B: 0 = stage-0 block + down conv 0 as two kernels, 1 = fused (default)")
     ap.add_argument("--dump-sequence", default=None,
                     help="write the engine's per-encode (stage, kernel) launch sequence here (PMC stage keys)")
     ap.add_argument("--pmc-pass", action="store_true",
@@ -453,6 +455,8 @@ def main():
     model = MimiHipModel(synthetic.make_state_dict(seed=0, num_quantizers=K), device=dev)
     if args.precision:
         model.set_precision(args.precision)
+    if args.stage0_fused is not None:
+        model.set_option("stage0_fused", args.stage0_fused)
     wl = Workload(args, model, dev, world, rank)
     if model.precision == "f16x3":
         model.calibrate()  # (otherwise inside the first encode) -- before the trace marker

@@ -167,6 +167,10 @@ int64_t mimi_f16_reruns(const mimi_engine* e);
  * Never used while profiling or taps are on.  enable = 0 drops the captured graphs.  Replays so far: */
 int mimi_set_graphs(mimi_engine* e, int32_t enable);
 int64_t mimi_graph_replays(const mimi_engine* e);
+/* Kernel-variant options (tuning / A-B checks; every setting gives identical codes).  key "stage0_fused":
+ * 0 = stage-0 residual block and down conv 0 as two kernels (y through HBM), 1 = one fused kernel (y stays on
+ * chip; default).  Unknown keys and values: MIMI_ERR_INVALID_ARGUMENT.  A change drops the captured graphs. */
+int mimi_set_option(mimi_engine* e, const char* key, int64_t value);
 /* MIMI_PRECISION_F16X3 diagnostics: per plane tensor (64-char names), its fixed activation scale and the max|x|
  * of the last waited encode (-1: not produced by it); an overflow is max * scale >= 2^15. */
 int mimi_act_scales(mimi_engine* e, int32_t max_n, char* names, float* scales, float* last_max, int32_t* n);

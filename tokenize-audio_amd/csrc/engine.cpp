@@ -324,6 +324,7 @@ struct mimi_engine {
     int64_t graph_replays = 0;
 
     bool taps = false;
+    int stage0_fused = 1;  // 0: stage-0 block + down conv 0 as two kernels; 1: one fused kernel
     struct Tap {
         float* d = nullptr;
         size_t cap = 0;
@@ -1351,11 +1352,33 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                 ra.hamax = ha.amax;
             }
             if (rg && !(h16 && (si == 0 || si == 1))) return set_err(MIMI_ERR_UNSUPPORTED, "ragged: fp16 blocks only");
-            LAUNCH_TRY(launch_resblock(C, ra, s, &kname), "resblock");
-            snprintf(nm, sizeof nm, "res_s%d", si);
             const double H = C / c.compress;
             const double BT = rows_of(si, (double)B * T);
             const double fl = 2.0 * BT * (3.0 * C * H + H * C) + (si == 0 ? 2.0 * BT * C * c.kernel_size : 0.0);
+            const DevConv& dc0 = e->down[0];
+            if (si == 0 && h16 && e->stage0_fused && C == 64 && dc0.cin == 64 && dc0.cout == 128 &&
+                dc0.k == 8 && dc0.stride == 4 && dc0.wh && dc0.b && p.T[1] == (T + 3) / 4) {
+                // y stays on chip: the block's output feeds down conv 0 in the same kernel (x1 = its fp32 output)
+                ra.wdown = dc0.wh;
+                ra.bdown = dc0.b;
+                ra.unscale_d = 1.0f / (yact.scale * dc0.wscale);
+                ra.xout = w.x;
+                ra.T1 = p.T[1];
+                ra.ilen1 = rg ? dT[1] : nullptr;
+                ra.yp = e->taps ? w.y : nullptr;  // taps only: y planes to HBM as well
+                LAUNCH_TRY(launch_stage0_fused(ra, s, &kname), "stage 0 + down conv 0");
+                const double BT1 = rows_of(1, (double)B * p.T[1]);
+                const double fld = 2.0 * BT1 * 128.0 * 512.0;
+                // HBM: audio in, x1 out, both weight sets (y never leaves the CU)
+                const double by = BT * 4 + BT1 * 128 * 4 + (3.0 * C * H + H * C) * 4 + 128.0 * 512 * 4;
+                rec.mark("res_down_s0", fl + fld, by, kname);
+                if ((rc = save_tap_planes(e, "res0_elu", w.y, ns, B, T, C, s, yact.scale))) return rc;
+                if ((rc = save_tap_planes(e, "down0", w.x, 0, B, p.T[1], 2 * C, s, 0.0f))) return rc;
+                C *= 2;
+                continue;
+            }
+            LAUNCH_TRY(launch_resblock(C, ra, s, &kname), "resblock");
+            snprintf(nm, sizeof nm, "res_s%d", si);
             const double by = BT * 4 * (si == 0 ? 1 + C : 2 * C) + (3.0 * C * H + H * C) * 4;
             rec.mark(nm, fl, by, kname);
         } else {
@@ -2203,6 +2226,22 @@ extern "C" int mimi_set_graphs(mimi_engine* e, int32_t enable) {
 }
 
 extern "C" int64_t mimi_graph_replays(const mimi_engine* e) { return e ? e->graph_replays : -1; }
+
+extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {
+    if (!e || !key) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine or key");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!strcmp(key, "stage0_fused")) {
+        if (value < 0 || value > 1) return set_err(MIMI_ERR_INVALID_ARGUMENT, "stage0_fused %lld (0 or 1)", (long long)value);
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->stage0_fused != (int)value) {  // captured graphs hold the other kernel sequence
+            drop_graphs(e);
+            e->graph_seen.clear();
+        }
+        e->stage0_fused = (int)value;
+        return MIMI_OK;
+    }
+    return set_err(MIMI_ERR_INVALID_ARGUMENT, "unknown option '%s'", key);
+}
 
 extern "C" int mimi_act_scales(mimi_engine* e, int32_t max_n, char* names, float* scales, float* last_max,
                                int32_t* n) {

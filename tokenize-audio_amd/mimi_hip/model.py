@@ -339,6 +339,11 @@ class MimiHipModel:
     def graph_replays(self) -> int:
         return int(self._lib.mimi_graph_replays(self._h))
 
+    def set_option(self, key: str, value: int):
+        """Kernel-variant option (identical codes either way): "stage0_fused" 0 = stage-0 block and down conv 0 as
+        two kernels, 1 = one fused kernel (default)."""
+        _lib.check(self._lib.mimi_set_option(self._h, key.encode(), int(value)))
+
     def act_scales(self):
         """f16x3 diagnostics: {tensor: (fixed scale, max|x| of the last encode, headroom 2^15 / (scale * max))}."""
         n = 256
