@@ -1356,15 +1356,17 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             const double BT = rows_of(si, (double)B * T);
             const double fl = 2.0 * BT * (3.0 * C * H + H * C) + (si == 0 ? 2.0 * BT * C * c.kernel_size : 0.0);
             const DevConv& dc0 = e->down[0];
+            bool t1_ceil = p.T[1] == (T + 3) / 4;  // the kernel's output steps: ceil(T0 / 4) per item
+            if (rg)
+                for (int b = 0; b < B; ++b) t1_ceil = t1_ceil && rg->plan[b].T[1] == (rg->plan[b].T[0] + 3) / 4;
             if (si == 0 && h16 && e->stage0_fused && C == 64 && dc0.cin == 64 && dc0.cout == 128 &&
-                dc0.k == 8 && dc0.stride == 4 && dc0.wh && dc0.b && p.T[1] == (T + 3) / 4) {
+                dc0.k == 8 && dc0.stride == 4 && dc0.wh && dc0.b && t1_ceil) {
                 // y stays on chip: the block's output feeds down conv 0 in the same kernel (x1 = its fp32 output)
                 ra.wdown = dc0.wh;
                 ra.bdown = dc0.b;
                 ra.unscale_d = 1.0f / (yact.scale * dc0.wscale);
                 ra.xout = w.x;
                 ra.T1 = p.T[1];
-                ra.ilen1 = rg ? dT[1] : nullptr;
                 ra.yp = e->taps ? w.y : nullptr;  // taps only: y planes to HBM as well
                 LAUNCH_TRY(launch_stage0_fused(ra, s, &kname), "stage 0 + down conv 0");
                 const double BT1 = rows_of(1, (double)B * p.T[1]);

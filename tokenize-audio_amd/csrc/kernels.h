@@ -233,13 +233,12 @@ struct ResArgs {
     const unsigned* istart;
     // stage 0 fused with down conv 0 (stage0_fused_h16_kernel): the down conv's 2 fp16 weight planes [2][128][512]
     // (K = tap-major 8 x 64, the planes GEMM's layout), bias, unscale_d = 1 / (yscale x weight scale), and its
-    // fp32 output [B][T1][128] (T1 = ceil(T / 4): the row stride; ragged: item b has ilen1[b] rows)
+    // fp32 output [B][T1][128] (T1 = ceil(T / 4): the row stride; ragged: item b has ceil(ilen[b] / 4) rows)
     const void* wdown;
     const float* bdown;
     float unscale_d;
     float* xout;
     long long T1;
-    const int* ilen1;
 };
 hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** kname);
 // stage 0 + down conv 0 in one kernel (PREC_F16X3)

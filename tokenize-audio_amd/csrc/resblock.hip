@@ -13,6 +13,7 @@
 #include <type_traits>
 
 #include "gemm_kernel.h"
+#include "resblock_h16.h"
 
 namespace mimi {
 
@@ -511,93 +512,6 @@ __global__ __launch_bounds__(256) void resblock0_wave_kernel(ResArgs p) {
 // LDS: weights 36 KB + biases + 12 x 9.75 KB per-wave slab / audio window = 153.6 KB.  12 waves (3 per SIMD, 168
 // VGPRs) beat 8: 0.70 vs 0.75 ms.
 // ------------------------------------------------------------------------------------------------
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-namespace r0h {
-constexpr int SLD = 72, SROWS = 34, SPL = SROWS * SLD;  // slab [2 planes][34][72 halves]: 144-B rows, 36 dwords
-                                                        // (an odd multiple of 16 B: conflict-free ds_read_b128
-                                                        // column reads); h [2][32][32] reuses rows 2..33
-constexpr int AUD = 48;                                 // audio window floats
-constexpr int WAVE_BYTES = 2 * SPL * 2 + AUD * 4;
-constexpr int NW = 12;
-constexpr int FR_W0 = 0, FR_W3 = 4, FR_W1 = 28, NFRAG = 36;  // 1-KB A fragments [64 lanes][8 halves]
-constexpr int BIAS = 64 + 32 + 64;                           // b0 | b3 | b1
-constexpr int LDS_BYTES = NFRAG * 1024 + BIAS * 4 + NW * WAVE_BYTES;
-static_assert(NFRAG == RES0_H16_FRAGS, "fragment count");
-static_assert(LDS_BYTES <= 160 * 1024, "LDS");
-}  // namespace r0h
-
-__device__ __forceinline__ f32x16 mfma_h(f16x8 a, f16x8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-}
-
-// fp16 planes of 4 already-scaled values t: hi = fp16(t) (packed converts), lo = fp16(t - hi), the difference
-// taken exactly in fp32 and rounded once by v_fma_mix{lo,hi}_f16 (the same bits as fp16(t - (float)hi), 2
-// instructions instead of 4 per pair)
-__device__ __forceinline__ void split4_t(const float (&t)[4], uint2& hi, uint2& lo) {
-    unsigned hu[2], lu[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const f16x2 h = __builtin_convertvector((f32x2){t[2 * q], t[2 * q + 1]}, f16x2);
-        hu[q] = __builtin_bit_cast(unsigned, h);
-        asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
-            "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-            : "=&v"(lu[q])
-            : "v"(hu[q]), "v"(t[2 * q]), "v"(t[2 * q + 1]));
-    }
-    hi = make_uint2(hu[0], hu[1]);
-    lo = make_uint2(lu[0], lu[1]);
-}
-
-// ELU(z) * s for a power-of-two s, two values at a time: med3(z s, fma(exp(z), s, -s), 0).  For z > 0 the
-// median is z s (exp(z) - 1 > z); for z <= 0 it is (exp(z) - 1) s (z <= exp(z) - 1 <= 0).  That is elu_fast's
-// select (exp as v_exp_f32 of z log2(e)) followed by an exact scaling, bit for bit, with no compare.
-__device__ __forceinline__ f32x2 elu_s2(f32x2 z, float s) {
-    const f32x2 l = z * 1.44269504f;
-    const f32x2 e = {__builtin_amdgcn_exp2f(l[0]), __builtin_amdgcn_exp2f(l[1])};
-    const f32x2 n = __builtin_elementwise_fma(e, (f32x2){s, s}, (f32x2){-s, -s});
-    const f32x2 zs = z * s;
-    return (f32x2){__builtin_amdgcn_fmed3f(zs[0], n[0], 0.0f), __builtin_amdgcn_fmed3f(zs[1], n[1], 0.0f)};
-}
-
-// 4 values z -> t = ELU(z) * s, max |t| into mx
-__device__ __forceinline__ void elu_s4(const float (&z)[4], float s, float (&t)[4], float& mx) {
-#pragma unroll
-    for (int q = 0; q < 4; q += 2) {
-        const f32x2 r = elu_s2((f32x2){z[q], z[q + 1]}, s);
-        t[q] = r[0];
-        t[q + 1] = r[1];
-        asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(mx) : "v"(mx), "v"(r[0]), "v"(r[1]));
-    }
-}
-
-// The persistent fp16 blocks' walk over 32-step tiles: the items' tiles concatenated (uniform: tpi per item;
-// ragged: item b's ceil(ilen[b] / 32) tiles from istart[b]), a wave / workgroup taking a contiguous range of them.
-struct TileWalk {
-    const ResArgs& p;
-    unsigned tpi;
-    unsigned b = 0;
-    long long t0 = 0;
-    __device__ TileWalk(const ResArgs& pa, unsigned tiles_per_item, unsigned g) : p(pa), tpi(tiles_per_item) {
-        if (p.istart) {
-            while (b + 1 < (unsigned)p.batch && p.istart[b + 1] <= g) ++b;
-            t0 = (long long)(g - p.istart[b]) * 32;
-        } else {
-            b = g / tpi;
-            t0 = (long long)(g - b * tpi) * 32;
-        }
-    }
-    __device__ long long len(unsigned bb) const { return p.ilen ? (long long)p.ilen[bb] : p.T; }
-    __device__ void next() {
-        t0 += 32;
-        if (t0 >= len(b)) {
-            ++b;
-            t0 = 0;
-        }
-    }
-};
 
 __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
     using namespace r0h;
@@ -624,7 +538,9 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
     float* aud = reinterpret_cast<float*>(slab + 2 * SPL);
 
     const long long T = p.T;  // row stride of the audio / y (and every item's length unless ragged)
-    const float* __restrict__ audio = io_pointer(p.audio_ref, p.audio);
+    // global (not flat) loads: a flat load in flight also holds lgkmcnt, so every LDS drain would wait for HBM
+    const __attribute__((address_space(1))) float* __restrict__ audio =
+        (const __attribute__((address_space(1))) float*)io_pointer(p.audio_ref, p.audio);
     const unsigned tpi = (unsigned)((T + 31) >> 5);  // tiles per item (host checks B x tpi < 2^32)
     const unsigned long long NT = p.istart ? p.istart[p.batch] : (unsigned long long)tpi * p.batch;
     const unsigned long long W = (unsigned long long)gridDim.x * NW;
@@ -641,7 +557,7 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
     // item's [0, T_b))
     auto aload = [&](unsigned bb, long long t0) {
         const long long pos = t0 - 8 + lane;
-        return (lane < AUD && pos >= 0 && pos < tw.len(bb)) ? audio[(long long)bb * T + pos] : 0.0f;
+        return (lane < AUD && pos >= 0 && pos < tw.Tb) ? audio[(long long)bb * T + pos] : 0.0f;  // (bb == tw.b)
     };
     // x0^T for the tile's 32 steps (lane column j = step t0 + j) from its audio window value av, + b0
     auto conv0 = [&](float av, f32x16 (&x0)[2]) {
@@ -699,7 +615,7 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
     for (unsigned g = g0; g < g1; ++g) {
         const unsigned b = tw.b;
         const long long t0 = tw.t0;
-        const long long Tb = tw.len(b);
+        const long long Tb = tw.Tb;
         if (t0 == 0) {  // causal zero padding of ELU(x0) before t = 0
             *reinterpret_cast<uint2*>(slab + cpl * SPL + crow * SLD + cc) = make_uint2(0u, 0u);
         } else if (g == g0) {  // range start inside an item: halo rows from the preceding tile's conv0
@@ -845,9 +761,6 @@ static_assert(NFRAG == RES1_H16_FRAGS, "fragment count");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 }  // namespace r1h
 
-__device__ __forceinline__ f32x4 mfma_h16(f16x8 a, f16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
 
 // Workgroup barrier for LDS hand-offs only: this wave's LDS operations complete, then s_barrier.  Unlike
 // __syncthreads() it does not drain vmcnt, so prefetched global loads and y stores stay in flight across it.
@@ -890,9 +803,9 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
 
     // x of the block at (item b, step t0), step t0 + off, channels 16(2mp + i) + 4lq .. +3 (zero outside the item's
     // [0, T_b))
-    auto xload = [&](unsigned b, long long t0b, long long off, f32x4 (&xv)[2]) {
+    auto xload = [&](unsigned b, long long Tlen, long long t0b, long long off, f32x4 (&xv)[2]) {
         const long long row = t0b + off;
-        const bool ok = row >= 0 && row < tw.len(b);
+        const bool ok = row >= 0 && row < Tlen;
         const float* xr = p.x + ((long long)b * T + (ok ? row : 0)) * C + 4 * lq;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -921,22 +834,22 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
 
     uint2 hhi[2], hlo[2];  // lanes with t >= 30: the halo planes for the next block
     f32x4 xn[2];
-    if (g0 < g1) xload(tw.b, tw.t0, t, xn);
+    if (g0 < g1) xload(tw.b, tw.Tb, tw.t0, t, xn);
     __syncthreads();  // weights and biases resident
     for (unsigned g = g0; g < g1; ++g) {
         const unsigned b = tw.b;
         const long long t0 = tw.t0;
-        const long long Tb = tw.len(b);
+        const long long Tb = tw.Tb;
         f32x4 xc[2] = {xn[0], xn[1]};
         tw.next();
-        if (g + 1 < g1) xload(tw.b, tw.t0, t, xn);  // flies under this block
+        if (g + 1 < g1) xload(tw.b, tw.Tb, tw.t0, t, xn);  // flies under this block
         // ---- slab: halo rows 0, 1 (lanes t = 30, 31), rows 2 + t
         if (t >= BM - 2) {
             if (t0 == 0) {
                 hhi[0] = hhi[1] = hlo[0] = hlo[1] = make_uint2(0u, 0u);
             } else if (g == g0) {
                 f32x4 xh[2];
-                xload(b, t0, t - BM, xh);  // steps t0 - 2, t0 - 1
+                xload(b, Tb, t0, t - BM, xh);  // steps t0 - 2, t0 - 1
                 xsplit(xh, hhi, hlo);
             }
             slab_row_put(t - (BM - 2), hhi, hlo);
@@ -1035,364 +948,6 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
     amax_commit(p.xamax, mxx * (1.0f / sx));
     amax_commit(p.hamax, mxh * (1.0f / sh));
     amax_commit(p.yamax, mxy * (1.0f / sy));
-}
-
-// ------------------------------------------------------------------------------------------------
-// Stage 0 with its down conv fused (PREC_F16X3): conv0 + residual block + ELU (resblock0_h16_kernel's per-block
-// arithmetic, unchanged) and down conv 0 (64 -> 128, k = 8, s = 4, TF/modeling_mimi.py:269-279 padding) in one
-// persistent kernel, so y -- the block's output, 2 fp16 planes, 4 B per channel-step -- never leaves the CU.
-// The codes are bit-identical to the unfused pair: every y plane value is resblock0_h16_kernel's, and every
-// down-conv MFMA (operand fragments, K-step order, product order) is the planes GEMM's (gemm_planes.h, FL_PAIR
-// K order: tap j, then j + 4, per 32-channel half; products lo.hi, hi.lo, hi.hi).
-//
-// One workgroup of 12 waves per CU (3 per SIMD, <= 168 VGPRs each), two roles meeting at one barrier per round:
-//   4 block waves (one per SIMD) -- each walks its own contiguous range of 32-step blocks, one per round: the
-//      block (conv0 -> slab -> GEMM1 -> h -> GEMM2 -> y) with y, zeroed past the item's end, written to section
-//      w of y buffer n % 2 (rows 4..35; rows 0..3 = the 4 causal halo steps: the same section's rows 32..35 of
-//      buffer (n-1) % 2, zeros at t = 0) + a descriptor (item, first 6 kHz step, rows to store)
-//   8 conv waves -- the down conv of round n-1's 4 sections (32 output steps, 8 per section) for 16 output
-//      channels each: 16 K steps x 2 tiles x 3 products of v_mfma_f32_16x16x32_f16, y fragments from buffer
-//      (n-1) % 2, the weights (16 channels x 512 k x 2 planes = 128 VGPRs) resident in registers.  Transposed (W
-//      is the A operand): a lane's accumulator is 4 consecutive channels of one step -> one 16-B fp32 store
-// so a SIMD runs one block wave (VALU-heavy: ELU, plane splits) beside two conv waves (MFMA + LDS only).  A block
-// wave whose range starts inside an item first recomputes the preceding block (round 0: its y only feeds the
-// halo; nothing is stored for it).
-// y buffer [plane][section 4][36 rows][72 halves] + 32 B between sections, 16-B chunk c of row r at c ^ 2 (r & 1):
-// the block waves' row writes (ds_write_b64) and the conv waves' fragment reads (ds_read_b128) are conflict-free.
-// LDS: block weights 36 KB + biases + 4 x 9.75 KB slabs + 2 x 40.75 KB y buffers = 157.3 KB.
-// ------------------------------------------------------------------------------------------------
-namespace s0f {
-constexpr int NA = 4, NC = 8, NW = NA + NC;  // block waves, conv waves
-constexpr int YLD = 72, YSR = 36, YSS = YSR * YLD + 16, YPS = 4 * YSS, YBS = 2 * YPS;  // halves
-constexpr int OFF_SLAB = r0h::NFRAG * 1024 + r0h::BIAS * 4;
-constexpr int OFF_Y = OFF_SLAB + NA * r0h::WAVE_BYTES;
-constexpr int OFF_D = OFF_Y + 2 * YBS * 2;
-constexpr int LDS_BYTES = OFF_D + 2 * NA * 16 + 16;
-static_assert(OFF_SLAB % 16 == 0 && OFF_Y % 16 == 0 && (YSS * 2) % 16 == 0, "16-B alignment");
-static_assert(LDS_BYTES <= 160 * 1024, "LDS");
-static_assert(NC * 16 == 128, "conv waves x 16 channels = down conv 0's output channels");
-}  // namespace s0f
-
-__global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
-    using namespace r0h;
-    constexpr int YLD = s0f::YLD, YSS = s0f::YSS, YPS = s0f::YPS, YBS = s0f::YBS, NA = s0f::NA;
-    __shared__ __attribute__((aligned(16))) char lds[s0f::LDS_BYTES];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(p.wh16);
-        uint4* dst = reinterpret_cast<uint4*>(lds);
-        for (int i = tid; i < NFRAG * 64; i += s0f::NW * 64) dst[i] = src[i];
-        float* bw = reinterpret_cast<float*>(lds + NFRAG * 1024);
-        if (tid < 64) {
-            bw[tid] = p.b0[tid];
-            bw[96 + tid] = p.b1[tid];
-        }
-        if (tid < 32) bw[64 + tid] = p.b3[tid];
-    }
-    _Float16* ybase = reinterpret_cast<_Float16*>(lds + s0f::OFF_Y);
-    int4* desc = reinterpret_cast<int4*>(lds + s0f::OFF_D);  // [buffer 2][section 4]: item, first step, rows
-    int* rcount = reinterpret_cast<int*>(lds + s0f::OFF_D + 2 * NA * 16);
-
-    const long long T = p.T;
-    const unsigned tpi = (unsigned)((T + 31) >> 5);
-    const unsigned long long NT = p.istart ? p.istart[p.batch] : (unsigned long long)tpi * p.batch;
-    const unsigned long long NWT = (unsigned long long)gridDim.x * NA;
-    // block wave w's range of blocks [g0, g1) (the conv waves compute it too, for the round count)
-    auto range = [&](int w, unsigned& g0, unsigned& g1) {
-        const unsigned long long wid = (unsigned long long)blockIdx.x * NA + w;
-        g0 = (unsigned)(wid * NT / NWT);
-        g1 = (unsigned)((wid + 1) * NT / NWT);
-    };
-    if (wave < NA) {
-        unsigned g0, g1;
-        range(wave, g0, g1);
-        TileWalk tw(p, tpi, g0);
-        if (lane == 0) {
-            rcount[wave] = (int)(g1 - g0) + ((g0 < g1 && tw.t0 > 0) ? 1 : 0);
-            desc[NA + wave] = make_int4(0, 0, 0, 0);  // round 0's conv (buffer 1) stores nothing
-        }
-    }
-    __syncthreads();
-    int R = 0;
-#pragma unroll
-    for (int w = 0; w < NA; ++w) R = max(R, rcount[w]);
-
-    if (wave >= NA) {
-        // ---------------- conv waves: output channels co0 .. co0 + 15 ----------------
-        const int co0 = 16 * (wave - NA);
-        const int c16 = lane & 15, kq = lane >> 4;
-        // wr[K step s][plane] = the planes GEMM's B fragment (channel lane & 15, k chunk lane >> 4) of K step
-        // s = 4 j + 2 lo + img: tap j + 4 img, input channels 32 lo .. 32 lo + 31
-        f16x8 wr[16][2];
-        {
-            const _Float16* wd = reinterpret_cast<const _Float16*>(p.wdown);
-#pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                const int tap = (s >> 2) + 4 * (s & 1), lo = (s >> 1) & 1;
-#pragma unroll
-                for (int pl = 0; pl < 2; ++pl)
-                    wr[s][pl] = *reinterpret_cast<const f16x8*>(wd + (long long)(pl * 128 + co0 + c16) * 512 + tap * 64 +
-                                                                32 * lo + 8 * kq);
-            }
-        }
-        const f32x4 bd = *reinterpret_cast<const f32x4*>(p.bdown + co0 + 4 * kq);
-        const float ud = p.unscale_d;
-        // output tile i: channels co0 + 4 kq + r (acc row) x 6 kHz step 16 i + (lane & 15) of the round = section
-        // 2 i + sec_l, step rho of that section (acc column)
-        const int sec_l = (lane >> 3) & 1, rho = lane & 7;
-        for (int n = 0; n <= R; ++n) {
-            if (n > 0) {
-                const _Float16* yb = ybase + ((n + 1) & 1) * YBS;
-                const int4* dsc = desc + ((n + 1) & 1) * NA;
-                f32x4 acc[2];
-#pragma unroll
-                for (int i = 0; i < 2; ++i) acc[i] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-                for (int s = 0; s < 16; ++s) {
-                    const int tap = (s >> 2) + 4 * (s & 1), lo = (s >> 1) & 1;
-                    const int row = 4 * rho + tap, ch = 4 * lo + kq;  // y step 4 (t1_0 + rho) - 4 + tap
-                    const int o = row * YLD + 8 * (ch ^ ((row & 1) * 2));
-                    f16x8 yf[2][2];
-#pragma unroll
-                    for (int i = 0; i < 2; ++i)
-#pragma unroll
-                        for (int pl = 0; pl < 2; ++pl)
-                            yf[pl][i] = *reinterpret_cast<const f16x8*>(yb + pl * YPS + (2 * i + sec_l) * YSS + o);
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        acc[i] = mfma_h16(wr[s][0], yf[1][i], acc[i]);  // y_lo w_hi
-                        acc[i] = mfma_h16(wr[s][1], yf[0][i], acc[i]);  // y_hi w_lo
-                        acc[i] = mfma_h16(wr[s][0], yf[0][i], acc[i]);  // y_hi w_hi
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const int4 d = dsc[2 * i + sec_l];
-                    if (rho < d.z) {
-                        f32x4 v;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] = acc[i][r] * ud + bd[r];  // the planes GEMM's EPI_BIAS
-                        *reinterpret_cast<f32x4*>(p.xout + ((long long)d.x * p.T1 + d.y + rho) * 128 + co0 + 4 * kq) = v;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-        return;
-    }
-
-    // ---------------- block waves ----------------
-    const f16x8* wf = reinterpret_cast<const f16x8*>(lds);
-    const float* bl = reinterpret_cast<const float*>(lds + NFRAG * 1024);
-    _Float16* slab = reinterpret_cast<_Float16*>(lds + s0f::OFF_SLAB + wave * WAVE_BYTES);
-    _Float16* hb = slab + 2 * SLD;
-    float* aud = reinterpret_cast<float*>(slab + 2 * SPL);
-    const float* __restrict__ audio = io_pointer(p.audio_ref, p.audio);
-    unsigned g0, g1;
-    range(wave, g0, g1);
-    TileWalk tw(p, tpi, g0);
-    const int hstart = (g0 < g1 && tw.t0 > 0) ? 1 : 0;  // range starts inside an item: recompute the block before
-    tw.t0 -= 32 * hstart;
-    const int Rw = (int)(g1 - g0) + hstart;  // this wave's rounds with a block
-    const int j = lane & 31, hh = lane >> 5;
-    const float sa = p.ascale, sx = p.xscale, sh = p.hscale, sy = p.yscale;
-    const float u0 = p.unscale0, u1 = p.unscale1, u2 = p.unscale2;
-    float mxa = 0.0f, mxx = 0.0f, mxh = 0.0f, mxy = 0.0f;
-    auto aload = [&](unsigned bb, long long t0) {
-        const long long pos = t0 - 8 + lane;
-        return (lane < AUD && pos >= 0 && pos < tw.len(bb)) ? audio[(long long)bb * T + pos] : 0.0f;
-    };
-    auto conv0 = [&](float av, f32x16 (&x0)[2]) {
-        if (lane < AUD) {
-            mxa = fmaxf(mxa, fabsf(av));
-            aud[lane] = av;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        f16x8 bq;
-#pragma unroll
-        for (int k = 0; k < 8; k += 2) {
-            const f32x2 t = {aud[j + 2 + k] * sa, aud[j + 3 + k] * sa};
-            const f16x2 h = __builtin_convertvector(t, f16x2);
-            const f16x2 l = __builtin_convertvector(t - __builtin_convertvector(h, f32x2), f16x2);
-            bq[k] = hh ? l[0] : h[0];
-            bq[k + 1] = hh ? l[1] : h[1];
-        }
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-            f32x16 acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-            acc = mfma_h(wf[(FR_W0 + 2 * mt + 1) * 64 + lane], bq, acc);
-            acc = mfma_h(wf[(FR_W0 + 2 * mt) * 64 + lane], bq, acc);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 32 * mt + 8 * g + 4 * hh);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) x0[mt][4 * g + q] = __builtin_fmaf(acc[4 * g + q], u0, bb[q]);
-            }
-        }
-    };
-    auto slab_put = [&](const f32x16 (&x0)[2], int rowoff) {
-        const int row = j + rowoff;
-        if (row < 0 || row >= SROWS) return;
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float z[4] = {x0[mt][4 * g], x0[mt][4 * g + 1], x0[mt][4 * g + 2], x0[mt][4 * g + 3]};
-                float t[4];
-                elu_s4(z, sx, t, mxx);
-                uint2 hi, lo;
-                split4_t(t, hi, lo);
-                const int o = row * SLD + 32 * mt + 8 * g + 4 * hh;
-                *reinterpret_cast<uint2*>(slab + o) = hi;
-                *reinterpret_cast<uint2*>(slab + SPL + o) = lo;
-            }
-    };
-    const int cpl = lane >> 5, crow = (lane >> 4) & 1, cc = (lane & 15) * 4;
-    // y halo copy lanes: plane, row 0..3, 16-B chunk (rows r and 32 + r have the same chunk order)
-    const int hrow = (lane >> 3) & 3;
-    const int hoff = (lane >> 5) * YPS + wave * YSS + hrow * YLD + 8 * ((lane & 7) ^ ((hrow & 1) * 2));
-    const int yrow = 4 + j, ysw = (yrow & 1) * 2;
-
-    float anext = Rw > 0 ? aload(tw.b, tw.t0) : 0.0f;
-    for (int n = 0; n <= R; ++n) {
-        _Float16* ycur = ybase + (n & 1) * YBS;
-        const _Float16* yprev = ybase + ((n + 1) & 1) * YBS;
-        int4* dcur = desc + (n & 1) * NA;
-        if (n < Rw) {
-            const unsigned b = tw.b;
-            const long long t0 = tw.t0;
-            const long long Tb = tw.len(b);
-            {
-                uint4 v = make_uint4(0u, 0u, 0u, 0u);
-                if (t0 > 0) v = *reinterpret_cast<const uint4*>(yprev + hoff + 32 * YLD);
-                *reinterpret_cast<uint4*>(ycur + hoff) = v;
-            }
-            if (lane == 0) {
-                const long long T1b = p.ilen1 ? (long long)p.ilen1[b] : p.T1;
-                const long long t10 = t0 >> 2;
-                dcur[wave] = make_int4((int)b, (int)t10, n < hstart ? 0 : (int)min(8LL, T1b - t10), 0);
-            }
-            if (t0 == 0) {
-                *reinterpret_cast<uint2*>(slab + cpl * SPL + crow * SLD + cc) = make_uint2(0u, 0u);
-            } else if (n == 0) {
-                f32x16 xp[2];
-                conv0(aload(b, t0 - 32), xp);
-                slab_put(xp, -30);
-            }
-            const float acur = anext;
-            tw.next();
-            if (n + 1 < Rw) anext = aload(tw.b, tw.t0);
-            f32x16 x0[2];
-            conv0(acur, x0);
-            slab_put(x0, 2);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-
-            f32x16 acc1;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc1[r] = 0.0f;
-#pragma unroll
-            for (int ks = 0; ks < 12; ++ks) {
-                const int o = (j + (ks >> 2)) * SLD + (ks & 3) * 16 + 8 * hh;
-                const f16x8 bx0 = *reinterpret_cast<const f16x8*>(slab + o);
-                const f16x8 bx1 = *reinterpret_cast<const f16x8*>(slab + SPL + o);
-                const f16x8 aw0 = wf[(FR_W3 + 2 * ks) * 64 + lane];
-                const f16x8 aw1 = wf[(FR_W3 + 2 * ks + 1) * 64 + lane];
-                acc1 = mfma_h(aw1, bx0, acc1);
-                acc1 = mfma_h(aw0, bx1, acc1);
-                acc1 = mfma_h(aw0, bx0, acc1);
-            }
-            {
-                _Float16* sp = slab + cpl * SPL;
-                const uint2 v = *reinterpret_cast<const uint2*>(sp + (32 + crow) * SLD + cc);
-                *reinterpret_cast<uint2*>(sp + crow * SLD + cc) = v;
-            }
-            asm volatile("" ::: "memory");
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) {
-                const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 64 + 8 * gq + 4 * hh);
-                float z[4], t[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) z[q] = __builtin_fmaf(acc1[4 * gq + q], u1, bb[q]);
-                elu_s4(z, sh, t, mxh);
-                uint2 hi, lo;
-                split4_t(t, hi, lo);
-                const int o = j * SLD + 8 * gq + 4 * hh;
-                *reinterpret_cast<uint2*>(hb + o) = hi;
-                *reinterpret_cast<uint2*>(hb + SPL + o) = lo;
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-
-            f32x16 acc2[2];
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc2[mt][r] = 0.0f;
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                const int o = j * SLD + ks * 16 + 8 * hh;
-                const f16x8 bh0 = *reinterpret_cast<const f16x8*>(hb + o);
-                const f16x8 bh1 = *reinterpret_cast<const f16x8*>(hb + SPL + o);
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    const f16x8 aw0 = wf[(FR_W1 + (mt * 2 + ks) * 2) * 64 + lane];
-                    const f16x8 aw1 = wf[(FR_W1 + (mt * 2 + ks) * 2 + 1) * 64 + lane];
-                    acc2[mt] = mfma_h(aw1, bh0, acc2[mt]);
-                    acc2[mt] = mfma_h(aw0, bh1, acc2[mt]);
-                    acc2[mt] = mfma_h(aw0, bh0, acc2[mt]);
-                }
-            }
-            // y = ELU(x0 + (acc + b1)) -> planes of y * yscale, section row 4 + j (zeros past the item's end)
-            float tmy = 0.0f;
-            const bool yin = t0 + j < Tb;
-            _Float16* ys = ycur + wave * YSS + yrow * YLD + 4 * hh;
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 96 + 32 * mt + 8 * gq + 4 * hh);
-                    float z[4], t[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) z[q] = x0[mt][4 * gq + q] + __builtin_fmaf(acc2[mt][4 * gq + q], u2, bb[q]);
-                    elu_s4(z, sy, t, tmy);
-                    uint2 hi, lo;
-                    split4_t(t, hi, lo);
-                    if (!yin) hi = lo = make_uint2(0u, 0u);
-                    const int o = 8 * ((4 * mt + gq) ^ ysw);
-                    *reinterpret_cast<uint2*>(ys + o) = hi;
-                    *reinterpret_cast<uint2*>(ys + YPS + o) = lo;
-                    if (p.yp && yin) {  // taps only: the y planes in resblock0_h16_kernel's HBM layout too
-                        _Float16* g = reinterpret_cast<_Float16*>(p.yp) + ((long long)b * T + t0 + j) * 64 + 32 * mt +
-                                      8 * gq + 4 * hh;
-                        *reinterpret_cast<uint2*>(g) = hi;
-                        *reinterpret_cast<uint2*>(g + p.y_pstride) = lo;
-                    }
-                }
-            if (yin) mxy = fmaxf(mxy, tmy);
-        } else if (lane == 0) {
-            dcur[wave] = make_int4(0, 0, 0, 0);
-        }
-        __syncthreads();
-    }
-    amax_commit(p.aamax, mxa);
-    amax_commit(p.xamax, mxx * (1.0f / sx));
-    amax_commit(p.hamax, mxh * (1.0f / sh));
-    amax_commit(p.yamax, mxy * (1.0f / sy));
-}
-
-hipError_t launch_stage0_fused(const ResArgs& a, hipStream_t s, const char** kname) {
-    if (a.T <= 0 || a.batch <= 0 || !a.audio || !a.wh16 || !a.wdown || !a.bdown || !a.xout ||
-        a.T1 != (a.T + 3) / 4 || (a.istart && !a.ilen1))
-        return hipErrorInvalidValue;
-    static const char* nm = "mimi::stage0_fused_h16_kernel(mimi::ResArgs)";
-    if (kname) *kname = nm;
-    int dev = 0, ncu = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    hipLaunchKernelGGL(stage0_fused_h16_kernel, dim3((unsigned)ncu), dim3(64 * s0f::NW), 0, s, a);
-    return hipGetLastError();
 }
 
 template <int C, int BM, bool WINDOW, bool FIRST, int W1M, int W1N, int W2M, int W2N, int NP>
