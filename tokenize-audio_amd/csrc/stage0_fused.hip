@@ -355,37 +355,37 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
             S0F_DRAIN();
             S0F_T(3);
 
-            f32x16 acc2[2];
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc2[mt][r] = 0.0f;
+            // GEMM2 + y per 32-channel half: the second half's MFMAs are independent of the first half's epilogue
+            f16x8 bh[2][2];
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 const int o = j * SLD + ks * 16 + 8 * hh;
-                const f16x8 bh0 = *reinterpret_cast<const f16x8*>(hb + o);
-                const f16x8 bh1 = *reinterpret_cast<const f16x8*>(hb + SPL + o);
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    const f16x8 aw0 = wf[(FR_W1 + (mt * 2 + ks) * 2) * 64 + lane];
-                    const f16x8 aw1 = wf[(FR_W1 + (mt * 2 + ks) * 2 + 1) * 64 + lane];
-                    acc2[mt] = mfma_h(aw1, bh0, acc2[mt]);
-                    acc2[mt] = mfma_h(aw0, bh1, acc2[mt]);
-                    acc2[mt] = mfma_h(aw0, bh0, acc2[mt]);
-                }
+                bh[ks][0] = *reinterpret_cast<const f16x8*>(hb + o);
+                bh[ks][1] = *reinterpret_cast<const f16x8*>(hb + SPL + o);
             }
             // y = ELU(x0 + (acc + b1)) -> planes of y * yscale, section row 4 + j (zeros past the item's end)
             float tmy = 0.0f;
             const bool yin = t0 + j < Tb;
             _Float16* ys = ycur + wave * YSS + yrow * YLD + 4 * hh;
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int mt = 0; mt < 2; ++mt) {
+                f32x16 acc2;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc2[r] = 0.0f;
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    const f16x8 aw0 = wf[(FR_W1 + (mt * 2 + ks) * 2) * 64 + lane];
+                    const f16x8 aw1 = wf[(FR_W1 + (mt * 2 + ks) * 2 + 1) * 64 + lane];
+                    acc2 = mfma_h(aw1, bh[ks][0], acc2);
+                    acc2 = mfma_h(aw0, bh[ks][1], acc2);
+                    acc2 = mfma_h(aw0, bh[ks][0], acc2);
+                }
 #pragma unroll
                 for (int gq = 0; gq < 4; ++gq) {
                     const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 96 + 32 * mt + 8 * gq + 4 * hh);
                     float z[4], t[4];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) z[q] = x0[mt][4 * gq + q] + __builtin_fmaf(acc2[mt][4 * gq + q], u2, bb[q]);
+                    for (int q = 0; q < 4; ++q) z[q] = x0[mt][4 * gq + q] + __builtin_fmaf(acc2[4 * gq + q], u2, bb[q]);
                     elu_s4<true>(z, sy, t, tmy);
                     uint2 hi, lo;
                     split4_t(t, hi, lo);
@@ -400,6 +400,7 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
                         *reinterpret_cast<uint2*>(g + p.y_pstride) = lo;
                     }
                 }
+            }
             if (yin) mxy = fmaxf(mxy, tmy);
             S0F_T(4);  // (slots: 0 halo + descriptor, 1 conv0, 2 slab, 3 GEMM1 + h, 4 GEMM2 + y, 5 barrier)
         } else if (lane == 0) {
