@@ -21,6 +21,13 @@
 
 #include "gemm_planes.h"
 
+#ifndef MIMI_QKV_V
+#define MIMI_QKV_V 1
+#endif
+#ifndef MIMI_FC1_V
+#define MIMI_FC1_V 0
+#endif
+
 namespace mimi {
 
 // ------------------------------------------------------------------------------------------------
@@ -271,9 +278,19 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         case ROLE_DOWN: return run_planes_big<EPI_BIAS, 0, 0, 2>(a, s, prec);
         case ROLE_DOWN_ELU: return run_planes_big_ld<EPI_BIAS_ELU, 3, 2, 3>(a, s, prec);  // planes out: final conv
         case ROLE_FINAL: return run_planes_small_ld<EPI_BIAS_OUT, 4>(a, s, prec);
-        case ROLE_QKV:  // fp16: a 2-stage ring, -10 % vs 4 stages (profiles/r1l_ab_small_kernels.txt); 4 loader waves:
-                        // -3.6 % (fc1 +11 % with them; 3 stages +1 %: profiles/r2e_ab_loaders_*.log)
-            if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 2, EPI_ROPE, 0, 5, 4, 32, 16, 0, true>(a, s);
+        case ROLE_QKV:  // fp16: persistent 128x128 tiles (M = 250 rows per item: 768 tiles, 1.5 rounds of a
+                        // non-persistent grid) on a 3-stage ring fed by 4 loader waves, the next tile's first stages
+                        // loading under the RoPE epilogue: 0.503 -> 0.485 ms per B = 32 step vs the 2-stage
+                        // non-persistent ring (profiles/r3c_ab_qkv_fc1.log; the same for fc1 measured +6 %)
+            if (prec == PREC_F16X3) {
+#if MIMI_QKV_V == 1
+                return run_planes<128, 128, 4, 2, 2, 3, EPI_ROPE, 0, 5, 4, 32, 16, FL_PERSIST | FL_PF, true>(a, s);
+#elif MIMI_QKV_V == 2
+                return run_planes<128, 128, 4, 2, 2, 2, EPI_ROPE, 0, 5, 0, 32, 16, 0, true>(a, s);
+#else
+                return run_planes<128, 128, 4, 2, 2, 2, EPI_ROPE, 0, 5, 4, 32, 16, 0, true>(a, s);
+#endif
+            }
             return run_planes_small<EPI_ROPE, 5>(a, s, prec);  // (256x256: -11 % alone, 0 in the engine)
         case ROLE_OPROJ: return run_planes_small_ld<EPI_SCALE_RES, 6>(a, s, prec);
         case ROLE_FC1:  // planes out: fc2; fp16: 128x128 on a 2-stage ring (two workgroups per CU): -4 % vs
@@ -281,7 +298,13 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
                         // r1l_ab_small_kernels.txt)
             // (256x128 persistent tiles with FL_PF: -8 % in tools/gemm_bench.hip, +5 % in the engine with the GELU
             // planes epilogue -- profiles/r2c_gemm_bench_pf.log, r2c_ab_fc1.log)
-            if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 2, EPI_GELU, 2, 7, 0, 32, 16, 0, true>(a, s);
+            if (prec == PREC_F16X3) {
+#if MIMI_FC1_V == 1
+                return run_planes<128, 128, 4, 2, 2, 3, EPI_GELU, 2, 7, 4, 32, 16, FL_PERSIST | FL_PF, true>(a, s);
+#else
+                return run_planes<128, 128, 4, 2, 2, 2, EPI_GELU, 2, 7, 0, 32, 16, 0, true>(a, s);
+#endif
+            }
             return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);
         case ROLE_FC2: return run_planes_small_ld<EPI_SCALE_RES, 8>(a, s, prec);
         case ROLE_DOWN_XE: return run_planes_big<EPI_BIAS, 3 | 8, 2 | 8, 11>(a, s, prec);

@@ -532,16 +532,53 @@ __device__ __forceinline__ int vt_key_pos(int r) {
     return (r & ~15) + 8 * ((k >> 2) & 1) + (k & 3) + 4 * ((k >> 3) & 1);
 }
 
-__global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __restrict__ qkv, int Ts, int H,
-                                                                 int window, float scale, void* __restrict__ outp,
-                                                                 long long pstride, float oscale,
-                                                                 unsigned* __restrict__ oamax,
-                                                                 const int* __restrict__ tlen) {
-    constexpr int D = 64, TM = 256, LDO = D + 1;
+// T <= 256 (every clip up to 10.24 s) on the fp16 matrix cores.  A workgroup of 16 waves holds one (item, head)'s
+// whole K / V as fp16 planes in LDS (power-of-two scales from the head's max |K|, |V|) and runs the causal 32-query
+// tiles as TASKS: tile t's key chunks (t + 1 of them at T = 256) are split into two halves, each run by one wave
+// with the online softmax of attn_chunk_h16, and the two partial states are merged once (m = max(m0, m1),
+// o = o0 c0 + o1 c1, l = l0 c0 + l1 c1, c_i = exp(m_i - m)).  That halves the longest chain of dependent chunks
+// (8 -> 4) and puts 4 waves on every SIMD (VGPRs <= 128) to hide the MFMA / exp latencies the 8-wave, one-tile-per-
+// wave form waited out.  qg > 1 (small batches: fewer (item, head) pairs than CUs): workgroup z of qg takes only some
+// tiles' tasks -- the SAME tasks, so every output is the same arithmetic whatever qg is (batch-size invariance):
+//   qg = 1: all 16 tasks, grouped so the 4 waves sharing a SIMD (w, w + 4, w + 8, w + 12) hold 9 chunks each;
+//   qg = 2: tiles {z, 3 - z, 4 + z, 7 - z} on waves 0-7;  qg = 4: tiles {7 - z, z} on waves 0-3.
+// Every workgroup still reads all of the head's K / V rows: the plane scales are the maxima over all of them.
+#ifndef ATTN_DIAG
+#define ATTN_DIAG 0  // tuning diagnostics (tools/attn_check.hip builds only; results garbage): 1 no chunk loop, 2 no K / V
+#endif               // plane image, 4 no merge
+__device__ __forceinline__ int attn_task(int qg, int z, int wave) {
+    unsigned long long tbl;
+    if (qg == 1) {
+        tbl = 0x31207456AB89DCFEull;  // wave w -> nibble w = 2 tile + half
+    } else if (qg == 2) {
+        if (wave >= 8) return -1;
+        tbl = z == 0 ? 0x670198FEull : 0x4523BADCull;
+    } else {
+        if (wave >= 4) return -1;
+        return 2 * (wave < 2 ? 7 - z : z) + (wave & 1);
+    }
+    return (int)((tbl >> (4 * wave)) & 15);
+}
+
+// tile t's output is stored by the workgroup that holds its tasks
+__device__ __forceinline__ bool attn_tile_in_wg(int qg, int z, int t) {
+    return qg == 1 || (qg == 2 ? ((t & 3) == z || (t & 3) == 3 - z) : (t == z || t == 7 - z));
+}
+
+__global__ __launch_bounds__(1024) void attention_t256_h16_kernel(const float* __restrict__ qkv, int Ts, int H,
+                                                                  int window, float scale, void* __restrict__ outp,
+                                                                  long long pstride, float oscale,
+                                                                  unsigned* __restrict__ oamax,
+                                                                  const int* __restrict__ tlen, int qg) {
+    constexpr int D = 64, TM = 256, LDO = D + 1, NWV = 16;
     constexpr int KLD = 72, KPL = TM * KLD;  // K planes: [256][72 halves]
     constexpr int VLD = 264, VPL = D * VLD;  // V^T planes: [64][264 halves]
     __shared__ __attribute__((aligned(16))) _Float16 lds[2 * KPL + 2 * VPL];
-    __shared__ float red[2][8];
+    __shared__ float red[2][NWV];
+    __shared__ float mlx[8][2][32];  // the half-1 task's m, l per query of each tile
+    // after the chunk loops the LDS holds the half-1 tasks' accumulators ([tile][32 regs][64 lanes] fp32, 64 KB)
+    // and, behind them, the merged tiles' output staging ([tile][32 queries][LDO] fp32)
+    static_assert(8 * 32 * 64 * 4 + 8 * 32 * LDO * 4 <= (2 * KPL + 2 * VPL) * 2, "merge + staging fit the K / V image");
     _Float16* Ks = lds;
     _Float16* Vt = lds + 2 * KPL;
     const int h = blockIdx.x, b = blockIdx.y;
@@ -554,20 +591,41 @@ __global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __
     const int hf = lane >> 5, col = lane & 31;
     const long long ld = 3LL * H * D;
     const float* base = qkv + (long long)b * Ts * ld;
-    // K / V rows 0 .. 255 (zeros past T) -> registers, head max |K|, |V|
-    constexpr int PER = TM * (D / 4) / 512;  // 8
-    f32x4 kv[PER], vv[PER];
+    const int task = attn_task(qg, (int)blockIdx.z, wave);
+    const int qt = task >> 1, kh = task & 1;  // (task < 0: no task -- the wave only loads)
+    // K / V rows 0 .. 255 (zeros past T) and the task's Q rows -> registers, all loads in flight before the first
+    // use (the maxima below wait for K / V, and Q's latency hides under theirs)
+    constexpr int PER = TM * (D / 4) / 1024;  // 4
+    const int qw = (task < 0 ? 0 : qt) * 32;
+    const int qi = qw + col;
+    f32x4 kv[PER], vv[PER], qa[4][2];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int idx = tid + q * 1024;
+        const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
+        const int rr = r < T ? r : T - 1;
+        kv[q] = *reinterpret_cast<const f32x4*>(base + (long long)rr * ld + H * D + h * D + c);
+        vv[q] = *reinterpret_cast<const f32x4*>(base + (long long)rr * ld + 2 * H * D + h * D + c);
+    }
+    // the task's 32 queries: lane (query col, half hf) holds dims 16 ks + 8 hf .. +7 (Q pre-scaled by 1/8)
+    const bool qok = task >= 0 && qi < T;
+    {
+        const float* qr = base + (long long)(qok ? qi : 0) * ld + h * D + 8 * hf;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            qa[ks][0] = *reinterpret_cast<const f32x4*>(qr + 16 * ks);
+            qa[ks][1] = *reinterpret_cast<const f32x4*>(qr + 16 * ks + 4);
+        }
+    }
     float mk = 0.0f, mv = 0.0f;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-        const int idx = tid + q * 512;
-        const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
-        const int rr = r < T ? r : T - 1;
-        const f32x4 k4 = *reinterpret_cast<const f32x4*>(base + (long long)rr * ld + H * D + h * D + c);
-        const f32x4 v4 = *reinterpret_cast<const f32x4*>(base + (long long)rr * ld + 2 * H * D + h * D + c);
+        const int r = (tid + q * 1024) / (D / 4);
         const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        kv[q] = r < T ? k4 : z;
-        vv[q] = r < T ? v4 : z;
+        if (r >= T) {
+            kv[q] = z;
+            vv[q] = z;
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             mk = fmaxf(mk, fabsf(kv[q][e]));
@@ -580,44 +638,39 @@ __global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __
         red[0][wave] = mk;
         red[1][wave] = mv;
     }
-    // this wave's 32 queries: lane (query col, half hf) holds dims 16 ks + 8 hf .. +7 (Q pre-scaled by 1/8)
-    const int qt = wave < 4 ? wave : 11 - wave;
-    const int qw = qt * 32;
-    const int qi = qw + col;
-    float qv[4][8];
-    float mq = 0.0f;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-        f32x4 a = {0.f, 0.f, 0.f, 0.f}, c = {0.f, 0.f, 0.f, 0.f};
-        if (qi < T) {
-            const float* qr = base + (long long)qi * ld + h * D + 16 * ks + 8 * hf;
-            a = *reinterpret_cast<const f32x4*>(qr);
-            c = *reinterpret_cast<const f32x4*>(qr + 4);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            qv[ks][e] = a[e] * scale;
-            qv[ks][4 + e] = c[e] * scale;
-            mq = fmaxf(mq, fmaxf(fabsf(qv[ks][e]), fabsf(qv[ks][4 + e])));
-        }
-    }
-    const float sq = pow2_scale(wave_max(mq));
     f16x8 qf[4][2];
+    {
+        float qv[4][8];
+        float mq = 0.0f;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) split8_h(qv[ks], sq, qf[ks][0], qf[ks][1]);
+        for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                qv[ks][e] = qok ? qa[ks][0][e] * scale : 0.0f;
+                qv[ks][4 + e] = qok ? qa[ks][1][e] * scale : 0.0f;
+                mq = fmaxf(mq, fmaxf(fabsf(qv[ks][e]), fabsf(qv[ks][4 + e])));
+            }
+        }
+        const float sq = pow2_scale(wave_max(mq));
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) split8_h(qv[ks], sq, qf[ks][0], qf[ks][1]);
+        if (lane == 0) mlx[0][0][wave] = sq;  // (read back below: keeps sq out of the chunk loop's registers)
+    }
     __syncthreads();
     mk = red[0][0];
     mv = red[1][0];
 #pragma unroll
-    for (int w = 1; w < 8; ++w) {
+    for (int w = 1; w < NWV; ++w) {
         mk = fmaxf(mk, red[0][w]);
         mv = fmaxf(mv, red[1][w]);
     }
     const float sk = pow2_scale(mk), sv = pow2_scale(mv);
+    const float us = 1.0f / (sk * mlx[0][0][wave]);  // S^T accumulator -> scores (exact)
     // K planes (rows as loaded) and V^T planes (keys permuted inside each 16: see above)
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-        const int idx = tid + q * 512;
+        if (ATTN_DIAG & 2) break;
+        const int idx = tid + q * 1024;
         const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
         typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
         f16x4 h0, h1;
@@ -638,8 +691,7 @@ __global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __
             Vt[VPL + (c + e) * VLD + pr] = (_Float16)(t - (float)a0);
         }
     }
-    const float us = 1.0f / (sk * sq);                // S^T accumulator -> scores (exact)
-    const float uo = 1.0f / (16384.0f * sv);          // O^T accumulator -> P V (exact)
+    const float uo = 1.0f / (16384.0f * sv);  // O^T accumulator -> P V (exact)
     f32x16 o[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -647,32 +699,91 @@ __global__ __launch_bounds__(512) void attention_t256_h16_kernel(const float* __
         for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
     float m = -INFINITY, l = 0.f;
     __syncthreads();
+    const bool active = task >= 0 && qw < T;
     const int kend = min(T - 1, qw + 31);
-    if (qw < T) {
+    if (active) {
+        // the tile's chunks kstart, kstart + 32, .., <= kend: half 0 the first ceil(n / 2), half 1 the rest
         const int kstart = max(0, qw - window + 1) & ~31;
-        for (int c0 = kstart; c0 <= kend; c0 += 32) {
+        const int n = (kend - kstart) / 32 + 1, n0 = (n + 1) >> 1;
+        const int cb = kstart + (kh ? 32 * n0 : 0), ce = kstart + 32 * (kh ? n : n0);
+        for (int c0 = cb; c0 < ce; c0 += 32) {
+            if (ATTN_DIAG & 1) break;
             attn_chunk_h16<KLD, KPL, VLD, VPL>(o, m, l, qf, Ks + c0 * KLD, Vt + c0, c0, qw, qi, kend, window, hf,
                                                col, us);
         }
     }
-    __syncthreads();  // K / V dead: the output staging reuses the LDS
-    float* ow = reinterpret_cast<float*>(lds) + wave * 32 * LDO;
-    const float inv = (l > 0.f) ? uo / l : 0.f;
+    __syncthreads();  // K / V dead: the merge and the output staging reuse the LDS
+    float* mo = reinterpret_cast<float*>(lds);
+    if (active && kh == 1 && !(ATTN_DIAG & 4)) {
+        float* dst = mo + qt * 32 * 64;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
-            ow[col * LDO + d] = o[t][r] * inv;
+            for (int r = 0; r < 16; ++r) dst[(t * 16 + r) * 64 + lane] = o[t][r];
+        if (hf == 0) {
+            mlx[qt][0][col] = m;
+            mlx[qt][1][col] = l;
         }
+    }
+    __syncthreads();
+    if (active && kh == 0) {
+        // merge with the half-1 task (none, or no chunks: m1 = -inf, c1 = 0, c0 = exp(0) = 1 -- o unchanged)
+        float m1 = -INFINITY, l1 = 0.0f;
+        const int n = (ATTN_DIAG & 4) ? 1 : (kend - (max(0, qw - window + 1) & ~31)) / 32 + 1;
+        if (n > 1) {
+            m1 = mlx[qt][0][col];
+            l1 = mlx[qt][1][col];
+        }
+        const float mm = fmaxf(m, m1);
+        const float c0 = (m == -INFINITY) ? 0.f : __expf(m - mm);
+        const float c1 = (m1 == -INFINITY) ? 0.f : __expf(m1 - mm);
+        l = l * c0 + l1 * c1;
+        const float* src = mo + qt * 32 * 64;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float o1 = n > 1 ? src[(t * 16 + r) * 64 + lane] : 0.0f;
+                o[t][r] = o[t][r] * c0 + o1 * c1;
+            }
+        // staging [tile][32 queries][LDO] behind the merge region
+        float* ow = mo + 8 * 32 * 64 + qt * 32 * LDO;
+        const float inv = (l > 0.f) ? uo / l : 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+                ow[col * LDO + d] = o[t][r] * inv;
+            }
+    }
+    __syncthreads();
+    // every wave stores 16 queries of a staged tile (wave w: tile w >> 1, queries 16 (w & 1) ..): lane = query
+    // 8 s + (lane >> 3) x dims 8 (lane & 7) .. +7, one 16-B store per plane (conflict-free staging reads)
     float mx = 0.0f;
-    for (int qq = 0; qq < 32; ++qq) {
-        const int q = qw + qq;
-        if (q < T)
-            store_act(nullptr, outp, pstride, 2, ((long long)b * Ts + q) * (H * D) + h * D + lane, ow[qq * LDO + lane],
-                      oscale, &mx);
+    const int st = wave >> 1;
+    if (attn_tile_in_wg(qg, (int)blockIdx.z, st)) {
+        const float* ows = mo + 8 * 32 * 64 + st * 32 * LDO;
+        const int d8 = (lane & 7) * 8;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int qq = 16 * (wave & 1) + 8 * s2 + (lane >> 3);
+            const int q = st * 32 + qq;
+            if (q < T) {
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = ows[qq * LDO + d8 + e];
+                store_act8(outp, pstride, 2, ((long long)b * Ts + q) * (H * D) + h * D + d8, v, oscale, &mx);
+            }
+        }
     }
     amax_commit(oamax, mx);
+}
+
+// query-tile groups per (item, head) for the T <= 256 kernel: enough workgroups to cover the CUs
+static int attn_qg(int batch, int H) {
+    const long long pairs = (long long)batch * H;
+    return pairs >= 256 ? 1 : pairs >= 128 ? 2 : 4;
 }
 
 // T > 256 (clips over 10.24 s) on the fp16 matrix cores: a workgroup = 128 queries of one (batch item, head), 4
@@ -852,8 +963,9 @@ hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int 
     if (tlen) {  // ragged batch: each item the kernel it would run alone (each exits on the other's items)
         if (!h16 || !(oscale > 0.0f && outns == 2) || max_tlen > T || min_tlen < 1) return hipErrorInvalidValue;
         if (min_tlen <= 256) {
-            hipLaunchKernelGGL(attention_t256_h16_kernel, dim3(H, batch), dim3(512), 0, s, qkv, T, H, window, scale,
-                               outp, out_pstride, oscale, oamax, tlen);
+            const int qg = attn_qg(batch, H);
+            hipLaunchKernelGGL(attention_t256_h16_kernel, dim3(H, batch, qg), dim3(1024), 0, s, qkv, T, H, window,
+                               scale, outp, out_pstride, oscale, oamax, tlen, qg);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -865,8 +977,9 @@ hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int 
     // (the banded kernel at T <= 256 measured slower at B = 1 and B = 32: profiles/r2d_ab_attention_band.log)
     if (h16 && T <= 256) {  // fp16-plane output (the engine's plane path at these lengths)
         if (!(oscale > 0.0f && outns == 2)) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(attention_t256_h16_kernel, dim3(H, batch), dim3(512), 0, s, qkv, T, H, window, scale, outp,
-                           out_pstride, oscale, oamax, nullptr);
+        const int qg = attn_qg(batch, H);
+        hipLaunchKernelGGL(attention_t256_h16_kernel, dim3(H, batch, qg), dim3(1024), 0, s, qkv, T, H, window, scale,
+                           outp, out_pstride, oscale, oamax, nullptr, qg);
         return hipGetLastError();
     }
     if (h16) {  // T > 256: fp16-plane output, or fp32 for clips too long for the plane buffers

@@ -167,6 +167,18 @@ int main(int argc, char** argv) {
         {"pair PERSIST DIAG nodma", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NODMA, true>, 64, 12, true},
         {"pair PERSIST DIAG nomma", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NOMMA, true>, 64, 12, true},
         {"pair PERSIST DIAG both", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NODMA | FL_DIAG_NOMMA, true>, 64, 12, true},
+        // transformer tiles (qkv: 8w+4ld s2; fc1: 8w s2; o_proj / fc2: 8w+4ld s3) with the DMA refills or the MFMAs removed
+        {"T 128x128 8w+4ld s2 DIAG nodma", launch_pl<128, 128, 4, 2, 2, 2, 4, 32, 16, FL_DIAG_NODMA, true>, 32, 12},
+        {"T 128x128 8w+4ld s2 DIAG nomma", launch_pl<128, 128, 4, 2, 2, 2, 4, 32, 16, FL_DIAG_NOMMA, true>, 32, 12},
+        {"T 128x128 8w+4ld s2 DIAG both", launch_pl<128, 128, 4, 2, 2, 2, 4, 32, 16, FL_DIAG_NODMA | FL_DIAG_NOMMA, true>, 32, 12},
+        {"T 128x128 8w s2 DIAG nodma", launch_pl<128, 128, 4, 2, 2, 2, 0, 32, 16, FL_DIAG_NODMA, true>, 32, 12},
+        {"T 128x128 8w s2 DIAG nomma", launch_pl<128, 128, 4, 2, 2, 2, 0, 32, 16, FL_DIAG_NOMMA, true>, 32, 12},
+        {"T 128x128 8w+4ld s3 DIAG nodma", launch_pl<128, 128, 4, 2, 2, 3, 4, 32, 16, FL_DIAG_NODMA, true>, 32, 12},
+        {"T 128x128 8w+4ld s3 DIAG nomma", launch_pl<128, 128, 4, 2, 2, 3, 4, 32, 16, FL_DIAG_NOMMA, true>, 32, 12},
+        {"T 128x128 8w+4ld s4", launch_pl<128, 128, 4, 2, 2, 4, 4, 32, 16, 0, true>, 32, 12},
+        {"T 256x128 8w+4ld s2", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, 0, true>, 32, 12},
+        {"T 128x256 8w+4ld s2", launch_pl<128, 256, 2, 4, 2, 2, 4, 32, 16, 0, true>, 32, 12},
+        {"T 256x256 8w+4ld s2", launch_pl<256, 256, 4, 2, 2, 2, 4, 32, 16, 0, true>, 32, 12},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
