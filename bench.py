@@ -294,6 +294,21 @@ def roofline_from_profile(prof, steps):
     whole = {"device_ms_per_step": round(tot_ms / steps, 3),
              "tflops_fp32_equivalent": round(tot_fl / (tot_ms / 1000) / 1e12, 2),
              "frac_f16x3_peak": round(tot_fl / (tot_ms / 1000) / 1e12 / F16X3_PEAK_TFLOPS, 4)}
+    # the other heavy kernels against their own ceilings (the dominant one is `roof`): by device time per step
+    top = []
+    for name, k in sorted(per_kernel.items(), key=lambda kv: -kv[1]["ms"])[:8]:
+        t = k["ms"] / 1000.0 / k["launches"]
+        e = {"kernel": name, "stages": k["stages"], "ms_per_step": round(k["ms"] / steps, 3),
+             "avg_launch_ms": round(1000 * t, 4)}
+        if k["flops"] > 0:
+            pk, _ = mfma_peak_for(name)
+            a = k["flops"] / k["launches"] / t / 1e12
+            e.update({"achieved_tflops": round(a, 1), "peak_tflops": round(pk, 1), "frac": round(a / pk, 4)})
+        else:
+            a = k["bytes"] / k["launches"] / t / 1e9
+            e.update({"achieved_GBps": round(a, 1), "frac_hbm_peak": round(a / HBM_PEAK_GBS, 4)})
+        top.append(e)
+    whole["top_kernels"] = top
     return roof, whole, pmc_path
 
 
@@ -590,10 +605,13 @@ def main():
         roof, whole, pmc_path = roofline_from_profile(prof, args.steps)
         result["roofline"] = roof
         result["whole_encode"] = whole
-        stages = {}
+        stages, sflops = {}, {}
         for s_, v in prof.items():  # per stage, summed over the kernel symbols that run it
             stages[s_.split("#")[0]] = stages.get(s_.split("#")[0], 0.0) + v["ms"] / args.steps
+            sflops[s_.split("#")[0]] = sflops.get(s_.split("#")[0], 0.0) + v["flops"] / args.steps
         result["stages_ms_per_step"] = {s_: round(v, 3) for s_, v in stages.items()}
+        result["stages_tflops"] = {s_: round(sflops[s_] / (v / 1e3) / 1e12, 1) for s_, v in stages.items()
+                                   if sflops[s_] > 0 and v > 0}
         result["north_star"] = north_star_groups(prof, args.steps, pmc_path)
     if args.bpe and wl.kind == "mls":
         result.update(train_bpe_over_codes(args, wl, dist, rank, world, dev.index, elapsed))
