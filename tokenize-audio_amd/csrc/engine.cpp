@@ -917,15 +917,26 @@ struct Workspace {
 // every kernel reads only its item's valid rows (the rest read as zero: the item's own extra padding) and
 // computes / stores / max-reduces only its valid rows.  The per-item lengths of every stage live in one small
 // device table, stage-major: T[0..4][B] (conv0 / down-conv outputs), T25[B], F[B] (12.5 Hz frames), then the
-// fused blocks' tile prefixes st0[B + 1], st1[B + 1] (32-step tiles over T[0] / T[1]).
+// fused blocks' tile prefixes st0[B + 1], st1[B + 1] (32-step tiles over T[0] / T[1]), then the transformer
+// section's PACKED row layout: toff[B] (item b's first row: the items' 25 Hz frames back to back, R rows in all).
+// Behind the table, in the workspace only, rpos[R]: the position of each packed row inside its item (RoPE), written
+// on the device from toff (launch_ragged_rows) -- the host table stays a few hundred bytes.
 struct RaggedTable {
     enum { NST = 7 };
     int B = 0;
+    int64_t R = 0;                // packed transformer rows: sum of the items' 25 Hz frames
     std::vector<StagePlan> plan;  // per item
     std::vector<int64_t> len;     // samples per item
     int minT25 = 0, maxT25 = 0;
-    static size_t ints(int B) { return (size_t)NST * B + 2 * ((size_t)B + 1); }
+    static size_t ints(int B) { return (size_t)NST * B + 2 * ((size_t)B + 1) + (size_t)B; }  // the host table
+    static size_t toff_at(int B) { return (size_t)NST * B + 2 * ((size_t)B + 1); }
     void fill(int* h) const {  // the device image (host side)
+        int* toff = h + toff_at(B);
+        int64_t r = 0;
+        for (int b = 0; b < B; ++b) {
+            toff[b] = (int)r;
+            r += plan[b].frames25;
+        }
         for (int b = 0; b < B; ++b) {
             for (int st = 0; st < 5; ++st) h[st * B + b] = (int)plan[b].T[st];
             h[5 * B + b] = (int)plan[b].frames25;
@@ -991,7 +1002,7 @@ static size_t ws_layout(const mimi_engine* e, int B, const StagePlan& p, Workspa
                             rvq_work_bytes((long long)p.frames12 * B) / sizeof(float),
                             act(xemax * B),
                             act(xemax / 2 * B),
-                            ragged ? RaggedTable::ints(B) : 0};
+                            ragged ? RaggedTable::ints(B) + (size_t)B * p.frames25 : 0};  // (+ rpos)
     size_t off = 0;
     float* rgp = nullptr;
     float** ptrs[] = {&w->x, &w->y, &w->t0, &w->t1, &w->qkv, &w->att, &w->ff, &w->dsout, &w->proj, &w->rvq,
@@ -1256,6 +1267,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     const int* dT[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     const int *dT25 = nullptr, *dF = nullptr;
     const unsigned *dst0 = nullptr, *dst1 = nullptr;
+    const int *dToff = nullptr, *dRpos = nullptr;  // the transformer section's packed rows (RaggedTable)
     if (rg) {
         if (!rg_pinned || rg->B != B || !w.rg) return set_err(MIMI_ERR_STATE, "ragged encode without its length table");
         HIP_TRY(hipMemcpyAsync(w.rg, rg_pinned, RaggedTable::ints(B) * sizeof(int), hipMemcpyHostToDevice, s));
@@ -1264,6 +1276,9 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         dF = w.rg + 6 * B;
         dst0 = reinterpret_cast<const unsigned*>(w.rg + RaggedTable::NST * B);
         dst1 = dst0 + B + 1;
+        dToff = w.rg + RaggedTable::toff_at(B);
+        dRpos = w.rg + RaggedTable::ints(B);
+        LAUNCH_TRY(launch_ragged_rows(w.rg + 5 * B, dToff, B, w.rg + RaggedTable::ints(B), s), "ragged rows");
     }
     // (profile bookkeeping) a GEMM's algorithmic FLOPs over the items' valid rows
     auto rows_of = [&](int st, double uniform) { return rg ? rg->rows(st) : uniform; };
@@ -1452,17 +1467,22 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     GemmArgs af = conv_args(e->final_conv, w.x, p.T[c.num_ratios], w.t0, T, B);
     if (ns) planes_in(af, w.x, (long long)B * p.T[c.num_ratios] * C);
     use_h(af, e->final_conv.wh, e->final_conv.wscale, xact);
-    if (rg) {
+    if (rg) {  // ragged: the output rows packed (item b's frames from row toff[b] on) for the transformer section
         af.a_rows = dT[c.num_ratios];
         af.m_rows = dT25;
+        af.c_boff = dToff;
     }
     LAUNCH_TRY(launch_gemm(ROLE_FINAL, af, s, &kname, prec), "final");
     const double rT25 = rows_of(5, (double)B * p.frames25) / ((double)B * p.frames25);  // ragged share of the rows
     rec.mark("final", gemm_flops(af) * rT25, gemm_bytes(af, false), kname);
-    if ((rc = save_tap(e, "encoder", w.t0, B, T, Hd, s))) return rc;
-
     // ---- transformer (x in t0) ----
-    const int64_t rows = (int64_t)B * T;
+    // rows: B x T, or for a ragged batch the items' frames PACKED back to back (R rows): every row-local stage
+    // (LayerNorm, q/k/v, o_proj, fc1, fc2) then runs the uniform kernels over exactly the valid rows -- no per-item
+    // tiles half empty -- and computes each row with the same instruction sequence as the per-item form; attention
+    // and the downsample address the items through toff, RoPE takes each row's position from rpos
+    const int64_t rows = rg ? rg->R : (int64_t)B * T;
+    const int64_t tapB = rg ? 1 : B, tapT = rg ? rg->R : T;  // (ragged taps of the transformer section: packed)
+    if ((rc = save_tap(e, "encoder", w.t0, tapB, tapT, Hd, s))) return rc;
     const int H = c.num_attention_heads, Dh = c.head_dim;
     // f16x3: downsample + input projections on fp16 planes too (zero-padded GEMM + replicate-edge fix)
     const bool ds_planes = h16 && e->ds_fix && e->inproj_h && c.downsample_kernel == 4 && c.downsample_stride == 2;
@@ -1478,23 +1498,12 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     } else {
         att_flops = att_fl(T) * B;
     }
-    // ragged: the row-local transformer GEMMs run per item (batch B, M = T rows each, the valid ones per item) --
-    // the same instruction sequence per output as the flattened [B x T] form
-    auto per_item = [&](GemmArgs& a, int64_t Mi, int Kd, int Nd, const int* valid) {
-        if (!rg) return;
-        a.batch = B;
-        a.M = (int)Mi;
-        a.a_bstride = Mi * Kd;
-        a.c_bstride = Mi * Nd;
-        a.a_len = Mi * Kd;
-        a.a_rows = a.m_rows = valid;
-    };
     for (int l = 0; l < c.num_hidden_layers; ++l) {
         const DevXfmr& x = e->xf[l];
         const long long nact = rows * Hd;
         const Act t1a = new_act(nmf("xf%d.ln1", l));
         LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1a.scale,
-                                    t1a.amax, rg ? dT25 : nullptr, (int)T),
+                                    t1a.amax),
                    "ln1");
         rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
         GemmArgs aq = linear_args(w.t1, T, Hd, x.wqkv, 3 * H * Dh, w.qkv);
@@ -1505,37 +1514,43 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         aq.rope_cos = e->rope_cos;
         aq.rope_sin = e->rope_sin;
         aq.rope_cols = 2 * H * Dh;
+        if (rg) {  // packed rows: one flat GEMM, RoPE positions from rpos
+            aq = linear_args(w.t1, rows, Hd, x.wqkv, 3 * H * Dh, w.qkv);
+            aq.Wsplit = x.wqkv_s;
+            aq.rope_cos = e->rope_cos;
+            aq.rope_sin = e->rope_sin;
+            aq.rope_cols = 2 * H * Dh;
+            aq.rope_pos = dRpos;
+        }
         if (ns) planes_in(aq, w.t1, nact);
         use_h(aq, x.wqkv_h, x.wqkv_hs, t1a);
-        if (rg) aq.a_rows = aq.m_rows = dT25;
         LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, prec), "qkv");
-        rec.mark("qkv", gemm_flops(aq) * rT25, gemm_bytes(aq, false), kname);
-        if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, B, T, 3 * H * Dh, s))) return rc;
+        rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
+        if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, tapB, tapT, 3 * H * Dh, s))) return rc;
         const Act atta = new_act(nmf("xf%d.att", l));
         // fp16-plane attention in f16x3 mode (also for the no-plane long clips: the same arithmetic as their
         // prefixes); true fp32 in f32 mode and the bf16 modes
         const bool ah16 = prec == PREC_F16X3;
         LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh), s,
                                     w.att, nact, ns, atta.scale, atta.amax, ah16, rg ? dT25 : nullptr,
-                                    rg ? rg->maxT25 : 0, rg ? rg->minT25 : 0),
+                                    rg ? rg->maxT25 : 0, rg ? rg->minT25 : 0, dToff),
                    "attention");
         rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4,
                  ah16 ? (T <= 256 ? "mimi::attention_t256_h16_kernel" : "mimi::attention_band_h16_kernel")
                      : (T <= 256 ? "mimi::attention_t256_kernel" : "mimi::attention_kernel"));
-        if ((rc = save_tap_planes(e, nmf("att%d", l).c_str(), w.att, ns, B, T, H * Dh, s, atta.scale))) return rc;
+        if ((rc = save_tap_planes(e, nmf("att%d", l).c_str(), w.att, ns, tapB, tapT, H * Dh, s, atta.scale))) return rc;
         GemmArgs ao = linear_args(w.att, rows, H * Dh, x.wo, Hd, w.t0);
         ao.Wsplit = x.wo_s;
         ao.R = w.t0;
         ao.scale = x.ls1;
         if (ns) planes_in(ao, w.att, nact);
         use_h(ao, x.wo_h, x.wo_hs, atta);
-        per_item(ao, T, H * Dh, Hd, dT25);
         LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
-        rec.mark("o_proj", gemm_flops(ao) * rT25, gemm_bytes(ao, true), kname);
-        if ((rc = save_tap(e, nmf("oproj%d", l).c_str(), w.t0, B, T, Hd, s))) return rc;
+        rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
+        if ((rc = save_tap(e, nmf("oproj%d", l).c_str(), w.t0, tapB, tapT, Hd, s))) return rc;
         const Act t1b = new_act(nmf("xf%d.ln2", l));
         LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1b.scale,
-                                    t1b.amax, rg ? dT25 : nullptr, (int)T),
+                                    t1b.amax),
                    "ln2");
         rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
         GemmArgs a1 = linear_args(w.t1, rows, Hd, x.w1, c.intermediate_size, w.ff);
@@ -1550,10 +1565,9 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             ffa = new_act(nmf("xf%d.ff", l));
             out_act(a1, ffa);
         }
-        per_item(a1, T, Hd, c.intermediate_size, dT25);
         LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, prec), "fc1");
-        rec.mark("fc1", gemm_flops(a1) * rT25, gemm_bytes(a1, false), kname);
-        if ((rc = save_tap_planes(e, nmf("ff%d", l).c_str(), w.ff, ns, B, T, c.intermediate_size, s, ffa.scale)))
+        rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
+        if ((rc = save_tap_planes(e, nmf("ff%d", l).c_str(), w.ff, ns, tapB, tapT, c.intermediate_size, s, ffa.scale)))
             return rc;
         GemmArgs a2 = linear_args(w.ff, rows, c.intermediate_size, x.w2, Hd, w.t0);
         a2.Wsplit = x.w2_s;
@@ -1567,11 +1581,10 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             dsin = new_act("ds.in");
             out_act(a2, dsin);
         }
-        per_item(a2, T, c.intermediate_size, Hd, dT25);
         LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname, prec), "fc2");
-        rec.mark("fc2", gemm_flops(a2) * rT25, gemm_bytes(a2, true), kname);
+        rec.mark("fc2", gemm_flops(a2), gemm_bytes(a2, true), kname);
         snprintf(nm, sizeof nm, "xfmr%d", l);
-        if ((rc = save_tap(e, nm, w.t0, B, T, Hd, s))) return rc;
+        if ((rc = save_tap(e, nm, w.t0, tapB, tapT, Hd, s))) return rc;
     }
 
     // ---- downsample (replicate pad) + input projections + RVQ ----
@@ -1585,15 +1598,16 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         dsouta = new_act("ds.out");
         out_act(ad, dsouta);
     }
-    if (rg) {
+    if (rg) {  // the packed encoder output in, per-item frames out
         if (!ds_planes) return set_err(MIMI_ERR_UNSUPPORTED, "ragged: planes downsample only");
         ad.a_rows = dT25;
         ad.m_rows = dF;
+        ad.a_boff = dToff;
     }
     LAUNCH_TRY(launch_gemm(ROLE_DOWNSAMPLE, ad, s, &kname, prec), "downsample");
     if (ds_planes)
         LAUNCH_TRY(launch_ds_edge_fix(w.t0, e->ds_fix, w.dsout, w.att, ad.c_pstride, dsouta.scale, dsouta.amax, B,
-                                      (int)T, (int)T2, Hd, Hd, s, rg ? dT25 : nullptr, rg ? dF : nullptr),
+                                      (int)T, (int)T2, Hd, Hd, s, rg ? dT25 : nullptr, rg ? dF : nullptr, dToff),
                    "downsample edges");
     const double rF = rows_of(6, (double)B * T2) / ((double)B * T2);
     rec.mark("downsample", gemm_flops(ad) * rF, gemm_bytes(ad, false), kname);
@@ -1604,7 +1618,15 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         planes_in(ap, w.att, (long long)B * T2 * Hd);
         use_h(ap, e->inproj_h, e->inproj_hs, dsouta);
     }
-    per_item(ap, T2, Hd, 2 * Dq, dF);
+    if (rg) {  // ragged: per item (batch B, M = T2 frames each, the valid ones per item) -- the same instruction
+               // sequence per output as the flattened [B x T2] form
+        ap.batch = B;
+        ap.M = (int)T2;
+        ap.a_bstride = T2 * Hd;
+        ap.c_bstride = T2 * 2 * Dq;
+        ap.a_len = T2 * Hd;
+        ap.a_rows = ap.m_rows = dF;
+    }
     LAUNCH_TRY(launch_gemm(ROLE_INPROJ, ap, s, &kname, ds_planes ? PREC_F16X3 : PREC_F32), "input_proj");
     rec.mark("input_proj", gemm_flops(ap) * rF, gemm_bytes(ap, false), kname);
     if ((rc = save_tap(e, "proj", w.proj, B, T2, 2 * Dq, s))) return rc;
@@ -1969,6 +1991,7 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
         for (const auto& pb : rt.plan) {
             rt.minT25 = std::min<int>(rt.minT25, (int)pb.frames25);
             rt.maxT25 = std::max<int>(rt.maxT25, (int)pb.frames25);
+            rt.R += pb.frames25;
         }
         const size_t need = RaggedTable::ints(B) * sizeof(int);
         if (P->rg_cap < need) {

@@ -190,6 +190,13 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
         }
     };
     auto a_len_of = [&](int b) { return RG ? (long long)p.a_rows[b] * p.a_cin : p.a_len; };
+    // item b's first A / C element (ragged batches with packed rows: a_boff / c_boff)
+    auto a_base_of = [&](int b) {
+        return (RG && p.a_boff) ? (long long)p.a_boff[b] * p.a_cin : (long long)b * p.a_bstride;
+    };
+    auto c_base_of = [&](int b) {
+        return (RG && p.c_boff) ? (long long)p.c_boff[b] * p.ldc : (long long)b * p.c_bstride;
+    };
 
     if constexpr (LW > 0) {
         // Warp-specialised: the loading waves run their own tile loop, meeting the compute waves at the same
@@ -214,7 +221,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                     int b, mt, nt;
                     decode(tile, b, mt, nt);
                     const int m0 = mt * BM, n0 = nt * BN;
-                    const __bf16* __restrict__ Abase = reinterpret_cast<const __bf16*>(p.Ap) + (long long)b * p.a_bstride;
+                    const __bf16* __restrict__ Abase = reinterpret_cast<const __bf16*>(p.Ap) + a_base_of(b);
 #pragma unroll
                     for (int pl = 0; pl < NS; ++pl)
                         arsrc[pl] = make_rsrc(Abase + (long long)pl * p.a_pstride, a_len_of(b) * 2);
@@ -298,7 +305,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
 
     // ---- DMA sources for this lane (RPP rows x CPR chunks per piece; lane -> row lane/CPR, chunk lane%CPR)
     const int prow = lane / CPR, pch = lane % CPR;
-    const __bf16* __restrict__ Abase = reinterpret_cast<const __bf16*>(p.Ap) + (long long)b * p.a_bstride;
+    const __bf16* __restrict__ Abase = reinterpret_cast<const __bf16*>(p.Ap) + a_base_of(b);
     __amdgpu_buffer_rsrc_t arsrc[NS];
 #pragma unroll
     for (int pl = 0; pl < NS; ++pl) arsrc[pl] = make_rsrc(Abase + (long long)pl * p.a_pstride, a_len_of(b) * 2);
@@ -471,7 +478,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     __syncthreads();  // every wave is done with the ring
     if (compute) {
     float* stg = reinterpret_cast<float*>(lds + PFS) + wave * (RW * LDE);
-    const float* __restrict__ Rb = p.R ? p.R + (long long)b * p.c_bstride : nullptr;
+    const float* __restrict__ Rb = p.R ? p.R + c_base_of(b) : nullptr;
     const int rbase = m0 + wm * RW;
     const int cbase = n0 + wn * CW + (lane & (MF - 1));
     const float us = F16 ? p.unscale : 1.0f;  // 1 / (activation scale x weight scale): exact power of two
@@ -510,8 +517,9 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                         // head_dim = 64: the pair (d, d + 32) sits in tiles j, j + 32/MF of the same lane
                         constexpr int PJ = 32 / MF;
                         const int d = col % 64;
-                        const float c = p.rope_cos[(long long)row * 32 + (d & 31)];
-                        const float sn = p.rope_sin[(long long)row * 32 + (d & 31)];
+                        const int pos = p.rope_pos ? p.rope_pos[row] : row;  // packed rows: the item's own position
+                        const float c = p.rope_cos[(long long)pos * 32 + (d & 31)];
+                        const float sn = p.rope_sin[(long long)pos * 32 + (d & 31)];
                         if (((j / PJ) & 1) == 0) {
                             const float x2 = F16 ? acc[i][j + PJ][r] * us : acc[i][j + PJ][r];
                             v = v * c + (-x2) * sn;
@@ -525,9 +533,9 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
             }
         }
     }
-    float* __restrict__ Cb = p.C ? p.C + (long long)b * p.c_bstride : nullptr;
+    float* __restrict__ Cb = p.C ? p.C + c_base_of(b) : nullptr;
     static_assert(!F16 || ONS == 0 || ONS == 2, "fp16 output planes: 2");
-    __bf16* __restrict__ Cpb = ONS ? reinterpret_cast<__bf16*>(p.Cp) + (long long)b * p.c_bstride : nullptr;
+    __bf16* __restrict__ Cpb = ONS ? reinterpret_cast<__bf16*>(p.Cp) + c_base_of(b) : nullptr;
     constexpr int LPR = CWC / 8;  // lanes per row
     constexpr int RPS = 64 / LPR;  // rows per pass
     static_assert(RW % RPS == 0, "epilogue: a wave's tile holds whole passes of 64 lanes x 8 columns");

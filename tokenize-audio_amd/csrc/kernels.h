@@ -169,6 +169,12 @@ struct GemmArgs {
     // rows past it are neither stored nor in max|out|); null = every item has M rows / a_len elements
     const int* a_rows;
     const int* m_rows;
+    // ragged batches whose items' rows are PACKED (the transformer section: item b's rows start at row a_boff[b] /
+    // c_boff[b] of one [sum of rows][...] tensor instead of at b x a_bstride / c_bstride; FL_RAGGED kernels only)
+    const int* a_boff;  // A: item b starts at element a_boff[b] * a_cin
+    const int* c_boff;  // C / Cp / R: item b starts at row c_boff[b] (element c_boff[b] * ldc)
+    // EPI_ROPE over packed rows: the RoPE position of output row m (null: m itself)
+    const int* rope_pos;
 };
 
 // Launch the GEMM for a given conv/linear role (the role picks tile shape and template flags).
@@ -266,7 +272,8 @@ hipError_t launch_layernorm(const float* x, const float* g, const float* b, floa
 // would run alone (tlen[b] <= 256: attention_t256_h16_kernel, else the banded one)
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window,
                             float scale, hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
-                            unsigned* oamax, bool h16, const int* tlen = nullptr, int max_tlen = 0, int min_tlen = 0);
+                            unsigned* oamax, bool h16, const int* tlen = nullptr, int max_tlen = 0, int min_tlen = 0,
+                            const int* toff = nullptr);
 
 // Replicate-padding fix of the downsample conv (k = 4, s = 2) run as a zero-padded planes GEMM: per item,
 // out[0] += (W_0 + W_1) . x[0] (the 2 left pad rows replicate x[0]) and, when T is odd (one right "extra" pad
@@ -275,7 +282,10 @@ hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int 
 // tlen / flen (ragged batches): per-item T and F (T, F are then the row strides)
 hipError_t launch_ds_edge_fix(const float* x, const float* wfix, float* out, void* outp, long long out_pstride,
                               float oscale, unsigned* oamax, int B, int T, int F, int C, int N, hipStream_t s,
-                              const int* tlen = nullptr, const int* flen = nullptr);
+                              const int* tlen = nullptr, const int* flen = nullptr, const int* toff = nullptr);
+
+// ragged batches with packed transformer rows: rpos[toff[b] + t] = t for t < tlen[b]
+hipError_t launch_ragged_rows(const int* tlen, const int* toff, int B, int* rpos, hipStream_t s);
 
 // the banded fp16-plane attention at any T (tools/attn_check.hip compares it with the T <= 256 kernel)
 hipError_t launch_attention_band(const float* qkv, int batch, int T, int H, int window, float scale,

@@ -569,7 +569,8 @@ __global__ __launch_bounds__(1024) void attention_t256_h16_kernel(const float* _
                                                                   int window, float scale, void* __restrict__ outp,
                                                                   long long pstride, float oscale,
                                                                   unsigned* __restrict__ oamax,
-                                                                  const int* __restrict__ tlen, int qg) {
+                                                                  const int* __restrict__ tlen, int qg,
+                                                                  const int* __restrict__ toff) {
     constexpr int D = 64, TM = 256, LDO = D + 1, NWV = 16;
     constexpr int KLD = 72, KPL = TM * KLD;  // K planes: [256][72 halves]
     constexpr int VLD = 264, VPL = D * VLD;  // V^T planes: [64][264 halves]
@@ -590,7 +591,8 @@ __global__ __launch_bounds__(1024) void attention_t256_h16_kernel(const float* _
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hf = lane >> 5, col = lane & 31;
     const long long ld = 3LL * H * D;
-    const float* base = qkv + (long long)b * Ts * ld;
+    const long long row0 = toff ? (long long)toff[b] : (long long)b * Ts;  // the item's first row (toff: packed rows)
+    const float* base = qkv + row0 * ld;
     const int task = attn_task(qg, (int)blockIdx.z, wave);
     const int qt = task >> 1, kh = task & 1;  // (task < 0: no task -- the wave only loads)
     // K / V rows 0 .. 255 (zeros past T) and the task's Q rows -> registers, all loads in flight before the first
@@ -773,7 +775,7 @@ __global__ __launch_bounds__(1024) void attention_t256_h16_kernel(const float* _
                 float v[8];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) v[e] = ows[qq * LDO + d8 + e];
-                store_act8(outp, pstride, 2, ((long long)b * Ts + q) * (H * D) + h * D + d8, v, oscale, &mx);
+                store_act8(outp, pstride, 2, (row0 + q) * (H * D) + h * D + d8, v, oscale, &mx);
             }
         }
     }
@@ -798,7 +800,8 @@ __global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __
                                                                  int Ts, int H, int window, float scale,
                                                                  void* __restrict__ outp, long long pstride, int outns,
                                                                  float oscale, unsigned* __restrict__ oamax,
-                                                                 const int* __restrict__ tlen) {
+                                                                 const int* __restrict__ tlen,
+                                                                 const int* __restrict__ toff) {
     constexpr int D = 64, KC = 32, LDO = D + 1;
     constexpr int KLD = 72, KPL = KC * KLD;  // K planes: [32 keys][72 halves] (conflict-free b128 fragment reads)
     constexpr int VLD = 40, VPL = D * VLD;   // V^T planes: [64 dims][40 halves]
@@ -817,7 +820,8 @@ __global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hf = lane >> 5, col = lane & 31;
     const long long ld = 3LL * H * D;
-    const float* base = qkv + (long long)b * Ts * ld;
+    const long long row0 = toff ? (long long)toff[b] : (long long)b * Ts;  // the item's first row (toff: packed rows)
+    const float* base = qkv + row0 * ld;
     const int qw = q0 + 32 * wave, qi = qw + col;
     const int kstart = max(0, q0 - window + 1) & ~31;
     const int kend = min(T - 1, q0 + 127);        // the workgroup's last key
@@ -943,7 +947,7 @@ __global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __
     for (int qq = 0; qq < 32; ++qq) {
         const int q = qw + qq;
         if (q < T)
-            store_act(out, outp, pstride, outns, ((long long)b * Ts + q) * (H * D) + h * D + lane,
+            store_act(out, outp, pstride, outns, (row0 + q) * (H * D) + h * D + lane,
                       ow[qq * LDO + lane], oscale, &mx);
     }
     amax_commit(oamax, mx);
@@ -952,26 +956,27 @@ __global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __
 hipError_t launch_attention_band(const float* qkv, int batch, int T, int H, int window, float scale,
                                  hipStream_t s, void* outp, long long out_pstride, float oscale, unsigned* oamax) {
     hipLaunchKernelGGL(attention_band_h16_kernel, dim3((T + 127) / 128, H, batch), dim3(256), 0, s, qkv, nullptr, T, H,
-                       window, scale, outp, out_pstride, 2, oscale, oamax, nullptr);
+                       window, scale, outp, out_pstride, 2, oscale, oamax, nullptr, nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window, float scale,
                             hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
-                            unsigned* oamax, bool h16, const int* tlen, int max_tlen, int min_tlen) {
+                            unsigned* oamax, bool h16, const int* tlen, int max_tlen, int min_tlen,
+                            const int* toff) {
     if (D != 64 || (outns != 0 && !outp) || (outns == 0 && !out) || (oscale > 0.0f && outns != 2)) return hipErrorInvalidValue;
     if (tlen) {  // ragged batch: each item the kernel it would run alone (each exits on the other's items)
         if (!h16 || !(oscale > 0.0f && outns == 2) || max_tlen > T || min_tlen < 1) return hipErrorInvalidValue;
         if (min_tlen <= 256) {
             const int qg = attn_qg(batch, H);
             hipLaunchKernelGGL(attention_t256_h16_kernel, dim3(H, batch, qg), dim3(1024), 0, s, qkv, T, H, window,
-                               scale, outp, out_pstride, oscale, oamax, tlen, qg);
+                               scale, outp, out_pstride, oscale, oamax, tlen, qg, toff);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
         if (max_tlen > 256)
             hipLaunchKernelGGL(attention_band_h16_kernel, dim3((max_tlen + 127) / 128, H, batch), dim3(256), 0, s, qkv,
-                               out, T, H, window, scale, outp, out_pstride, outns, oscale, oamax, tlen);
+                               out, T, H, window, scale, outp, out_pstride, outns, oscale, oamax, tlen, toff);
         return hipGetLastError();
     }
     // (the banded kernel at T <= 256 measured slower at B = 1 and B = 32: profiles/r2d_ab_attention_band.log)
@@ -979,12 +984,12 @@ hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int 
         if (!(oscale > 0.0f && outns == 2)) return hipErrorInvalidValue;
         const int qg = attn_qg(batch, H);
         hipLaunchKernelGGL(attention_t256_h16_kernel, dim3(H, batch, qg), dim3(1024), 0, s, qkv, T, H, window, scale,
-                           outp, out_pstride, oscale, oamax, nullptr, qg);
+                           outp, out_pstride, oscale, oamax, nullptr, qg, nullptr);
         return hipGetLastError();
     }
     if (h16) {  // T > 256: fp16-plane output, or fp32 for clips too long for the plane buffers
         hipLaunchKernelGGL(attention_band_h16_kernel, dim3((T + 127) / 128, H, batch), dim3(256), 0, s, qkv, out, T, H,
-                           window, scale, outp, out_pstride, outns, oscale, oamax, nullptr);
+                           window, scale, outp, out_pstride, outns, oscale, oamax, nullptr, nullptr);
         return hipGetLastError();
     }
     if (T <= 256) {
@@ -1007,7 +1012,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                                                           float* __restrict__ out, void* __restrict__ outp,
                                                           long long pstride, float oscale, unsigned* __restrict__ oamax,
                                                           int Ts, int Fs, int C, int N, const int* __restrict__ tlen,
-                                                          const int* __restrict__ flen) {
+                                                          const int* __restrict__ flen, const int* __restrict__ toff) {
     const int b = blockIdx.x, edge = blockIdx.y;
     const int T = tlen ? tlen[b] : Ts, F = flen ? flen[b] : Fs;  // (Ts, Fs: the row strides)
     const bool right = (T & 1) != 0;                 // a right "extra" row exists
@@ -1023,7 +1028,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     for (int e = edge; e <= last_edge; ++e) {
         const int t = e == 0 ? 0 : T - 1;
         const float* __restrict__ wc = wfix + (long long)e * C * N + n0 + 4 * g;  // [edge][c][n]
-        const float* __restrict__ xr = x + ((long long)b * Ts + t) * C;
+        const float* __restrict__ xr = x + ((toff ? (long long)toff[b] : (long long)b * Ts) + t) * C;  // (toff: packed)
         f32x4 a = {0.f, 0.f, 0.f, 0.f};
         // 16 channels per round: all 20 loads issued before the first FMA (a plain loop let the compiler wait out
         // each load's latency in turn: 13.8 us per launch at any batch); same FMA order as the plain loop
@@ -1063,11 +1068,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 }
 hipError_t launch_ds_edge_fix(const float* x, const float* wfix, float* out, void* outp, long long out_pstride,
                               float oscale, unsigned* oamax, int B, int T, int F, int C, int N, hipStream_t s,
-                              const int* tlen, const int* flen) {
-    if (B <= 0 || T <= 0 || F <= 0 || N % 64 || C % 256 || (outp && !(oscale > 0.0f)) || (!tlen != !flen))
+                              const int* tlen, const int* flen, const int* toff) {
+    if (B <= 0 || T <= 0 || F <= 0 || N % 64 || C % 256 || (outp && !(oscale > 0.0f)) || (!tlen != !flen) ||
+        (toff && !tlen))
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(ds_edge_fix_kernel, dim3(B, 2, N / 64), dim3(256), 0, s, x, wfix, out, outp, out_pstride,
-                       oscale, oamax, T, F, C, N, tlen, flen);
+                       oscale, oamax, T, F, C, N, tlen, flen, toff);
+    return hipGetLastError();
+}
+
+// ragged batches, packed transformer rows: rpos[toff[b] + t] = t for t < tlen[b] (RoPE positions)
+__global__ __launch_bounds__(256) void ragged_rows_kernel(const int* __restrict__ tlen, const int* __restrict__ toff,
+                                                          int* __restrict__ rpos) {
+    const int b = blockIdx.x, T = tlen[b], o = toff[b];
+    for (int t = threadIdx.x; t < T; t += 256) rpos[o + t] = t;
+}
+hipError_t launch_ragged_rows(const int* tlen, const int* toff, int B, int* rpos, hipStream_t s) {
+    if (B <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ragged_rows_kernel, dim3(B), dim3(256), 0, s, tlen, toff, rpos);
     return hipGetLastError();
 }
 
