@@ -92,6 +92,10 @@ __device__ __forceinline__ int chunk_swz(int row) {
 enum : int { FL_PRIO = 2, FL_PAIR = 4, FL_PERSIST = 8, FL_KG2 = 16, FL_KG4 = 32, FL_PF = 256, FL_RAGGED = 512 };
 // tuning diagnostics (tools/gemm_bench.hip only; results are garbage): no DMA refills after the prologue / no MFMAs
 enum : int { FL_DIAG_NODMA = 64, FL_DIAG_NOMMA = 128 };
+// timing probe of an interleaved plane layout (tools/gemm_bench.hip only, results garbage): the loader waves fetch
+// 8 rows x 128 B per piece (the hi and lo 64-B segments of a row adjacent, as if stored [row][k / 32][plane][32])
+// instead of 16 rows x 64 B of one plane; same pieces per stage, same LDS writes
+enum : int { FL_DIAG_ILV = 1024 };
 
 template <int BM, int BN, int WM, int WN, int NS, int STAGES, int EPI, int OUTP, int TAG, int LW = 0, int BK = 32,
           int MF = 32, int FL = 0, bool F16 = false>
@@ -210,7 +214,9 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
             const int c = pch ^ chunk_swz<BK, MF>(prow);  // the swizzle depends on the row's low bits only
             const __bf16* __restrict__ Wp = reinterpret_cast<const __bf16*>(p.Wsplit);
             const __amdgpu_buffer_rsrc_t wrsrc = make_rsrc(Wp, (long long)NS * N * K * 2);
-            const int a_rb = RPP * p.a_rs * 2, b_rb = RPP * K * 2, b_pl = N * K * 2;
+            constexpr bool ILV = (FL & FL_DIAG_ILV) != 0;
+            const int a_rb = ILV ? 8 * p.a_rs * 4 : RPP * p.a_rs * 2, b_rb = ILV ? 8 * K * 4 : RPP * K * 2,
+                      b_pl = N * K * 2;
             auto run_loader = [&](auto Wc) {
                 constexpr int W = decltype(Wc)::value;
                 constexpr int PW = (TP - W + NLD - 1) / NLD;  // this wave's pieces per stage
@@ -224,19 +230,43 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                     const __bf16* __restrict__ Abase = reinterpret_cast<const __bf16*>(p.Ap) + a_base_of(b);
 #pragma unroll
                     for (int pl = 0; pl < NS; ++pl)
-                        arsrc[pl] = make_rsrc(Abase + (long long)pl * p.a_pstride, a_len_of(b) * 2);
-                    a_lane = (int)((p.a_off + (long long)(m0 + prow) * p.a_rs + c * 8) * 2);
-                    b_lane = ((n0 + prow) * K + c * 8) * 2;
+                        arsrc[pl] = make_rsrc(Abase + (long long)pl * p.a_pstride, a_len_of(b) * 2 * (ILV ? 2 : 1));
+                    if constexpr (ILV) {
+                        const int r8 = lane / 8, c8 = lane % 8;
+                        a_lane = (int)(((p.a_off + (long long)(m0 + r8) * p.a_rs) * 2 + c8 * 8) * 2);
+                        b_lane = ((n0 + r8) * K * 2 + c8 * 8) * 2;
+                    } else {
+                        a_lane = (int)((p.a_off + (long long)(m0 + prow) * p.a_rs + c * 8) * 2);
+                        b_lane = ((n0 + prow) * K + c * 8) * 2;
+                    }
                     ko.init(p, PAIR);
                     kimg = PAIR ? ko.s * ko.cin : 0;  // K offset of a stage's second tap
                 };
                 auto issue_w = [&](int stage) {
                     __bf16* st = lds + stage * STG;
-                    const int kb = ko.offset() * 2;
+                    const int kb = ko.offset() * 2 * (ILV ? 2 : 1);
                     ko.next();
 #pragma unroll
                     for (int q = 0; q < PW; ++q) {
                         const int j = W + q * NLD;
+                        if (ILV) {
+                            // DIAG: pieces of 8 rows x 128 B (both planes of a row), A then B, same LDS destinations
+                            if (j < TPA) {
+                                const int pl = j / (AR / RPP), rb = j % (AR / RPP);
+                                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                                    arsrc[0], (__attribute__((address_space(3))) void*)(st + pl * APL + rb * RPP * BK),
+                                    16, a_lane + j * a_rb + kb, 0, 0, 0);
+                            } else {
+                                const int jb = j - TPA;
+                                const int pi = jb / (BN / RPP), rb = jb % (BN / RPP);
+                                const int img = jb / (2 * BN / RPP), r8 = jb % (2 * BN / RPP);
+                                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                                    wrsrc,
+                                    (__attribute__((address_space(3))) void*)(st + NS * APL + pi * BPL + rb * RPP * BK),
+                                    16, b_lane + r8 * b_rb + kb + img * kimg * 4, 0, 0, 0);
+                            }
+                            continue;
+                        }
                         if (j < TPA) {
                             const int pl = j / (AR / RPP), rb = j % (AR / RPP);
                             __builtin_amdgcn_raw_ptr_buffer_load_lds(

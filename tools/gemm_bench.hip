@@ -179,6 +179,13 @@ int main(int argc, char** argv) {
         {"T 256x128 8w+4ld s2", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, 0, true>, 32, 12},
         {"T 128x256 8w+4ld s2", launch_pl<128, 256, 2, 4, 2, 2, 4, 32, 16, 0, true>, 32, 12},
         {"T 256x256 8w+4ld s2", launch_pl<256, 256, 4, 2, 2, 2, 4, 32, 16, 0, true>, 32, 12},
+        // interleaved-plane timing probe (FL_DIAG_ILV: 8 rows x 128 B pieces; results garbage)
+        {"pair PERSIST 8w+4ld s2 ILV", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_ILV, true>, 64, 12, true},
+        {"pair PERSIST DIAG nomma ILV", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NOMMA | FL_DIAG_ILV, true>, 64, 12, true},
+        {"T 128x128 8w+4ld s2 ILV", launch_pl<128, 128, 4, 2, 2, 2, 4, 32, 16, FL_DIAG_ILV, true>, 32, 12},
+        {"T 128x128 8w+4ld s3 ILV", launch_pl<128, 128, 4, 2, 2, 3, 4, 32, 16, FL_DIAG_ILV, true>, 32, 12},
+        {"T 128x128 8w+4ld s2 DIAG nomma ILV", launch_pl<128, 128, 4, 2, 2, 2, 4, 32, 16, FL_DIAG_NOMMA | FL_DIAG_ILV, true>, 32, 12},
+        {"256x128 8w+4ld s3 ILV", launch_pl<256, 128, 4, 2, 2, 3, 4, 32, 16, FL_DIAG_ILV, true>, 32, 12},
     };
     const int nv = sizeof(vars) / sizeof(vars[0]);
     hipStream_t st;
