@@ -1398,10 +1398,10 @@ __global__ __launch_bounds__(512) void rvq_level_kernel(RvqArgs p, int L) {
     }
 }
 
+template <int NSL = 2048 / RVQ_CS>
 __global__ __launch_bounds__(256) void rvq_final_kernel(RvqArgs p, int L) {
     const long long f = (long long)blockIdx.x * 256 + threadIdx.x;
     if (f >= p.frames) return;
-    constexpr int NSL = 2048 / RVQ_CS;
     const RvqWork w = rvq_work(p, NSL);
     rvq_store_code(p, L, f, rvq_merge<NSL>(w, rvq_slot(p, L), f, p.ncodes));
     if (rvq_sem_split(p) && L > 0) rvq_store_code(p, 0, f, rvq_merge<NSL>(w, rvq_slot(p, 0), f, p.ncodes));
@@ -1425,9 +1425,15 @@ constexpr int RVQ_CAND = 2048;
 // 32 frames per workgroup (64-frame tiles, which halve the per-CU codebook stream, were slower: 1 workgroup per CU,
 // profiles/r2d_rvq_ft64.log).  PF: codebook k-steps in flight per wave (4: two workgroups per CU; 16 = all of them, for small batches whose few
 // workgroups wait on L2 / Infinity-Cache latency); EX: float4 of a code row in flight per exact re-score round
-template <int D, int PF = 4, int EX = 16, bool RG = false>
+// CW: codes per wave (32, or 64 as two 32-code MFMA tiles): a slice of 8 CW codes, NSL = 2048 / (8 CW) slices.  The
+// large-batch form takes 64 (4 slices: 500 workgroups at B = 32 x 10 s -- one round of two per CU -- instead of 1000
+// in two rounds, each round paying the whole merge / residual / |r|^2 / plane prologue chain again).
+template <int D, int PF = 4, int EX = 16, bool RG = false, int CW = 32>
 // (HIP's second launch bound is waves per SIMD: 4 = two 8-wave workgroups per CU, i.e. <= 128 VGPRs)
 __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(RvqArgs p, int L0) {
+    constexpr int TNC = CW / 32;          // 32-code MFMA tiles per wave
+    constexpr int SLC = 8 * CW;           // codes per slice
+    constexpr int NSL = 2048 / SLC;       // slices
     // RG (a ragged batch: p.flen): a workgroup none of whose frames is valid has nothing to do -- no later level
     // reads what it would write (only valid frames' residuals and partial argmins are ever read)
     if constexpr (RG) {
@@ -1437,7 +1443,6 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
     constexpr int FT = 32;
     constexpr int LDH = D / 2 + 4;
     constexpr int RLD = D + 8;  // fp16 plane rows: 528 B = 132 dwords (conflict-free b128 fragment reads)
-    constexpr int NSL = 2048 / RVQ_CS;
     typedef _Float16 h8 __attribute__((ext_vector_type(8)));
     __shared__ __attribute__((aligned(16))) float img[2][FT][LDH];  // -2 r, split by k parity (exact chain)
     __shared__ __attribute__((aligned(16))) _Float16 rpl[2][FT][RLD];  // fp16 planes of r * rs
@@ -1535,64 +1540,80 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
     }
     __syncthreads();
 
-    // ---- approximate r.e for FT frames x this wave's 32 codes; the wave's 32 KB of codebook planes stream from
-    // L2 with 4 k-steps in flight
-    const int code0 = slice * RVQ_CS + wave * 32;
+    // ---- approximate r.e for FT frames x this wave's CW codes; the wave's codebook planes stream from L2 with PF
+    // k-steps in flight
+    const int code0 = slice * SLC + wave * CW;
     const h8* bp = reinterpret_cast<const h8*>(p.cb_h16) +
                    ((long long)L * (p.ncodes / 32) + code0 / 32) * (D / 16) * 2 * 64 + lane;
-    f32x16 acc;
+    constexpr int TST = (D / 16) * 2 * 64;  // h8 per 32-code block of the fragment image
+    f32x16 acc[TNC];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-    h8 bq[PF][2];
+    for (int t = 0; t < TNC; ++t)
 #pragma unroll
-    for (int q = 0; q < PF; ++q) {
-        bq[q][0] = bp[q * 128];
-        bq[q][1] = bp[q * 128 + 64];
-    }
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    h8 bq[PF][TNC][2];
+#pragma unroll
+    for (int q = 0; q < PF; ++q)
+#pragma unroll
+        for (int t = 0; t < TNC; ++t) {
+            bq[q][t][0] = bp[t * TST + q * 128];
+            bq[q][t][1] = bp[t * TST + q * 128 + 64];
+        }
     auto kstep = [&](int ks) {
         const int cur = ks % PF;
-        const h8 b0 = bq[cur][0], b1 = bq[cur][1];
+        h8 b0[TNC], b1[TNC];
+#pragma unroll
+        for (int t = 0; t < TNC; ++t) {
+            b0[t] = bq[cur][t][0];
+            b1[t] = bq[cur][t][1];
+        }
         if (ks + PF < D / 16) {
-            bq[cur][0] = bp[(ks + PF) * 128];
-            bq[cur][1] = bp[(ks + PF) * 128 + 64];
+#pragma unroll
+            for (int t = 0; t < TNC; ++t) {
+                bq[cur][t][0] = bp[t * TST + (ks + PF) * 128];
+                bq[cur][t][1] = bp[t * TST + (ks + PF) * 128 + 64];
+            }
         }
         const h8 a0 = *reinterpret_cast<const h8*>(&rpl[0][lane & 31][ks * 16 + 8 * h]);
         const h8 a1 = *reinterpret_cast<const h8*>(&rpl[1][lane & 31][ks * 16 + 8 * h]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < TNC; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0[t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1[t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0[t], acc[t], 0, 0, 0);
+        }
     };
     // (a template-dependent `#pragma unroll PF` is not honoured by hipcc -- the loop is then fully unrolled and
-    // the prefetch loads sunk to their uses -- so the two depths spell their unroll factor out)
+    // the prefetch loads sunk to their uses -- so the depths spell their unroll factor out)
     if constexpr (PF == 4) {
 #pragma unroll 4
-        for (int ks = 0; ks < D / 16; ++ks) {
-            const int cur = ks % 4;
-            const h8 b0 = bq[cur][0], b1 = bq[cur][1];
-            if (ks + 4 < D / 16) {
-                bq[cur][0] = bp[(ks + 4) * 128];
-                bq[cur][1] = bp[(ks + 4) * 128 + 64];
-            }
-            const h8 a0 = *reinterpret_cast<const h8*>(&rpl[0][lane & 31][ks * 16 + 8 * h]);
-            const h8 a1 = *reinterpret_cast<const h8*>(&rpl[1][lane & 31][ks * 16 + 8 * h]);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
-        }
+        for (int ks = 0; ks < D / 16; ++ks) kstep(ks);
+    } else if constexpr (PF == 2) {
+#pragma unroll 2
+        for (int ks = 0; ks < D / 16; ++ks) kstep(ks);
     } else {
         __builtin_amdgcn_sched_barrier(0);  // all PF k-steps' loads issued before the first MFMA
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) kstep(ks);
     }
-    const int code = code0 + (lane & 31);
-    const float yn = p.cb_norm[(long long)L * p.ncodes + code];
     const float cus = p.cb_unscale[L];
-    float ad[16];
+    float ad[TNC][16];
+    float mrow[16];
+#pragma unroll
+    for (int t = 0; t < TNC; ++t) {
+        const int code = code0 + 32 * t + (lane & 31);
+        const float yn = p.cb_norm[(long long)L * p.ncodes + code];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            ad[t][r] = (-2.0f * (acc[t][r] * (rus[row] * cus)) + xn[row]) + yn;
+            mrow[r] = t == 0 ? ad[t][r] : fminf(mrow[r], ad[t][r]);
+        }
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        ad[r] = (-2.0f * (acc[r] * (rus[row] * cus)) + xn[row]) + yn;
-        float m = ad[r];
+        float m = mrow[r];
 #pragma unroll
         for (int o = 16; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o));
         if ((lane & 31) == 0) redd[wave][row] = m;
@@ -1609,12 +1630,16 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        // NaN distances (a non-finite residual) are candidates too: the exact path decides
-        if (!(ad[r] > smin[row] + win[row]) && f0 + row < p.frames) {
-            const unsigned slot = atomicAdd(&ncand, 1u);
-            if (slot < RVQ_CAND) cand[slot] = ((unsigned)row << 16) | (unsigned)(code - slice * RVQ_CS);
+    for (int t = 0; t < TNC; ++t) {
+        const int code = code0 + 32 * t + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            // NaN distances (a non-finite residual) are candidates too: the exact path decides
+            if (!(ad[t][r] > smin[row] + win[row]) && f0 + row < p.frames) {
+                const unsigned slot = atomicAdd(&ncand, 1u);
+                if (slot < RVQ_CAND) cand[slot] = ((unsigned)row << 16) | (unsigned)(code - slice * SLC);
+            }
         }
     }
     __syncthreads();
@@ -1622,10 +1647,10 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
     const float* cbr = p.cb_rows + (long long)L * p.ncodes * D;
     const unsigned nc = ncand;
     const bool all = nc > RVQ_CAND;
-    const unsigned total = all ? FT * RVQ_CS : nc;
+    const unsigned total = all ? FT * SLC : nc;
     for (unsigned i = tid; i < total; i += 512) {
         const int row = all ? (int)(i % FT) : (int)(cand[i] >> 16);
-        const int c = slice * RVQ_CS + (all ? (int)(i / FT) : (int)(cand[i] & 0xffff));
+        const int c = slice * SLC + (all ? (int)(i / FT) : (int)(cand[i] & 0xffff));
         if (f0 + row >= p.frames) continue;
         const f32x4* e = reinterpret_cast<const f32x4*>(cbr + (long long)c * D);
         float a = 0.0f;
@@ -1666,29 +1691,35 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
     if (a.cb_h16 && a.cb_unscale && a.cb_emax) {
         // (64-frame tiles, which halve the per-CU codebook stream, measured slower at B = 32: 0.56 vs 0.42 ms for 8
         // levels -- one workgroup per CU and 16 spilled VGPRs; profiles/r2d_rvq_ft64.log)
-        // small batches (fewer workgroups than CUs): every codebook k-step in flight at once and half a code row per
-        // exact round -- the same arithmetic, latency-bound waves wait once instead of four times
-        const dim3 grid((unsigned)((a.frames + 31) / 32), 2048 / RVQ_CS);
-        const bool small = grid.x * grid.y < 256;
+        // small batches (fewer 256-code-slice workgroups than CUs): 8 slices, every codebook k-step in flight at once
+        // and half a code row per exact round -- the same arithmetic, latency-bound waves wait once instead of four
+        // times; large batches: 4 slices of 512 codes (64 per wave, 2 k-steps in flight per 32-code tile)
+        const unsigned ftiles = (unsigned)((a.frames + 31) / 32);
+        const bool small = ftiles * 8 < 256;
         const bool split = a.sem_split != 0;  // levels 0 and 1 in one launch (rvq_sem_split)
-        *kname = a.flen ? (small ? "mimi::rvq_level_h16_kernel<256, 16, 32, true>" : "mimi::rvq_level_h16_kernel<256, 4, 16, true>")
-                        : (small ? "mimi::rvq_level_h16_kernel<256, 16, 32, false>" : "mimi::rvq_level_h16_kernel<256, 4, 16, false>");
+        *kname = a.flen ? (small ? "mimi::rvq_level_h16_kernel<256, 16, 32, true, 32>" : "mimi::rvq_level_h16_kernel<256, 2, 16, true, 64>")
+                        : (small ? "mimi::rvq_level_h16_kernel<256, 16, 32, false, 32>" : "mimi::rvq_level_h16_kernel<256, 2, 16, false, 64>");
         for (int L = 0; L < a.levels; L += (split && L == 0) ? 2 : 1) {
-            const dim3 g(grid.x, grid.y, (split && L == 0) ? 2 : 1);
+            const dim3 g(ftiles, small ? 8 : 4, (split && L == 0) ? 2 : 1);
             if (a.flen) {  // ragged: workgroups of invalid frames exit (rvq_level_h16_kernel<..., RG>)
                 if (small)
-                    hipLaunchKernelGGL((rvq_level_h16_kernel<256, 16, 32, true>), g, dim3(512), 0, s, a, L);
+                    hipLaunchKernelGGL((rvq_level_h16_kernel<256, 16, 32, true, 32>), g, dim3(512), 0, s, a, L);
                 else
-                    hipLaunchKernelGGL((rvq_level_h16_kernel<256, 4, 16, true>), g, dim3(512), 0, s, a, L);
+                    hipLaunchKernelGGL((rvq_level_h16_kernel<256, 2, 16, true, 64>), g, dim3(512), 0, s, a, L);
             } else if (small) {
-                hipLaunchKernelGGL((rvq_level_h16_kernel<256, 16, 32>), g, dim3(512), 0, s, a, L);
+                hipLaunchKernelGGL((rvq_level_h16_kernel<256, 16, 32, false, 32>), g, dim3(512), 0, s, a, L);
             } else {
-                hipLaunchKernelGGL((rvq_level_h16_kernel<256>), g, dim3(512), 0, s, a, L);
+                hipLaunchKernelGGL((rvq_level_h16_kernel<256, 2, 16, false, 64>), g, dim3(512), 0, s, a, L);
             }
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(rvq_final_kernel, dim3((unsigned)((a.frames + 255) / 256)), dim3(256), 0, s, a, a.levels - 1);
+        if (small)
+            hipLaunchKernelGGL(rvq_final_kernel<8>, dim3((unsigned)((a.frames + 255) / 256)), dim3(256), 0, s, a,
+                               a.levels - 1);
+        else
+            hipLaunchKernelGGL(rvq_final_kernel<4>, dim3((unsigned)((a.frames + 255) / 256)), dim3(256), 0, s, a,
+                               a.levels - 1);
         return hipGetLastError();
     }
     // small batches (fewer 64-frame workgroups than CUs, B < 16 x 10 s): 32-frame tiles
@@ -1704,7 +1735,7 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(rvq_final_kernel, dim3((unsigned)((a.frames + 255) / 256)), dim3(256), 0, s, a, a.levels - 1);
+    hipLaunchKernelGGL(rvq_final_kernel<>, dim3((unsigned)((a.frames + 255) / 256)), dim3(256), 0, s, a, a.levels - 1);
     return hipGetLastError();
 }
 
