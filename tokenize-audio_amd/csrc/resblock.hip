@@ -736,6 +736,8 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
 // Stage 1 (C = 128, H = 64) on the fp16 matrix cores (PREC_F16X3): residual block + ELU, persistent, one
 // workgroup of 8 waves per CU walking a contiguous range of 32-step blocks.  Both weight images stay resident
 // in LDS (W3 96 KB + W1 32 KB, 16x16x32 A fragments); per block:
+// W3 (96 KB) is register-resident instead: each wave holds the 24 fragments of its M tile (96 VGPRs, loaded once), so
+// GEMM1 reads only the slab from LDS -- with W3 in LDS every block re-read 192 KB of fragments per CU.
 //   load    x[t0 .. t0+31][128] fp32, each lane 2 float4 in the GEMM2 output layout (time t = 16n + lane&15,
 //           channels 16m + 4(lane>>4) .. +3) -- they stay in registers as the identity skip; the next block's
 //           x is prefetched under this one
@@ -756,7 +758,9 @@ constexpr int SLD = 144, SROWS = BM + 2, SPL = SROWS * SLD;  // halves
 constexpr int HLD = 80, HPL = BM * HLD;
 constexpr int FR_W3 = 0, FR_W1 = 96, NFRAG = 128;  // W3 [mt 4][ks 12][pl 2], W1 [mt 8][ks 2][pl 2]
 constexpr int BIAS = H + C;                         // b3 | b1
-constexpr int LDS_BYTES = NFRAG * 1024 + 2 * SPL * 2 + 2 * HPL * 2 + BIAS * 4;
+// W3's fragments live in the waves' registers (each wave its M tile's 24: 96 VGPRs), only W1's 32 in LDS
+constexpr int LFRAG = NFRAG - FR_W1;
+constexpr int LDS_BYTES = LFRAG * 1024 + 2 * SPL * 2 + 2 * HPL * 2 + BIAS * 4;
 static_assert(NFRAG == RES1_H16_FRAGS, "fragment count");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 }  // namespace r1h
@@ -775,17 +779,17 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    _Float16* slab = reinterpret_cast<_Float16*>(lds + NFRAG * 1024);
+    _Float16* slab = reinterpret_cast<_Float16*>(lds + LFRAG * 1024);
     _Float16* hb = slab + 2 * SPL;
     float* bl = reinterpret_cast<float*>(hb + 2 * HPL);
     {
-        const uint4* src = reinterpret_cast<const uint4*>(p.wh16);
+        const uint4* src = reinterpret_cast<const uint4*>(p.wh16) + FR_W1 * 64;  // W1's fragments
         uint4* dst = reinterpret_cast<uint4*>(lds);
-        for (int i = tid; i < NFRAG * 64; i += NW * 64) dst[i] = src[i];
+        for (int i = tid; i < LFRAG * 64; i += NW * 64) dst[i] = src[i];
         if (tid < H) bl[tid] = p.b3[tid];
         if (tid < C) bl[H + tid] = p.b1[tid];
     }
-    const f16x8* wf = reinterpret_cast<const f16x8*>(lds);
+    const f16x8* wf = reinterpret_cast<const f16x8*>(lds) - FR_W1 * 64;  // (indexed by the full image's numbering)
 
     const long long T = p.T;  // row stride of x / y (and every item's length unless ragged)
     const unsigned tpi = (unsigned)((T + BM - 1) / BM);  // blocks per item (host checks B x tpi < 2^32)
@@ -800,6 +804,15 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
     const float sx = p.xscale, sh = p.hscale, sy = p.yscale;
     const float u1 = p.unscale1, u2 = p.unscale2;
     float mxx = 0.0f, mxh = 0.0f, mxy = 0.0f;
+    // this wave's W3 fragments (M tile mp: 12 K steps x 2 planes), resident for the whole launch
+    f16x8 w3r[12][2];
+    {
+        const f16x8* wg = reinterpret_cast<const f16x8*>(p.wh16);
+#pragma unroll
+        for (int ks = 0; ks < 12; ++ks)
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl) w3r[ks][pl] = wg[(FR_W3 + (mp * 12 + ks) * 2 + pl) * 64 + lane];
+    }
 
     // x of the block at (item b, step t0), step t0 + off, channels 16(2mp + i) + 4lq .. +3 (zero outside the item's
     // [0, T_b))
@@ -875,11 +888,9 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
             const int o = (16 * n + li + (ks >> 2)) * SLD + (ks & 3) * 32 + 8 * lq;
             const f16x8 bx0 = *reinterpret_cast<const f16x8*>(slab + o);
             const f16x8 bx1 = *reinterpret_cast<const f16x8*>(slab + SPL + o);
-            const f16x8 aw0 = wf[(FR_W3 + (mp * 12 + ks) * 2) * 64 + lane];
-            const f16x8 aw1 = wf[(FR_W3 + (mp * 12 + ks) * 2 + 1) * 64 + lane];
-            acc1 = mfma_h16(aw1, bx0, acc1);
-            acc1 = mfma_h16(aw0, bx1, acc1);
-            acc1 = mfma_h16(aw0, bx0, acc1);
+            acc1 = mfma_h16(w3r[ks][1], bx0, acc1);
+            acc1 = mfma_h16(w3r[ks][0], bx1, acc1);
+            acc1 = mfma_h16(w3r[ks][0], bx0, acc1);
         }
         {  // h = ELU(acc + b3): step t, hch 16 mp + 4 lq .. +3
             const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 16 * mp + 4 * lq);

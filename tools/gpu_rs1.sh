@@ -1,0 +1,14 @@
+#!/bin/bash
+set -u
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+for v in prev "" prev ""; do
+  for bt in "32 250" "1 250"; do
+    timeout -k 10 60 tools/bin/attn_check${v:+_$v} $bt > gpurun_out/ac.log 2>&1 || { echo "attn_check $v $bt failed"; cat gpurun_out/ac.log; exit 2; }
+    echo "${v:-new} $bt: $(grep 'attention_t256_h16 ' gpurun_out/ac.log | sed 's/ *attention_t256_h16 *//') $(grep 'rep 0' gpurun_out/ac.log | sed 's/.*= //;s/,.*//')"
+  done
+done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_ragged.py tests/test_stage0_fused.py -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf -x -q > gpurun_out/pytest_rs1.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_rs1.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+LIBS="base new" ROUNDS=3 KEYS="res_s1 attention rvq" bash tools/ab_libs.sh || exit 3
