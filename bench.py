@@ -207,15 +207,23 @@ def pmc_stage(pmc, stage, kernel):
     return None, None, False
 
 
-def north_star_groups(prof, steps, pmc_path):
+def load_pmc(pmc_path, workload):
+    """profiles/pmc_summary.json if its PMC passes ran this workload (per-launch bytes are workload-specific: the
+    B = 1 or ragged launches of a stage move different bytes from the B = 32 ones), else ({}, why)."""
+    if not os.path.exists(pmc_path):
+        return {}, "no profiles/pmc_summary.json"
+    with open(pmc_path) as f:
+        pmc = json.load(f)
+    if pmc.get("workload") != workload:
+        return {}, f"PMC passes ran workload {pmc.get('workload')}, not this one ({workload})"
+    return pmc, None
+
+
+def north_star_groups(prof, steps, pmc, pmc_note=None):
     """BASELINE.json's reporting asks: HBM GB/s and TFLOP/s of the SEANet conv stack, MFMA utilisation of the
     transformer.  Device ms and algorithmic FLOPs from the engine's events; HBM bytes = the PMC passes'
     FETCH_SIZE x 2 + WRITE_SIZE per launch of each STAGE (profiles/pmc_summary.json, keyed by stage; by kernel
     symbol as a fallback) x that stage's launches."""
-    pmc = {}
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            pmc = json.load(f)
     base = lambda s: s.split("#")[0]  # noqa: E731  ("fc2#2": the same stage on a second kernel symbol)
     groups = {
         "conv_stack": [s for s in prof if base(s).startswith(("res", "down_s", "final"))],
@@ -237,6 +245,8 @@ def north_star_groups(prof, steps, pmc_path):
             d["hbm_measured_on_other_kernel"] = stale
         if missing:
             d["hbm_unmeasured_stages"] = missing
+            if pmc_note:
+                d["hbm_unmeasured_why"] = pmc_note
         else:
             by = sum(b * prof[s]["launches"] / steps for (b, _, _), s in zip(looked, stages))
             d.update({"hbm_bytes_per_step": round(by), "hbm_GBps": round(by / (ms / 1e3) / 1e9, 1),
@@ -245,7 +255,7 @@ def north_star_groups(prof, steps, pmc_path):
     return out
 
 
-def roofline_from_profile(prof, steps):
+def roofline_from_profile(prof, steps, pmc, pmc_note=None):
     per_kernel = {}
     for stage, st in prof.items():
         k = per_kernel.setdefault(st["kernel"], {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "launches": 0,
@@ -267,11 +277,8 @@ def roofline_from_profile(prof, steps):
         achieved = dom["bytes"] / dom["launches"] / t_launch / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4)}
-    traffic, traffic_src = None, None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            pmc = json.load(f)
+    traffic, traffic_src = None, pmc_note
+    if pmc:
         # the dominant kernel's stages, launch-weighted
         looked = [(pmc_stage(pmc, st, dom_name), prof[st]["launches"]) for st in dom["stages"]]
         if all(b is not None for (b, _, _), _ in looked):
@@ -309,7 +316,7 @@ def roofline_from_profile(prof, steps):
             e.update({"achieved_GBps": round(a, 1), "frac_hbm_peak": round(a / HBM_PEAK_GBS, 4)})
         top.append(e)
     whole["top_kernels"] = top
-    return roof, whole, pmc_path
+    return roof, whole
 
 
 class Workload:
@@ -602,7 +609,9 @@ def main():
         result["stages_source"] = "a separate profiled pass of the same steps (timed region: hipGraph replays)"
     result["graph_replays"] = model.graph_replays
     if prof:
-        roof, whole, pmc_path = roofline_from_profile(prof, args.steps)
+        pmc, pmc_note = load_pmc(os.path.join(ROOT, "profiles", "pmc_summary.json"),
+                                 {"kind": wl.kind, "batch": args.batch, "seconds": args.seconds})
+        roof, whole = roofline_from_profile(prof, args.steps, pmc, pmc_note)
         result["roofline"] = roof
         result["whole_encode"] = whole
         stages, sflops = {}, {}
@@ -612,7 +621,7 @@ def main():
         result["stages_ms_per_step"] = {s_: round(v, 3) for s_, v in stages.items()}
         result["stages_tflops"] = {s_: round(sflops[s_] / (v / 1e3) / 1e12, 1) for s_, v in stages.items()
                                    if sflops[s_] > 0 and v > 0}
-        result["north_star"] = north_star_groups(prof, args.steps, pmc_path)
+        result["north_star"] = north_star_groups(prof, args.steps, pmc, pmc_note)
     if args.bpe and wl.kind == "mls":
         result.update(train_bpe_over_codes(args, wl, dist, rank, world, dev.index, elapsed))
     if rank == 0 and world == 1 and args.cpu_baseline_seconds > 0 and not args.pmc_pass:

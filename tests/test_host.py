@@ -126,7 +126,7 @@ def test_import_without_gpu_has_no_fallback():
 
 def test_bench_north_star_groups(tmp_path):
     """bench.py's north-star breakdown: stage grouping, PMC lookup by stage (then by bare symbol), HBM rate
-    arithmetic, and a stage measured on another build's kernel flagged."""
+    arithmetic, a stage measured on another build's kernel flagged, and PMC bytes of another workload not used."""
     import sys
     sys.path.insert(0, ROOT)
     import bench
@@ -138,7 +138,15 @@ def test_bench_north_star_groups(tmp_path):
                        "launches": 10},
             "down_s0": {"ms": 10.0, "flops": 2.5e12, "kernel": "void mimi::gemm_planes_kernel<1, 2>", "launches": 10},
             "qkv": {"ms": 5.0, "flops": 1.0e12, "kernel": "unknown", "launches": 80}}
-    g = bench.north_star_groups(prof, 10, str(p))
+    wl = {"kind": "batch", "batch": 32, "seconds": 10.0}
+    assert bench.load_pmc(str(p), wl)[0] == {}  # no workload key: not this workload's bytes
+    pmc["workload"] = wl
+    p.write_text(json.dumps(pmc))
+    other, why = bench.load_pmc(str(p), dict(wl, batch=1))
+    assert other == {} and "batch" in why
+    g0 = bench.north_star_groups(prof, 10, other, why)
+    assert "hbm_GBps" not in g0["conv_stack"] and g0["conv_stack"]["hbm_unmeasured_why"] == why
+    g = bench.north_star_groups(prof, 10, bench.load_pmc(str(p), wl)[0])
     cs = g["conv_stack"]
     assert cs["stages"] == ["res_s0", "down_s0"] and cs["ms_per_step"] == 1.7
     assert cs["hbm_bytes_per_step"] == 3_000_000_000 and abs(cs["hbm_GBps"] - 3e9 / 1.7e-3 / 1e9) < 0.1

@@ -71,6 +71,9 @@ def stage_bytes(src, seq):
     return per
 
 
+PMC_WORKLOAD = {"kind": "batch", "batch": 32, "seconds": 10.0}
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
@@ -79,7 +82,8 @@ def main(tag):
     bj = os.path.join(src, "bench_under_trace.json")
     if os.path.exists(bj):
         shutil.copy(bj, os.path.join(dst, f"{tag}_bench_under_trace.json"))
-    out = {"tag": tag, "units": "bytes per launch", "fetch_correction": 2.0,
+    # the PMC passes run bench.py's default workload (B = 32 x 10 s resident batch): per-launch bytes hold for it only
+    out = {"tag": tag, "units": "bytes per launch", "fetch_correction": 2.0, "workload": PMC_WORKLOAD,
            "note": "FETCH_SIZE (KB) x 1024 x 2 (gfx950 reports half of wide streaming reads), WRITE_SIZE (KB) x 1024;"
                    " separate --pmc passes of `bench.py --steps 2 --warmup 1`; dispatches after bench.py's spin_kernel marker"
                    " only (the finalize-time calibration encode precedes it)", "kernels": {}}
