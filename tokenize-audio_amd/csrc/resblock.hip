@@ -749,8 +749,8 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
 //   GEMM2   y^T[128][32] = W1 . h^T: wave w, tiles (ch 16(2(w>>1)+i), t 16(w&1)), 12 MFMAs
 //   out     y = ELU(x + (acc + b1)) -> planes staged over slab rows 2..33                     barrier
 //           -> 1-KB row stores (256-B rows, 4 per wave instruction)                           barrier
-// Slab rows are 288 B (72 dwords = 8 mod 64) and h rows 160 B: the 16x16x32 fragment reads (row lane&15,
-// 16-B chunk lane>>4) are conflict-free.  LDS: 128 KB weights + 19.1 KB slab + 10 KB h + biases = 157.9 KB.
+// Slab rows are 288 B (72 dwords = 8 mod 64) and h rows 160 B, 16-B chunks XOR-swizzled by row (r1h_swz): the
+// 16x16x32 fragment reads (row lane&15, 16-B chunk lane>>4) are conflict-free, the row writes 2-way.  LDS: 128 KB weights + 19.1 KB slab + 10 KB h + biases = 157.9 KB.
 // ------------------------------------------------------------------------------------------------
 namespace r1h {
 constexpr int C = 128, H = 64, BM = 32, NW = 8;
@@ -772,6 +772,13 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+}
+
+// 16-B chunk c of slab / h row r at c ^ ((r >> 2) & 1): the 16-lane groups of the ds_write_b64 row writes (16
+// consecutive rows, one 8-B piece each) 2-way instead of 4-way on the 288-B / 160-B rows, the 16x16x32 fragment
+// reads still conflict-free (MI355X_MICROARCH.md LDS banking; SQ_LDS_BANK_CONFLICT 6.1e7 per launch before)
+__device__ __forceinline__ int r1h_swz(int row, int ld, int ch) {
+    return row * ld + 8 * ((ch >> 3) ^ ((row >> 2) & 1)) + (ch & 7);
 }
 
 __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
@@ -839,7 +846,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
     auto slab_row_put = [&](int row, const uint2 (&hi)[2], const uint2 (&lo)[2]) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const int o = row * SLD + 16 * (2 * mp + i) + 4 * lq;
+            const int o = r1h_swz(row, SLD, 16 * (2 * mp + i) + 4 * lq);
             *reinterpret_cast<uint2*>(slab + o) = hi[i];
             *reinterpret_cast<uint2*>(slab + SPL + o) = lo[i];
         }
@@ -885,7 +892,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
         f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 12; ++ks) {
-            const int o = (16 * n + li + (ks >> 2)) * SLD + (ks & 3) * 32 + 8 * lq;
+            const int o = r1h_swz(16 * n + li + (ks >> 2), SLD, (ks & 3) * 32 + 8 * lq);
             const f16x8 bx0 = *reinterpret_cast<const f16x8*>(slab + o);
             const f16x8 bx1 = *reinterpret_cast<const f16x8*>(slab + SPL + o);
             acc1 = mfma_h16(w3r[ks][1], bx0, acc1);
@@ -900,7 +907,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
             elu_s4(z, sh, tt, mxh);
             uint2 hi, lo;
             split4_t(tt, hi, lo);
-            const int o = t * HLD + 16 * mp + 4 * lq;
+            const int o = r1h_swz(t, HLD, 16 * mp + 4 * lq);
             *reinterpret_cast<uint2*>(hb + o) = hi;
             *reinterpret_cast<uint2*>(hb + HPL + o) = lo;
         }
@@ -910,7 +917,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
         f32x4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            const int o = (16 * n + li) * HLD + ks * 32 + 8 * lq;
+            const int o = r1h_swz(16 * n + li, HLD, ks * 32 + 8 * lq);
             const f16x8 bh0 = *reinterpret_cast<const f16x8*>(hb + o);
             const f16x8 bh1 = *reinterpret_cast<const f16x8*>(hb + HPL + o);
 #pragma unroll
@@ -936,7 +943,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
                 elu_s4(z, sy, tt, tmy);
                 uint2 hi, lo;
                 split4_t(tt, hi, lo);
-                const int o = (2 + t) * SLD + ch;
+                const int o = r1h_swz(2 + t, SLD, ch);
                 *reinterpret_cast<uint2*>(slab + o) = hi;
                 *reinterpret_cast<uint2*>(slab + SPL + o) = lo;
             }
@@ -948,7 +955,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
             for (int k = 0; k < 2; ++k) {
                 const int idx = tid + k * NW * 64;
                 const int pl = idx >> 9, r = (idx >> 4) & 31, c = (idx & 15) * 8;
-                const uint4 v = *reinterpret_cast<const uint4*>(slab + pl * SPL + (2 + r) * SLD + c);
+                const uint4 v = *reinterpret_cast<const uint4*>(slab + pl * SPL + r1h_swz(2 + r, SLD, c));
                 if (t0 + r < Tb)
                     *reinterpret_cast<uint4*>(reinterpret_cast<_Float16*>(p.yp) + pl * p.y_pstride +
                                               ((long long)b * T + t0 + r) * C + c) = v;
