@@ -430,7 +430,8 @@ __global__ __launch_bounds__(512) void attention_t256_kernel(const float* __rest
 //                    split at 2^14 straight from the S^T accumulator registers
 // The k index of the P . V product runs over a chunk's keys in the order the S^T accumulator holds them
 // (lane half h, element e <-> key (e & 3) + 8 (e >> 2) + 4 h of each 16), so V^T is stored with that
-// permutation and P needs no shuffle.  Scales are chosen in-kernel (powers of two): K and V from the head's
+// permutation and P needs no shuffle (the banded kernel; the T <= 256 kernel keeps V row-major and reads the same
+// V^T fragments with ds_read_b64_tr_b16: attn_vrow_off).  Scales are chosen in-kernel (powers of two): K and V from the head's
 // max |.| (workgroup reduction), Q from the wave's max; max |.| s lands in [2^13, 2^14).
 // ------------------------------------------------------------------------------------------------
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -456,11 +457,15 @@ __device__ __forceinline__ void split8_h(const float (&v)[8], float sc, f16x8& h
 // 3 fp16 plane products each, fp32 online softmax (as attn_chunk).  Kc: the chunk's 32 K rows (plane stride KPL,
 // row stride KLD); Vc: column 0 of the chunk's keys in the V^T planes (plane stride VPL, row stride VLD, keys
 // permuted inside each 16 as the S^T accumulator holds them); us = 1 / (K scale x Q scale).
-template <int KLD, int KPL, int VLD, int VPL>
+// TRV (the T <= 256 kernel): V as row-major planes [256 keys][64 dims] (16-B chunks XOR-swizzled by key, see
+// attn_vrow_off), the V^T fragments read with ds_read_b64_tr_b16 -- two 4-key reads per fragment, the same 8 values in
+// the same order as the V^T image's b128 read; vlb[t]: this lane's offset for dim tile t (attn_vlane_base).
+template <int KLD, int KPL, int VLD, int VPL, bool TRV = false>
 __device__ __forceinline__ void attn_chunk_h16(f32x16 (&o)[2], float& m, float& l, const f16x8 (&qf)[4][2],
                                                const _Float16* Kc, const _Float16* Vc, int c0, int qw, int qi,
                                                int kend, int window, int hf, int col, float us,
-                                               float ofac = 1.0f, float pscale = 16384.0f) {
+                                               float ofac = 1.0f, float pscale = 16384.0f, int vlb0 = 0,
+                                               int vlb1 = 0) {
     // S^T[key][query] = K . Q^T
     f32x16 st;
 #pragma unroll
@@ -517,9 +522,23 @@ __device__ __forceinline__ void attn_chunk_h16(f32x16 (&o)[2], float& m, float& 
         split8_h(pe, pscale, p0, p1);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-            const int vo = (32 * t + col) * VLD + 16 * ks + 8 * hf;
-            const f16x8 v0 = *reinterpret_cast<const f16x8*>(Vc + vo);
-            const f16x8 v1 = *reinterpret_cast<const f16x8*>(Vc + VPL + vo);
+            f16x8 v0, v1;
+            if constexpr (TRV) {
+                typedef short v4s __attribute__((vector_size(8)));
+                typedef __attribute__((address_space(3))) v4s lv4s;
+                const _Float16* vb = Vc + (c0 + 16 * ks) * 64 + (t ? vlb1 : vlb0);  // keys +0..3 / +8..11 of the half
+                const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lv4s*)(vb));
+                const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lv4s*)(vb + 8 * 64));
+                const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lv4s*)(vb + VPL));
+                const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lv4s*)(vb + VPL + 8 * 64));
+                typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+                v0 = __builtin_shufflevector(__builtin_bit_cast(h4, a0), __builtin_bit_cast(h4, a1), 0, 1, 2, 3, 4, 5, 6, 7);
+                v1 = __builtin_shufflevector(__builtin_bit_cast(h4, b0), __builtin_bit_cast(h4, b1), 0, 1, 2, 3, 4, 5, 6, 7);
+            } else {
+                const int vo = (32 * t + col) * VLD + 16 * ks + 8 * hf;
+                v0 = *reinterpret_cast<const f16x8*>(Vc + vo);
+                v1 = *reinterpret_cast<const f16x8*>(Vc + VPL + vo);
+            }
             o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1, p0, o[t], 0, 0, 0);
             o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0, p1, o[t], 0, 0, 0);
             o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0, p0, o[t], 0, 0, 0);
@@ -530,6 +549,18 @@ __device__ __forceinline__ void attn_chunk_h16(f32x16 (&o)[2], float& m, float& 
 __device__ __forceinline__ int vt_key_pos(int r) {
     const int k = r & 15;
     return (r & ~15) + 8 * ((k >> 2) & 1) + (k & 3) + 4 * ((k >> 3) & 1);
+}
+// row-major V planes of the T <= 256 kernel: dim d of key r at 16-B chunk (d >> 3) ^ 4 ((r >> 1) & 1) of the 128-B
+// row -- the 16-lane row writes (ds_write_b64) and the transposed reads (4 keys x 32 dims per 32-lane half) are
+// both conflict-free (MI355X_MICROARCH.md LDS banking)
+__device__ __forceinline__ int attn_vrow_off(int r, int d) { return r * 64 + 8 * ((d >> 3) ^ (((r >> 1) & 1) << 2)) + (d & 7); }
+// this lane's ds_read_b64_tr_b16 address inside a 16-key step of dim tile t, relative to that step's first row: lane
+// 4 q + p of its 16-lane group supplies row (key) 4 hf + q, dims 32 t + 16 ((lane >> 4) & 1) + 4 p .. +3, and
+// receives dim 32 t + (lane & 31) of the 4 keys -- the A-operand order of the S^T accumulator (keys 4 hf + 0..3,
+// then + 8)
+__device__ __forceinline__ int attn_vlane_base(int lane, int t) {
+    const int q = (lane >> 2) & 3, p = lane & 3, hf = lane >> 5;
+    return attn_vrow_off(4 * hf + q, 32 * t + 16 * ((lane >> 4) & 1) + 4 * p);
 }
 
 // T <= 256 (every clip up to 10.24 s) on the fp16 matrix cores.  A workgroup of 16 waves holds one (item, head)'s
@@ -573,7 +604,7 @@ __global__ __launch_bounds__(1024) void attention_t256_h16_kernel(const float* _
                                                                   const int* __restrict__ toff) {
     constexpr int D = 64, TM = 256, LDO = D + 1, NWV = 16;
     constexpr int KLD = 72, KPL = TM * KLD;  // K planes: [256][72 halves]
-    constexpr int VLD = 264, VPL = D * VLD;  // V^T planes: [64][264 halves]
+    constexpr int VLD = D, VPL = TM * D;     // V planes: [256 keys][64 dims] (attn_vrow_off), read transposed
     __shared__ __attribute__((aligned(16))) _Float16 lds[2 * KPL + 2 * VPL];
     __shared__ float red[2][NWV];
     __shared__ float mlx[8][2][32];  // the half-1 task's m, l per query of each tile
@@ -668,7 +699,7 @@ __global__ __launch_bounds__(1024) void attention_t256_h16_kernel(const float* _
     }
     const float sk = pow2_scale(mk), sv = pow2_scale(mv);
     const float us = 1.0f / (sk * mlx[0][0][wave]);  // S^T accumulator -> scores (exact)
-    // K planes (rows as loaded) and V^T planes (keys permuted inside each 16: see above)
+    // K planes (rows as loaded) and V planes (rows as loaded, chunk-swizzled: attn_vrow_off; read transposed)
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         if (ATTN_DIAG & 2) break;
@@ -684,14 +715,14 @@ __global__ __launch_bounds__(1024) void attention_t256_h16_kernel(const float* _
         }
         *reinterpret_cast<f16x4*>(Ks + r * KLD + c) = h0;
         *reinterpret_cast<f16x4*>(Ks + KPL + r * KLD + c) = h1;
-        const int pr = vt_key_pos(r);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const float t = vv[q][e] * sv;
-            const _Float16 a0 = (_Float16)t;
-            Vt[(c + e) * VLD + pr] = a0;
-            Vt[VPL + (c + e) * VLD + pr] = (_Float16)(t - (float)a0);
+            h0[e] = (_Float16)t;
+            h1[e] = (_Float16)(t - (float)h0[e]);
         }
+        *reinterpret_cast<f16x4*>(Vt + attn_vrow_off(r, c)) = h0;
+        *reinterpret_cast<f16x4*>(Vt + VPL + attn_vrow_off(r, c)) = h1;
     }
     const float uo = 1.0f / (16384.0f * sv);  // O^T accumulator -> P V (exact)
     f32x16 o[2];
@@ -703,6 +734,7 @@ __global__ __launch_bounds__(1024) void attention_t256_h16_kernel(const float* _
     __syncthreads();
     const bool active = task >= 0 && qw < T;
     const int kend = min(T - 1, qw + 31);
+    const int vlb0 = attn_vlane_base(lane, 0), vlb1 = attn_vlane_base(lane, 1);
     if (active) {
         // the tile's chunks kstart, kstart + 32, .., <= kend: half 0 the first ceil(n / 2), half 1 the rest
         const int kstart = max(0, qw - window + 1) & ~31;
@@ -710,8 +742,8 @@ __global__ __launch_bounds__(1024) void attention_t256_h16_kernel(const float* _
         const int cb = kstart + (kh ? 32 * n0 : 0), ce = kstart + 32 * (kh ? n : n0);
         for (int c0 = cb; c0 < ce; c0 += 32) {
             if (ATTN_DIAG & 1) break;
-            attn_chunk_h16<KLD, KPL, VLD, VPL>(o, m, l, qf, Ks + c0 * KLD, Vt + c0, c0, qw, qi, kend, window, hf,
-                                               col, us);
+            attn_chunk_h16<KLD, KPL, VLD, VPL, true>(o, m, l, qf, Ks + c0 * KLD, Vt, c0, qw, qi, kend, window, hf,
+                                                     col, us, 1.0f, 16384.0f, vlb0, vlb1);
         }
     }
     __syncthreads();  // K / V dead: the merge and the output staging reuse the LDS
