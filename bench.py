@@ -92,6 +92,8 @@ def parse():
     ap.add_argument("--no-f32-mode", action="store_true", help="skip the fp32-MFMA comparison run")
     ap.add_argument("--precision", default=None, help="GEMM precision mode (default: the engine's)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--ln-fused", type=int, default=None,
+                    help="A/B: 0 = LayerNorm launches, 1 = LayerNorm prologue in small-grid q/k/v / fc1 (default)")
     ap.add_argument("--stage0-fused", type=int, default=None,
                     help="kernel variant A/B: 0 = stage-0 block + down conv 0 as two kernels, 1 = fused (default)")
     ap.add_argument("--dump-sequence", default=None,
@@ -479,6 +481,8 @@ def main():
         model.set_precision(args.precision)
     if args.stage0_fused is not None:
         model.set_option("stage0_fused", args.stage0_fused)
+    if args.ln_fused is not None:
+        model.set_option("ln_fused", args.ln_fused)
     wl = Workload(args, model, dev, world, rank)
     if model.precision == "f16x3":
         model.calibrate()  # (otherwise inside the first encode) -- before the trace marker

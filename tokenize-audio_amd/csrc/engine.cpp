@@ -325,6 +325,10 @@ struct mimi_engine {
 
     bool taps = false;
     int stage0_fused = 1;  // 0: stage-0 block + down conv 0 as two kernels; 1: one fused kernel
+    // LayerNorm prologue on small grids (gemm_planes.h FL_LNA): 0 off, 1 fc1 (default), 2 fc1 and q/k/v.  Batch 1
+    // (rocprofv3, profiles/r3j_*): fc1 15.0 us with it vs 10.1 + 5.2 us (+ a launch gap) for fc1 + LayerNorm; q/k/v
+    // 20.8 vs 10.4 + 5.2 us -- its one compute wave and 16-row tiles leave the prologue's chain exposed
+    int ln_fused = 1;
     struct Tap {
         float* d = nullptr;
         size_t cap = 0;
@@ -1502,10 +1506,18 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         const DevXfmr& x = e->xf[l];
         const long long nact = rows * Hd;
         const Act t1a = new_act(nmf("xf%d.ln1", l));
-        LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1a.scale,
-                                    t1a.amax),
-                   "ln1");
-        rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
+        // LayerNorm + fc1 (ln_fused >= 1) / q/k/v (ln_fused 2): on small grids one launch whose tiles compute their
+        // rows' LayerNorm (the same bits as the LayerNorm kernel's planes, gemm_planes.h FL_LNA)
+        auto ln_into = [&](GemmArgs& g, int role, const float* lw, const float* lb, const Act& act) {
+            if (!h16 || e->ln_fused < (role == ROLE_QKV ? 2 : 1) || !gemm_ln_prologue_ok(role, g, prec)) return false;
+            g.ln_x = w.t0;
+            g.ln_g = lw;
+            g.ln_b = lb;
+            g.ln_eps = c.norm_eps;
+            g.ln_scale = act.scale;
+            g.ln_amax = act.amax;
+            return true;
+        };
         GemmArgs aq = linear_args(w.t1, T, Hd, x.wqkv, 3 * H * Dh, w.qkv);
         aq.Wsplit = x.wqkv_s;
         aq.batch = B;
@@ -1524,6 +1536,12 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         }
         if (ns) planes_in(aq, w.t1, nact);
         use_h(aq, x.wqkv_h, x.wqkv_hs, t1a);
+        if (!ln_into(aq, ROLE_QKV, x.ln1_w, x.ln1_b, t1a)) {
+            LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1a.scale,
+                                        t1a.amax),
+                       "ln1");
+            rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
+        }
         LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, prec), "qkv");
         rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
         if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, tapB, tapT, 3 * H * Dh, s))) return rc;
@@ -1549,10 +1567,6 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
         if ((rc = save_tap(e, nmf("oproj%d", l).c_str(), w.t0, tapB, tapT, Hd, s))) return rc;
         const Act t1b = new_act(nmf("xf%d.ln2", l));
-        LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1b.scale,
-                                    t1b.amax),
-                   "ln2");
-        rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
         GemmArgs a1 = linear_args(w.t1, rows, Hd, x.w1, c.intermediate_size, w.ff);
         a1.Wsplit = x.w1_s;
         Act ffa;
@@ -1564,6 +1578,12 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             a1.C = nullptr;
             ffa = new_act(nmf("xf%d.ff", l));
             out_act(a1, ffa);
+        }
+        if (!ln_into(a1, ROLE_FC1, x.ln2_w, x.ln2_b, t1b)) {
+            LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1b.scale,
+                                        t1b.amax),
+                       "ln2");
+            rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
         }
         LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, prec), "fc1");
         rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
@@ -2263,6 +2283,16 @@ extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {
             e->graph_seen.clear();
         }
         e->stage0_fused = (int)value;
+        return MIMI_OK;
+    }
+    if (!strcmp(key, "ln_fused")) {
+        if (value < 0 || value > 2) return set_err(MIMI_ERR_INVALID_ARGUMENT, "ln_fused %lld (0, 1 or 2)", (long long)value);
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->ln_fused != (int)value) {
+            drop_graphs(e);
+            e->graph_seen.clear();
+        }
+        e->ln_fused = (int)value;
         return MIMI_OK;
     }
     return set_err(MIMI_ERR_INVALID_ARGUMENT, "unknown option '%s'", key);

@@ -71,7 +71,7 @@ static hipError_t run_split(const GemmArgs& a, hipStream_t s) {
 template <int BM, int BN, int WM, int WN, int NS, int ST, int EPI, int OUTP, int TAG, int LW = 0, int BK = 32, int MF = 32,
           int FL = 0, bool F16 = false>
 static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
-    if constexpr (F16 && !(FL & FL_RAGGED)) {  // ragged batch: the same tile with per-item rows (gemm_planes.h)
+    if constexpr (F16 && !(FL & (FL_RAGGED | FL_LNA))) {  // ragged batch: the same tile with per-item rows (gemm_planes.h)
         if (a.m_rows || a.a_rows) {
             if (!a.m_rows || !a.a_rows) return hipErrorInvalidValue;
             return run_planes<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL | FL_RAGGED, F16>(a, s);
@@ -236,9 +236,28 @@ static hipError_t run_small_h16(const GemmArgs& a, hipStream_t s) {
     return run_planes<16, BN2, 1, WN2, 2, ST, EPI, OUTP, TAG, 4, 32, 16, FL, true>(a, s);
 }
 
+// The LayerNorm prologue (FL_LNA, gemm_planes.h) replaces the LayerNorm launch in front of q/k/v and fc1 on the
+// small grids: every tile recomputes its rows' LayerNorm (N / BN times per row), cheap beside a launch when the
+// rows are few (batch 1-4), and its A image (BM x 2 KiB) fits beside the ring for the 16-64-row tiles.
+bool gemm_ln_prologue_ok(int role, const GemmArgs& a, int precision) {
+    return precision == PREC_F16X3 && (role == ROLE_QKV || role == ROLE_FC1) && a.K == 512 && a.a_rs == 512 &&
+           a.a_off == 0 && !a.a_rows && !a.m_rows && !a.a_boff && tiles(a, 128, 128) < kSmallGrid;
+}
+
 static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
     const int prec = g_prec;
     if (prec != PREC_BF16X6 && prec != PREC_BF16X3 && prec != PREC_F16X3) return hipErrorInvalidValue;
+    if (a.ln_x) {  // LayerNorm prologue: only where it is built (never silently dropped)
+        if (!gemm_ln_prologue_ok(role, a, prec) || !a.ln_g || !a.ln_b || !(a.ln_scale > 0.0f)) return hipErrorInvalidValue;
+        // the tile rule of run_small_h16 (q/k/v never reaches its 64-row tile on a small grid)
+        if (role == ROLE_QKV) {
+            if (tiles(a, 32, 128) >= 256) return run_planes<32, 128, 2, 2, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
+            return run_planes<16, 64, 1, 1, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
+        }
+        if (tiles(a, 64, 64) >= 256) return run_planes<64, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
+        if (tiles(a, 32, 64) >= 256) return run_planes<32, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
+        return run_planes<16, 64, 1, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
+    }
     if (prec == PREC_F16X3 && tiles(a, 128, 128) < kSmallGrid) {
         // <EPI, OUTP, TAG, 64-row BN, 32-row BM x BN / waves, 16-row BN / waves>; 16 x 16 wave tiles are too small for
         // the staged epilogue (64 lanes x 8 columns), and RoPE needs 64 columns per wave

@@ -89,7 +89,13 @@ __device__ __forceinline__ int chunk_swz(int row) {
 //           needed).
 //           FL_RAGGED -- per-item valid rows (GemmArgs a_rows / m_rows: ragged batches); a separate instantiation so
 //           the uniform batches' kernels carry none of its bookkeeping (it cost them 2-7 % when it was run-time)
-enum : int { FL_PRIO = 2, FL_PAIR = 4, FL_PERSIST = 8, FL_KG2 = 16, FL_KG4 = 32, FL_PF = 256, FL_RAGGED = 512 };
+//           FL_LNA -- A = LayerNorm(p.ln_x) for the tile's BM rows, computed by every wave before the K loop with
+//           layernorm_kernel's arithmetic (kernels.h ln_row_coeffs), its fp16 planes written straight into an LDS
+//           image of the whole K = 512 (same rows, chunk swizzle and K-step layout as the DMA'd A images): the ring
+//           carries B only and the LayerNorm launch + its planes' HBM round trip are gone.  Small grids only (the
+//           LayerNorm is recomputed per N tile; a 512-wide A image is BM x 2 KiB of LDS).
+enum : int { FL_PRIO = 2, FL_PAIR = 4, FL_PERSIST = 8, FL_KG2 = 16, FL_KG4 = 32, FL_PF = 256, FL_RAGGED = 512,
+             FL_LNA = 2048 };
 // tuning diagnostics (tools/gemm_bench.hip only; results are garbage): no DMA refills after the prologue / no MFMAs
 enum : int { FL_DIAG_NODMA = 64, FL_DIAG_NOMMA = 128 };
 // timing probe of an interleaved plane layout (tools/gemm_bench.hip only, results garbage): the loader waves fetch
@@ -114,10 +120,12 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     constexpr int NB = PAIR ? 2 : 1;             // B images (K steps) per stage
     constexpr int AR = BM + XR;                  // A image rows
     constexpr int APL = AR * BK, BPL = BN * BK;  // bf16 per plane image
-    constexpr int STG = NS * (APL + NB * BPL);   // bf16 per stage
+    constexpr bool LNA = (FL & FL_LNA) != 0;     // A from the LayerNorm prologue (LDS-resident, not in the ring)
+    constexpr int BOFF = LNA ? 0 : NS * APL;     // B images' offset in a stage
+    constexpr int STG = BOFF + NS * NB * BPL;    // bf16 per stage
     // DMA pieces of a stage: A planes [0, TPA), then B [plane][image] images; piece j is issued by loading wave
     // j % NLD
-    constexpr int TPA = NS * AR / RPP, TP = TPA + NS * NB * BN / RPP;
+    constexpr int TPA = LNA ? 0 : NS * AR / RPP, TP = TPA + NS * NB * BN / RPP;
     constexpr int PMAX = (TP + NLD - 1) / NLD;   // pieces per loading wave per stage (the first TP % NLD waves)
     constexpr int PMIN = TP / NLD;               // (the others)
     static_assert(BK == 32 || (BK == 16 && MF == 32), "BK");
@@ -128,6 +136,9 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     static_assert(PMAX * (STAGES - 2 * KG) <= 63, "vmcnt range");
     static_assert(EPI != EPI_ROPE || (MF == 32 ? TN % 2 == 0 : TN % 4 == 0), "rope pairs (d, d+32) in one lane");
     static_assert(!F16 || NS == 2, "fp16 planes: 2 planes, 3 products");
+    static_assert(!LNA || (F16 && !PAIR && !(FL & (FL_PERSIST | FL_RAGGED | FL_DIAG_ILV))), "LayerNorm prologue");
+    constexpr int LNK = 512;                     // (FL_LNA) the LayerNorm width = K
+    constexpr int LNE = LNA ? LNK / BK * NS * APL : 0;  // bf16 of the LDS A image [K step][plane][row][BK]
     // OUTP: 0 = fp32 C only; 2/3 = that many bf16 planes of the output (+ fp32 C when p.C is set);
     // | 8 = the planes hold ELU(output) (fp32 C keeps the raw value)
     constexpr int ONS = OUTP & 7;
@@ -150,8 +161,8 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     constexpr int TNC = TN / JH, CWC = TNC * MF, LDE = CWC + 4;
     static_assert(TNC * JH == TN, "epilogue passes");  // (RoPE pairs are read from acc, not from the staging)
     constexpr int LDS_EL = STAGES * STG > PFS + NW * RW * LDE * 2 ? STAGES * STG : PFS + NW * RW * LDE * 2;
-    static_assert(LDS_EL * 2 <= 160 * 1024, "LDS");
-    __shared__ __attribute__((aligned(16))) __bf16 lds[LDS_EL];
+    static_assert((LDS_EL + LNE) * 2 <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) __bf16 lds[LDS_EL + LNE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -201,6 +212,64 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     auto c_base_of = [&](int b) {
         return (RG && p.c_boff) ? (long long)p.c_boff[b] * p.ldc : (long long)b * p.c_bstride;
     };
+
+    // LayerNorm prologue (FL_LNA; one tile per workgroup): the tile's rows over all waves, one wave per row, all of
+    // a wave's rows loaded before the first reduction.  Loader waves run it after issuing their first ring stages;
+    // the barrier behind it (one extra on both sides) publishes the A image.
+    float ln_mx = 0.0f;  // max|LayerNorm output| of this wave's rows, committed at the wave's end (not before the barrier)
+    auto ln_prologue = [&]() __attribute__((always_inline)) {
+        int b, mt, nt;
+        decode((int)blockIdx.x, b, mt, nt);
+        constexpr int PER = LNK / 64, NWA = NW + LW, LRW = (BM + NWA - 1) / NWA;
+        float mx = 0.0f;
+        const float* __restrict__ xb = p.ln_x + a_base_of(b) + p.a_off;
+        // gamma / beta of this lane's columns beside the rows (not after the reductions: one more memory round trip)
+        f32x4 gv[PER / 4], bv[PER / 4];
+#pragma unroll
+        for (int q = 0; q < PER / 4; ++q) {
+            gv[q] = *reinterpret_cast<const f32x4*>(p.ln_g + q * 256 + lane * 4);
+            bv[q] = *reinterpret_cast<const f32x4*>(p.ln_b + q * 256 + lane * 4);
+        }
+        float v[LRW][PER];
+#pragma unroll
+        for (int i = 0; i < LRW; ++i) {
+            const int m = mt * BM + wave + i * NWA;
+            if (wave + i * NWA < BM && m < M) {
+                const float* xr = xb + (long long)m * p.a_rs;
+#pragma unroll
+                for (int q = 0; q < PER / 4; ++q) {
+                    const f32x4 t = *reinterpret_cast<const f32x4*>(xr + q * 256 + lane * 4);
+                    v[i][q * 4 + 0] = t.x; v[i][q * 4 + 1] = t.y; v[i][q * 4 + 2] = t.z; v[i][q * 4 + 3] = t.w;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < LRW; ++i) {
+            const int r = wave + i * NWA, m = mt * BM + r;
+            if (r >= BM) continue;  // (wave-uniform)
+            float sc = 0.0f, bi = 0.0f;
+            if (m < M) ln_row_coeffs<LNK>(v[i], p.ln_eps, sc, bi);  // (m is wave-uniform: whole-wave shuffles)
+#pragma unroll
+            for (int q = 0; q < PER / 4; ++q) {
+                const int c0 = q * 256 + lane * 4;  // 4 columns inside one 16-B chunk of K step c0 / BK
+                uint2 hi = make_uint2(0u, 0u), lo = make_uint2(0u, 0u);
+                if (m < M) {
+                    float o[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = ln_affine(v[i][q * 4 + e], sc, bi, gv[q][e], bv[q][e]);
+                    ln_split4_f16(o, p.ln_scale, hi, lo);
+                    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+                }
+                const int ks = c0 / BK, ch = (c0 % BK) / 8;
+                __bf16* d = lds + LDS_EL + ks * NS * APL + r * BK + (ch ^ chunk_swz<BK, MF>(r)) * 8 + (c0 % 8);
+                *reinterpret_cast<uint2*>(d) = hi;
+                *reinterpret_cast<uint2*>(d + APL) = lo;
+            }
+        }
+        ln_mx = mx;
+        __syncthreads();
+    };
+    if constexpr (LNA && LW == 0) ln_prologue();
 
     if constexpr (LW > 0) {
         // Warp-specialised: the loading waves run their own tile loop, meeting the compute waves at the same
@@ -262,7 +331,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                                 const int img = jb / (2 * BN / RPP), r8 = jb % (2 * BN / RPP);
                                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                                     wrsrc,
-                                    (__attribute__((address_space(3))) void*)(st + NS * APL + pi * BPL + rb * RPP * BK),
+                                    (__attribute__((address_space(3))) void*)(st + BOFF + pi * BPL + rb * RPP * BK),
                                     16, b_lane + r8 * b_rb + kb + img * kimg * 4, 0, 0, 0);
                             }
                             continue;
@@ -278,7 +347,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                             const int pl = pi / NB, img = pi % NB;
                             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                                 wrsrc,
-                                (__attribute__((address_space(3))) void*)(st + NS * APL + pi * BPL + rb * RPP * BK),
+                                (__attribute__((address_space(3))) void*)(st + BOFF + pi * BPL + rb * RPP * BK),
                                 16, b_lane + pl * b_pl + rb * b_rb + kb + img * kimg * 2, 0, 0, 0);
                         }
                     }
@@ -291,6 +360,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                 };
                 const int first = (int)blockIdx.x;
                 if (first < ntiles) prologue(first);
+                if constexpr (LNA) ln_prologue();  // (after this wave's first ring stages are in flight)
                 for (int tile = first; tile < ntiles;) {
                     for (int kt = 0; kt < KT; kt += KG) {
                         const int ng = min(KG, KT - kt);
@@ -324,6 +394,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                 case 6: if constexpr (LW > 6) run_loader(std::integral_constant<int, 6>()); break;
                 default: if constexpr (LW > 7) run_loader(std::integral_constant<int, 7>()); break;
             }
+            if constexpr (LNA) amax_commit(p.ln_amax, ln_mx);
             return;  // (no barrier follows in the compute waves)
         }
     }
@@ -392,7 +463,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                 const int img = pi % NB;
                 __builtin_amdgcn_global_load_lds(
                     (const void*)(Wp + soff[q] + k0 + img * kimg),
-                    (__attribute__((address_space(3))) void*)(st + NS * APL + pi * BPL + rb * RPP * BK), 16, 0, 0);
+                    (__attribute__((address_space(3))) void*)(st + BOFF + pi * BPL + rb * RPP * BK), 16, 0, 0);
             }
         }
     };
@@ -435,6 +506,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     // MFMAs); the ring keeps the next group(s) in flight, STAGES >= 2 KG
     if constexpr (LW > 0) {
         {  // compute waves (the loaders run their own loop above)
+            if constexpr (LNA) ln_prologue();
             for (int kt = 0; kt < KT; kt += KG) {
                 const int ng = min(KG, KT - kt);
                 __builtin_amdgcn_s_barrier();
@@ -442,8 +514,8 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
 #pragma unroll
                 for (int q = 0; q < KG; ++q) {
                     if (q >= ng) break;
-                    const __bf16* As = lds + ((kt + q) % STAGES) * STG;
-                    const __bf16* Bs = As + NS * APL;
+                    const __bf16* Bs = lds + ((kt + q) % STAGES) * STG + BOFF;
+                    const __bf16* As = LNA ? lds + LDS_EL + (kt + q) * NS * APL : Bs - BOFF;
                     bf16x8 af[NS][TM], bf[NS][TN];
 #pragma unroll
                     for (int img = 0; img < NB; ++img)
@@ -485,8 +557,8 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
 #pragma unroll
         for (int q = 0; q < KG; ++q) {
             if (q >= ng) break;
-            const __bf16* As = lds + ((kt + q) % STAGES) * STG;
-            const __bf16* Bs = As + NS * APL;
+            const __bf16* Bs = lds + ((kt + q) % STAGES) * STG + BOFF;
+            const __bf16* As = LNA ? lds + LDS_EL + (kt + q) * NS * APL : Bs - BOFF;
             bf16x8 af[NS][TM], bf[NS][TN];
 #pragma unroll
             for (int img = 0; img < NB; ++img)
@@ -611,6 +683,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     }
     }  // tiles
     if (F16 && ONS && compute) amax_commit(p.out_amax, omx);
+    if (LNA && compute) amax_commit(p.ln_amax, ln_mx);
 #endif
 }
 

@@ -101,6 +101,48 @@ __device__ __forceinline__ void amax_commit(unsigned* amax, float mx) {
     }
 }
 
+// LayerNorm row arithmetic (TF/modeling_mimi.py:737-738), shared by layernorm_kernel (ops.hip) and the LayerNorm
+// prologue of the small-batch q/k/v and fc1 GEMMs (gemm_planes.h FL_LNA), so both give the same bits: one wave
+// per row of C, lane l holding columns q*256 + 4l + e; two-pass mean / variance in fp32, then
+// y = (x * rstd + (-mean * rstd)) * gamma + beta as the torch CPU kernel forms it.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+template <int C>
+__device__ __forceinline__ void ln_row_coeffs(const float (&v)[C / 64], float eps, float& sc, float& bi) {
+    constexpr int PER = C / 64;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) s += v[i];
+    const float mean = wave_sum(s) / (float)C;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const float d = v[i] - mean;
+        s2 += d * d;
+    }
+    const float var = wave_sum(s2) / (float)C;
+    const float rstd = 1.0f / sqrtf(var + eps);
+    sc = rstd;
+    bi = -rstd * mean;
+}
+__device__ __forceinline__ float ln_affine(float v, float sc, float bi, float g, float b) { return (v * sc + bi) * g + b; }
+// fp16 planes of 4 LayerNorm outputs o * yscale (PREC_F16X3): hi / lo as 4 halves each
+__device__ __forceinline__ void ln_split4_f16(const float (&o)[4], float yscale, uint2& hi, uint2& lo) {
+    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+    h4_t h0, h1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float t = o[e] * yscale;
+        h0[e] = (_Float16)t;
+        h1[e] = (_Float16)(t - (float)h0[e]);
+    }
+    hi = __builtin_bit_cast(uint2, h0);
+    lo = __builtin_bit_cast(uint2, h1);
+}
+
 // A pointer a captured hipGraph reads at run time: the engine's io block, written by set_io_kernel in front of
 // every replay (a vector load that bypasses the scalar cache, made wave-uniform).  ref == null: direct.
 template <typename T>
@@ -175,7 +217,18 @@ struct GemmArgs {
     const int* c_boff;  // C / Cp / R: item b starts at row c_boff[b] (element c_boff[b] * ldc)
     // EPI_ROPE over packed rows: the RoPE position of output row m (null: m itself)
     const int* rope_pos;
+    // LayerNorm prologue (small-batch q/k/v and fc1 in f16x3, gemm_planes.h FL_LNA): A = LayerNorm(ln_x) (fp32, the
+    // same [rows][K] indexing as the A planes, which are then not read), computed per tile as layernorm_kernel
+    // computes it; its fp16 planes (of A * ln_scale) go straight to LDS, max|A| to ln_amax.  ln_x == null: off.
+    const float* ln_x;
+    const float* ln_g;
+    const float* ln_b;
+    float ln_eps;
+    float ln_scale;
+    unsigned* ln_amax;
 };
+// true when launch_gemm(role, a, precision) runs a tile with the LayerNorm prologue (a.ln_* then feed A)
+bool gemm_ln_prologue_ok(int role, const GemmArgs& a, int precision);
 
 // Launch the GEMM for a given conv/linear role (the role picks tile shape and template flags).
 enum GemmRole : int {

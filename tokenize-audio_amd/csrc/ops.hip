@@ -64,11 +64,7 @@ hipError_t launch_conv0(const float* x, long long L, int batch, const float* w, 
 // LayerNorm(512) (TF/modeling_mimi.py:737-738): one wave per row, two-pass mean / variance in fp32,
 // y = (x * rstd + (-mean * rstd)) * gamma + beta as the torch CPU kernel forms it.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
+// (wave_sum and the row arithmetic: kernels.h ln_row_coeffs / ln_affine / ln_split4_f16)
 
 // RPW rows per wave, all loads in flight before the first reduction; 8 waves per workgroup.
 template <int C, int RPW>
@@ -108,43 +104,28 @@ __global__ __launch_bounds__(512) void layernorm_kernel(const float* __restrict_
     if (row >= rows) break;
     if (row_len && row % row_T >= row_len[row / row_T]) continue;  // ragged: past the item's frames
     float (&v)[PER] = vr[rr];
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) s += v[i];
-    const float mean = wave_sum(s) / (float)C;
-    float s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const float d = v[i] - mean;
-        s2 += d * d;
-    }
-    const float var = wave_sum(s2) / (float)C;
-    const float rstd = 1.0f / sqrtf(var + eps);
-    const float sc = rstd;
-    const float bi = -rstd * mean;
+    float sc, bi;
+    ln_row_coeffs<C>(v, eps, sc, bi);
     float* yr = y + row * C;
 #pragma unroll
     for (int q = 0; q < PER / 4; ++q) {
         const int c0 = q * 256 + lane * 4;
         const f32x4 gg = gv[q], bb = bv[q];
         f32x4 o;
-        o.x = (v[q * 4 + 0] * sc + bi) * gg.x + bb.x;
-        o.y = (v[q * 4 + 1] * sc + bi) * gg.y + bb.y;
-        o.z = (v[q * 4 + 2] * sc + bi) * gg.z + bb.z;
-        o.w = (v[q * 4 + 3] * sc + bi) * gg.w + bb.w;
+        o.x = ln_affine(v[q * 4 + 0], sc, bi, gg.x, bb.x);
+        o.y = ln_affine(v[q * 4 + 1], sc, bi, gg.y, bb.y);
+        o.z = ln_affine(v[q * 4 + 2], sc, bi, gg.z, bb.z);
+        o.w = ln_affine(v[q * 4 + 3], sc, bi, gg.w, bb.w);
         if (yns == 0) {
             *reinterpret_cast<f32x4*>(yr + c0) = o;
         } else if (yscale > 0.0f) {
             // fp16 planes of o * yscale (PREC_F16X3)
-            typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
             _Float16* pr = reinterpret_cast<_Float16*>(yp) + row * C + c0;
-            const f32x4 t = o * yscale;
-            f16x4 h0, h1;
-            h0.x = (_Float16)t.x; h0.y = (_Float16)t.y; h0.z = (_Float16)t.z; h0.w = (_Float16)t.w;
-            h1.x = (_Float16)(t.x - (float)h0.x); h1.y = (_Float16)(t.y - (float)h0.y);
-            h1.z = (_Float16)(t.z - (float)h0.z); h1.w = (_Float16)(t.w - (float)h0.w);
-            *reinterpret_cast<f16x4*>(pr) = h0;
-            *reinterpret_cast<f16x4*>(pr + pstride) = h1;
+            const float ov[4] = {o.x, o.y, o.z, o.w};
+            uint2 h0, h1;
+            ln_split4_f16(ov, yscale, h0, h1);
+            *reinterpret_cast<uint2*>(pr) = h0;
+            *reinterpret_cast<uint2*>(pr + pstride) = h1;
             mx = fmaxf(mx, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
         } else {
             // planes for the split-bf16 GEMMs that read this row (q/k/v, fc1)
@@ -1216,7 +1197,7 @@ constexpr int RVQ_CS = 256;
 
 size_t rvq_work_bytes(long long frames) {
     const long long fp = (frames + RVQ_FT - 1) / RVQ_FT * RVQ_FT;
-    const int nsl = 2048 / RVQ_CS;
+    const int nsl = 32;  // the most code slices any rvq_level_h16_kernel form may use (NWV = 2: 64-code slices)
     return (size_t)(2 * fp * 256 * 4 + 2 * 3 * fp * nsl * 4);
 }
 
@@ -1460,12 +1441,15 @@ constexpr int RVQ_CAND = 2048;
 // CW: codes per wave (32, or 64 as two 32-code MFMA tiles): a slice of 8 CW codes, NSL = 2048 / (8 CW) slices.  The
 // large-batch form takes 64 (4 slices: 500 workgroups at B = 32 x 10 s -- one round of two per CU -- instead of 1000
 // in two rounds, each round paying the whole merge / residual / |r|^2 / plane prologue chain again).
-template <int D, int PF = 4, int EX = 16, bool RG = false, int CW = 32>
+// NWV: waves per workgroup (8; 2 and 4 were timed for small grids, not kept: launch_rvq)
+template <int D, int PF = 4, int EX = 16, bool RG = false, int CW = 32, int NWV = 8>
 // (HIP's second launch bound is waves per SIMD: 4 = two 8-wave workgroups per CU, i.e. <= 128 VGPRs)
-__global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(RvqArgs p, int L0) {
+__global__ __launch_bounds__(64 * NWV, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(RvqArgs p, int L0) {
+    constexpr int NT = 64 * NWV;          // threads
     constexpr int TNC = CW / 32;          // 32-code MFMA tiles per wave
-    constexpr int SLC = 8 * CW;           // codes per slice
+    constexpr int SLC = NWV * CW;         // codes per slice
     constexpr int NSL = 2048 / SLC;       // slices
+    static_assert(NSL <= 32 && NSL % 4 == 0, "slices: rvq_work_bytes, rvq_merge");
     // RG (a ragged batch: p.flen): a workgroup none of whose frames is valid has nothing to do -- no later level
     // reads what it would write (only valid frames' residuals and partial argmins are ever read)
     if constexpr (RG) {
@@ -1480,7 +1464,7 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
     __shared__ __attribute__((aligned(16))) _Float16 rpl[2][FT][RLD];  // fp16 planes of r * rs
     __shared__ float xn[FT], rus[FT], win[FT], smin[FT];
     __shared__ int prev[FT];
-    __shared__ float redd[8][FT];
+    __shared__ float redd[NWV][FT];
     __shared__ unsigned cand[RVQ_CAND];
     __shared__ unsigned ncand;
     __shared__ unsigned long long best[FT];
@@ -1510,7 +1494,7 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
     const float* rin = w.res((L + 1) & 1);
     float* rout = w.res(L & 1);
 #pragma unroll 4
-    for (int idx = tid; idx < FT * D / 4; idx += 512) {
+    for (int idx = tid; idx < FT * D / 4; idx += NT) {
         const int i = idx / (D / 4), k = (idx % (D / 4)) * 4;
         const long long f = f0 + i;
         f32x4 r = {0.f, 0.f, 0.f, 0.f};
@@ -1531,8 +1515,8 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
     }
     __syncthreads();
     // |r|^2 in torch's order (rvq_level_kernel) and max|r| per frame (16 threads per frame)
-    {
-        const int fi = tid >> 4, l = tid & 15;
+    for (int fi = tid >> 4; fi < FT; fi += NT / 16) {
+        const int l = tid & 15;
         if (l < 8) {
             float a[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
@@ -1560,7 +1544,7 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
     }
     __syncthreads();
     // fp16 planes of r * rs
-    for (int idx = tid; idx < FT * D / 2; idx += 512) {
+    for (int idx = tid; idx < FT * D / 2; idx += NT) {
         const int i = idx / (D / 2), k = (idx % (D / 2)) * 2;
         const float rs = -0.5f * win[i];
         const float t0 = img[0][i][k >> 1] * rs, t1 = img[1][i][k >> 1] * rs;
@@ -1654,7 +1638,7 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
     if (tid < FT) {
         float m = redd[0][tid];
 #pragma unroll
-        for (int q = 1; q < 8; ++q) m = fminf(m, redd[q][tid]);
+        for (int q = 1; q < NWV; ++q) m = fminf(m, redd[q][tid]);
         smin[tid] = m;
         const float emax = p.cb_emax[L];
         const float rn = __builtin_sqrtf(fmaxf(xn[tid], 0.0f)) + emax;
@@ -1680,7 +1664,7 @@ __global__ __launch_bounds__(512, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(Rvq
     const unsigned nc = ncand;
     const bool all = nc > RVQ_CAND;
     const unsigned total = all ? FT * SLC : nc;
-    for (unsigned i = tid; i < total; i += 512) {
+    for (unsigned i = tid; i < total; i += NT) {
         const int row = all ? (int)(i % FT) : (int)(cand[i] >> 16);
         const int c = slice * SLC + (all ? (int)(i / FT) : (int)(cand[i] & 0xffff));
         if (f0 + row >= p.frames) continue;
@@ -1729,29 +1713,39 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
         const unsigned ftiles = (unsigned)((a.frames + 31) / 32);
         const bool small = ftiles * 8 < 256;
         const bool split = a.sem_split != 0;  // levels 0 and 1 in one launch (rvq_sem_split)
-        *kname = a.flen ? (small ? "mimi::rvq_level_h16_kernel<256, 16, 32, true, 32>" : "mimi::rvq_level_h16_kernel<256, 2, 16, true, 64>")
-                        : (small ? "mimi::rvq_level_h16_kernel<256, 16, 32, false, 32>" : "mimi::rvq_level_h16_kernel<256, 2, 16, false, 64>");
+        // (2- and 4-wave workgroups on small grids -- 32 / 16 slices, 4x / 2x the workgroups, each streaming a quarter /
+        // half of the codebook bytes -- were slower at batch 1 and 4: rvq 0.14 -> 0.21 / 0.16 ms per batch-1 encode,
+        // the per-workgroup prologue chain on fewer threads outweighs the shorter stream; profiles/r3j_ab_*)
+        constexpr int nwv = 8;
+        const unsigned nsl = 2048 / (small ? nwv * 32 : 8 * 64);
+        static char kn[96];
+        snprintf(kn, sizeof kn, "mimi::rvq_level_h16_kernel<256, %d, %d, %s, %d, %d>", small ? 16 : 2, small ? 32 : 16,
+                 a.flen ? "true" : "false", small ? 32 : 64, nwv);
+        *kname = kn;
         for (int L = 0; L < a.levels; L += (split && L == 0) ? 2 : 1) {
-            const dim3 g(ftiles, small ? 8 : 4, (split && L == 0) ? 2 : 1);
-            if (a.flen) {  // ragged: workgroups of invalid frames exit (rvq_level_h16_kernel<..., RG>)
-                if (small)
-                    hipLaunchKernelGGL((rvq_level_h16_kernel<256, 16, 32, true, 32>), g, dim3(512), 0, s, a, L);
-                else
-                    hipLaunchKernelGGL((rvq_level_h16_kernel<256, 2, 16, true, 64>), g, dim3(512), 0, s, a, L);
-            } else if (small) {
-                hipLaunchKernelGGL((rvq_level_h16_kernel<256, 16, 32, false, 32>), g, dim3(512), 0, s, a, L);
-            } else {
-                hipLaunchKernelGGL((rvq_level_h16_kernel<256, 2, 16, false, 64>), g, dim3(512), 0, s, a, L);
-            }
+            const dim3 g(ftiles, nsl, (split && L == 0) ? 2 : 1);
+            const dim3 blk(64 * nwv);
+            // (ragged, RG: workgroups of invalid frames exit)
+#define RVQ_LAUNCH(PF_, EX_, CW_, NWV_)                                                                   \
+    do {                                                                                                  \
+        if (a.flen)                                                                                       \
+            hipLaunchKernelGGL((rvq_level_h16_kernel<256, PF_, EX_, true, CW_, NWV_>), g, blk, 0, s, a, L);  \
+        else                                                                                              \
+            hipLaunchKernelGGL((rvq_level_h16_kernel<256, PF_, EX_, false, CW_, NWV_>), g, blk, 0, s, a, L); \
+    } while (0)
+            if (!small)
+                RVQ_LAUNCH(2, 16, 64, 8);
+            else
+                RVQ_LAUNCH(16, 32, 32, 8);
+#undef RVQ_LAUNCH
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
-        if (small)
-            hipLaunchKernelGGL(rvq_final_kernel<8>, dim3((unsigned)((a.frames + 255) / 256)), dim3(256), 0, s, a,
-                               a.levels - 1);
+        const dim3 gf((unsigned)((a.frames + 255) / 256));
+        if (nsl == 4)
+            hipLaunchKernelGGL(rvq_final_kernel<4>, gf, dim3(256), 0, s, a, a.levels - 1);
         else
-            hipLaunchKernelGGL(rvq_final_kernel<4>, dim3((unsigned)((a.frames + 255) / 256)), dim3(256), 0, s, a,
-                               a.levels - 1);
+            hipLaunchKernelGGL(rvq_final_kernel<8>, gf, dim3(256), 0, s, a, a.levels - 1);
         return hipGetLastError();
     }
     // small batches (fewer 64-frame workgroups than CUs, B < 16 x 10 s): 32-frame tiles

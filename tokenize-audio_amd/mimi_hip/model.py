@@ -341,7 +341,8 @@ class MimiHipModel:
 
     def set_option(self, key: str, value: int):
         """Kernel-variant option (identical codes either way): "stage0_fused" 0 = stage-0 block and down conv 0 as
-        two kernels, 1 = one fused kernel (default)."""
+        two kernels, 1 = one fused kernel (default); "ln_fused" 0 = LayerNorm launches before q/k/v and fc1, on small
+        grids (batch 1-4) 1 = fc1 computes the LayerNorm of its rows itself (default), 2 = fc1 and q/k/v do."""
         _lib.check(self._lib.mimi_set_option(self._h, key.encode(), int(value)))
 
     def act_scales(self):
