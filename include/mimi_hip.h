@@ -169,7 +169,9 @@ int mimi_set_graphs(mimi_engine* e, int32_t enable);
 int64_t mimi_graph_replays(const mimi_engine* e);
 /* Kernel-variant options (tuning / A-B checks; every setting gives identical codes).  key "stage0_fused":
  * 0 = stage-0 residual block and down conv 0 as two kernels (y through HBM), 1 = one fused kernel (y stays on
- * chip; default).  Unknown keys and values: MIMI_ERR_INVALID_ARGUMENT.  A change drops the captured graphs. */
+ * chip; default).  key "ln_fused": on small grids (batch 1-4) 0 = LayerNorm launches before q/k/v and fc1, 1 = fc1
+ * computes the LayerNorm of its own rows (default), 2 = fc1 and q/k/v do.  Unknown keys and values:
+ * MIMI_ERR_INVALID_ARGUMENT.  A change drops the captured graphs. */
 int mimi_set_option(mimi_engine* e, const char* key, int64_t value);
 /* MIMI_PRECISION_F16X3 diagnostics: per plane tensor (64-char names), its fixed activation scale and the max|x|
  * of the last waited encode (-1: not produced by it); an overflow is max * scale >= 2^15. */
