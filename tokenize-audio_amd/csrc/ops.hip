@@ -149,23 +149,10 @@ hipError_t launch_layernorm(const float* x, const float* g, const float* b, floa
                             unsigned* yamax, const int* row_len, int row_T) {
     if (row_len && row_T <= 0) return hipErrorInvalidValue;
     if (C != 512 || (yns != 0 && !yp) || (yscale > 0.0f && yns != 2)) return hipErrorInvalidValue;
-    // rows per wave (2: 16 rows per workgroup; MIMI_LN_RPW = 1 / 4 for the A/B -- the same arithmetic per row)
-    static const int rpw = [] {
-        const char* v = getenv("MIMI_LN_RPW");
-        const int r = v ? atoi(v) : 2;
-        return (r == 1 || r == 4) ? r : 2;
-    }();
-    const dim3 grid((unsigned)((rows + 8 * rpw - 1) / (8 * rpw)));
-    __bf16* ypb = reinterpret_cast<__bf16*>(yp);
-    if (rpw == 1)
-        hipLaunchKernelGGL((layernorm_kernel<512, 1>), grid, dim3(512), 0, s, x, g, b, y, rows, eps, ypb, y_pstride, yns,
-                           yscale, yamax, row_len, row_T);
-    else if (rpw == 4)
-        hipLaunchKernelGGL((layernorm_kernel<512, 4>), grid, dim3(512), 0, s, x, g, b, y, rows, eps, ypb, y_pstride, yns,
-                           yscale, yamax, row_len, row_T);
-    else
-        hipLaunchKernelGGL((layernorm_kernel<512, 2>), grid, dim3(512), 0, s, x, g, b, y, rows, eps, ypb, y_pstride, yns,
-                           yscale, yamax, row_len, row_T);
+    constexpr int RPW = 2;  // 16 rows per workgroup
+    hipLaunchKernelGGL((layernorm_kernel<512, RPW>), dim3((unsigned)((rows + 8 * RPW - 1) / (8 * RPW))), dim3(512), 0, s,
+                       x, g, b, y,
+                       rows, eps, reinterpret_cast<__bf16*>(yp), y_pstride, yns, yscale, yamax, row_len, row_T);
     return hipGetLastError();
 }
 
