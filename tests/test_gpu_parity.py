@@ -457,9 +457,11 @@ def test_thread_safety(engine):
     assert all(torch.equal(r, ref) for r in results)
 
 
-@pytest.mark.parametrize("mode,tol", [("f32", ACT_TOL), ("bf16x6", ACT_TOL), ("bf16x3", ACT_TOL)])
-def test_precision_modes(engine, golden, mode, tol, state_dict, parity_log):
-    """The non-default GEMM modes stay within the activation tolerance and explain every code flip."""
+@pytest.mark.parametrize("mode,tol,exact_min", [("f32", ACT_TOL, EXACT_MIN), ("bf16x6", ACT_TOL, EXACT_MIN),
+                                                ("bf16x3", ACT_TOL, 0.995)])
+def test_precision_modes(engine, golden, mode, tol, exact_min, state_dict, parity_log):
+    """The non-default GEMM modes stay within the activation tolerance and explain every code flip, with an
+    exact-match floor (bf16x3, the opt-in 2-plane bf16 mode at ~1.3e-5, measured 99.83 % at K = 32: floor 0.995)."""
     arrays, meta = golden
     x = synthetic.speech_like(240000, meta["audio_seed"], 6)
     default = engine.precision
@@ -476,6 +478,7 @@ def test_precision_modes(engine, golden, mode, tol, state_dict, parity_log):
     frac, bad, flips, thr = derived_audit(codes, ref, emb, arrays["emb_speech10s"], state_dict)
     record(parity_log, f"precision[{mode}]", codes, ref, flips, thr, emb_rel_err=rel_err(emb, arrays["emb_speech10s"]))
     assert not bad, (mode, frac, bad[:5])
+    assert frac >= exact_min, (mode, frac)
 
 
 def test_long_clip_without_planes_matches_prefix(engine):

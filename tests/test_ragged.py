@@ -120,3 +120,45 @@ def test_encoder_chunks_and_batches(engine):
     a = np.concatenate([x.ravel() for x in enc.encode_audio_batch(clips[5:11], 24000)])
     b = np.concatenate([x.ravel() for x in literal.encode_audio_batch(clips[5:11], 24000)])
     assert a.shape == b.shape and (a == b).mean() > 0.99
+
+
+def test_encoder_empty_item_in_batch(engine):
+    """An empty item among non-empty ones: the reference pads it and trims it to 0 frames
+    (emilia-mimi/process_shard.py:113-139), so it comes back as (K, 0); the other items are unchanged."""
+    from mimi_hip.encoder import MimiEncoder
+    enc = MimiEncoder(device="cuda:0", model=engine, num_quantizers=8)
+    clips = [synthetic.speech_like(L, 47, i) for i, L in enumerate((30000, 5000))]
+    empty = np.zeros(0, np.float32)
+    got = enc.encode_audio_batch([clips[0], empty, clips[1]], 24000)
+    want = enc.encode_audio_batch(clips, 24000)
+    assert got[1].shape == (8, 0) and got[1].dtype == np.int64
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[2], want[1])
+    literal = MimiEncoder(device="cuda:0", model=engine, num_quantizers=8, ragged=False)
+    assert literal.encode_audio_batch([clips[0], empty], 24000)[1].shape == (8, 0)
+    with pytest.raises(ValueError):
+        enc.encode_audio_batch([empty, empty], 24000)
+
+
+def test_encoder_threads_share_one_encoder(engine):
+    """Several threads calling encode_audio_batch / encode_audio_chunks on ONE MimiEncoder (the YODAS2
+    ThreadPoolExecutor, yodas2-mimi/process_shard.py:691-717) get exactly the serial results: every thread stages
+    through its own pipeline buffers."""
+    from concurrent.futures import ThreadPoolExecutor
+    from mimi_hip.encoder import MimiEncoder
+    enc = MimiEncoder(device="cuda:0", model=engine, num_quantizers=8)
+    jobs = []
+    for j in range(12):
+        lens = synthetic.random_lengths(3 + j % 4, 0.5, 12.0, seed=300 + j)
+        jobs.append([synthetic.speech_like(L, 300 + j, i) for i, L in enumerate(lens)])
+    serial = [enc.encode_audio_batch(b, 24000) if j % 3 else enc.encode_audio_chunks(b, 24000)
+              for j, b in enumerate(jobs)]
+
+    def run(j):
+        b = jobs[j]
+        return enc.encode_audio_batch(b, 24000) if j % 3 else enc.encode_audio_chunks(b, 24000)
+
+    for _ in range(2):
+        with ThreadPoolExecutor(max_workers=4) as ex:
+            par = list(ex.map(run, range(len(jobs))))
+        for j, (s, p) in enumerate(zip(serial, par)):
+            assert len(s) == len(p) and all(np.array_equal(x, y) for x, y in zip(s, p)), j

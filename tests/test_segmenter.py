@@ -52,9 +52,11 @@ def test_missing_audio_leaves_entry_alone():
 
 
 def test_parse_chunk_id():
-    assert parse_chunk_id("Yg-Y2--S7q8-00026-00003279-00003300") == ("Yg-Y2--S7q8", 26, 3279, 3300)
-    with pytest.raises(ValueError):
+    assert parse_chunk_id("Yg-Y2--S7q8-00026-00003279-00003300") == ("Yg-Y2--S7q8", "00026", 3279, 3300)
+    # the reference asserts four parts (yodas2-mimi/process_shard.py:405) and never parses the index field
+    with pytest.raises(AssertionError, match="Invalid chunk_id format"):
         parse_chunk_id("no-dashes")
+    assert parse_chunk_id("a-idx-00000001-00000002")[1] == "idx"
 
 
 def test_bucketed_mode_same_chunks_fewer_pad_samples():

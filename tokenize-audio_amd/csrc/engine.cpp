@@ -1980,7 +1980,9 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
     const bool h16 = prec == PREC_F16X3 && act_planes(e, plan_lengths(e->cfg, L), prec) == 2;
     int rc;
     int n = 0;
-    if (h16 && !e->calibrated && (rc = calibrate_scales(e))) return rc;
+    // Calibrate whenever f16x3 is on, not only when this batch's longest item gets planes: a ragged batch whose
+    // longest item is past the plane limit runs its short items through the planes path item by item.
+    if (prec == PREC_F16X3 && !e->calibrated && (rc = calibrate_scales(e))) return rc;
     RaggedTable rt;
     if (lengths) {
         const mimi_config& c = e->cfg;

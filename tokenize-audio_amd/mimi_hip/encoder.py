@@ -16,6 +16,16 @@ multiple of 1920 needs no extra padding at any stage), which are its own samples
 padding.  So the batch runs as ONE ragged encode (``mimi_encode_ragged``) with item i at length E_i: the codes the
 caller keeps are the padded batch's, and the compute the padding would cost is skipped (U[1.5, 20] s YODAS2
 batches: about 45 % of a pad-to-longest encode).  ``ragged=False`` runs the literal padded encode instead.
+Ragged mode equals the literal padded encode up to near-ties only: an item of 256 or fewer 25 Hz frames can run
+different kernels (the T <= 256 attention instead of the banded one) than the same item inside a longer padded
+batch, so a code whose top-2 distances differ by a rounding error may flip.  Against the reference wrapper's own
+output this path is held to the derived near-tie audit (``tests/test_gpu_parity.py``
+``test_padded_batch_b32_vs_reference_wrapper[ragged]``: 0.999993 exact, the one flip at margin 1e-7).
+An empty item among non-empty ones comes back as a ``(K, 0)`` array, as in the reference's padded batch.
+
+Threads: every thread that calls ``encode_audio_batch`` / ``encode_batches`` / ``encode_audio_chunks`` gets its own
+staging pipeline (pinned, input and output buffers and streams), so concurrent callers sharing one ``MimiEncoder``
+-- the YODAS2 ``ThreadPoolExecutor`` (``yodas2-mimi/process_shard.py:691-717``) -- never share a buffer.
 
 Added for the per-utterance callers (MLS ``mls-en-mimi-pretrain/process_shard.py:268-307`` and LibriSpeech call
 ``encode_audio_chunk`` once per utterance): ``encode_audio_chunks(list, sr)`` returns exactly
@@ -33,6 +43,7 @@ from __future__ import annotations
 
 import logging
 import math
+import threading
 from typing import Iterable, Iterator, List, Optional, Sequence
 
 import numpy as np
@@ -123,7 +134,7 @@ class MimiEncoder:
         self.concurrency = max(1, int(concurrency))  # (kept for API compatibility; ragged batches replace it)
         self.ragged = bool(ragged) and hasattr(self.model, "encode_ragged_async")
         self.chunk_batch = max(1, int(chunk_batch))
-        self._pipe = None
+        self._local = threading.local()  # per-thread _Pipeline (its buffers are never shared between callers)
         logger.info("Mimi model loaded successfully")
 
     @property
@@ -165,9 +176,10 @@ class MimiEncoder:
         return self.model.encode_async(x, self._K).wait().cpu().numpy()
 
     def _pipeline(self) -> _Pipeline:
-        if self._pipe is None:
-            self._pipe = _Pipeline(self.model, self._K)
-        return self._pipe
+        pipe = getattr(self._local, "pipe", None)
+        if pipe is None or pipe.K != self._K:
+            pipe = self._local.pipe = _Pipeline(self.model, self._K)
+        return pipe
 
     def encode_audio_chunk(self, audio_array: np.ndarray, sample_rate: int = 24000) -> np.ndarray:
         with torch.no_grad():
@@ -175,13 +187,16 @@ class MimiEncoder:
             return self._encode_padded([a])[0].astype(np.int64)
 
     def _batch_plan(self, items: List[np.ndarray], sample_rate: int):
-        if any(a.shape[0] == 0 for a in items):
+        if all(a.shape[0] == 0 for a in items):
             raise ValueError("empty audio")
         samples_per_frame = sample_rate / 12.5
         # item i keeps the frames its own samples produce, int(ceil(L_i / samples_per_frame)), of the padded
         # batch's codes (the reference's trim)
         keep = [int(np.ceil(len(a) / samples_per_frame)) for a in items]
-        return padded_batch_lengths([len(a) for a in items]), keep
+        # an empty item keeps 0 frames (the reference pads it and trims to (K, 0)); it is encoded as one zero
+        # sample so the ragged encode has no zero-length item
+        enc = [max(1, n) for n in padded_batch_lengths([len(a) for a in items])]
+        return enc, keep
 
     def encode_audio_batch(self, audio_arrays: List[np.ndarray], sample_rate: int = 24000) -> List[np.ndarray]:
         if len(audio_arrays) == 0:

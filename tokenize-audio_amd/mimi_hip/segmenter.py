@@ -31,14 +31,15 @@ import numpy as np
 __all__ = ["parse_chunk_id", "Segment", "slice_segments", "encode_segments", "process_audio_entry"]
 
 
-def parse_chunk_id(chunk_id: str) -> Tuple[str, int, int, int]:
+def parse_chunk_id(chunk_id: str) -> Tuple[str, str, int, int]:
     """``{audio_id}-{index:05d}-{start_cs:08d}-{end_cs:08d}`` -> (audio_id, index, start_cs, end_cs).
 
-    Ref ``yodas2-mimi/process_shard.py:402-412`` (``rsplit('-', 3)``, asserting four parts)."""
+    Ref ``yodas2-mimi/process_shard.py:402-412``: ``rsplit('-', 3)``, an ``AssertionError`` unless there are four
+    parts, and only the two timestamps parsed as integers (the index field is never parsed, so it stays a string)."""
     parts = chunk_id.rsplit("-", 3)
     if len(parts) != 4:
-        raise ValueError(f"Invalid chunk_id format: {chunk_id}")
-    return parts[0], int(parts[1]), int(parts[2]), int(parts[3])
+        raise AssertionError(f"Invalid chunk_id format: {chunk_id}")
+    return parts[0], parts[1], int(parts[2]), int(parts[3])
 
 
 class Segment:
