@@ -105,6 +105,8 @@ def parse():
                     help="A/B: 0 = LayerNorm launches, 1 = LayerNorm prologue in small-grid q/k/v / fc1 (default)")
     ap.add_argument("--stage0-fused", type=int, default=None,
                     help="kernel variant A/B: 0 = stage-0 block + down conv 0 as two kernels, 1 = fused (default)")
+    ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
+                    help="engine option (mimi_set_option) for A/B runs, e.g. rvq_form=1; repeatable")
     ap.add_argument("--dump-sequence", default=None,
                     help="write the engine's per-encode (stage, kernel) launch sequence here (PMC stage keys)")
     ap.add_argument("--pmc-pass", action="store_true",
@@ -554,6 +556,9 @@ def main():
         model.set_option("stage0_fused", args.stage0_fused)
     if args.ln_fused is not None:
         model.set_option("ln_fused", args.ln_fused)
+    for kv in args.option:
+        k, v = kv.split("=", 1)
+        model.set_option(k, int(v))
     wl = Workload(args, model, dev, world, rank)
     if model.precision == "f16x3":
         model.calibrate()  # (otherwise inside the first encode) -- before the trace marker

@@ -73,6 +73,25 @@ def test_quantizer_bit_exact_on_reference_embedding(engine, golden):
         assert np.array_equal(codes, ref), f"{tag}: {(codes != ref).sum()} of {ref.size} codes differ"
 
 
+@pytest.mark.parametrize("form", [1, 2, 3])
+def test_quantizer_forms_bit_exact(engine, golden, form):
+    """Every RVQ level-kernel form (engine option rvq_form: 1 = three fp16 products, 2 = one product with the widened
+    rigorous window, 3 = one product on 64-frame tiles) gives the reference quantizer's codes bit for bit, on the
+    small-batch grid (one clip) and on the large-batch grid (4 x the 60 s embedding = 3000 frames), at K = 32."""
+    arrays, _ = golden
+    engine.set_option("rvq_form", form)
+    try:
+        for tag in ("speech10s", "noise5s"):
+            emb = torch.from_numpy(arrays[f"emb_{tag}"])[None].cuda()
+            assert np.array_equal(engine.quantize(emb, 32)[0].cpu().numpy(), arrays[f"embcodes_{tag}"]), (form, tag)
+        emb = torch.from_numpy(arrays["emb_speech60s"])[None].repeat(4, 1, 1).cuda()
+        codes = engine.quantize(emb, 32).cpu().numpy()
+        for i in range(4):
+            assert np.array_equal(codes[i], arrays["embcodes_speech60s"]), (form, i)
+    finally:
+        engine.set_option("rvq_form", 0)
+
+
 def test_stage_tensors_within_tolerance(engine, golden):
     arrays, meta = golden
     x = torch.from_numpy(synthetic.speech_like(12000, meta["audio_seed"], 100))[None, None].cuda()

@@ -329,6 +329,7 @@ struct mimi_engine {
     // (rocprofv3, profiles/r3j_*): fc1 15.0 us with it vs 10.1 + 5.2 us (+ a launch gap) for fc1 + LayerNorm; q/k/v
     // 20.8 vs 10.4 + 5.2 us -- its one compute wave and 16-row tiles leave the prologue's chain exposed
     int ln_fused = 1;
+    int rvq_form = 0;  // RVQ level-kernel form (mimi_set_option "rvq_form"; RvqArgs::form)
     struct Tap {
         float* d = nullptr;
         size_t cap = 0;
@@ -1210,6 +1211,7 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     r.codes = codes;
     r.codes_ref = e->capturing ? reinterpret_cast<int32_t* const*>(e->io_dev + 1) : nullptr;
     r.frames_per_item = frames_per_item;
+    r.form = e->rvq_form;
     const char* kname = "?";
     LAUNCH_TRY(launch_rvq(r, s, &kname), "rvq");
     rec.mark("rvq", 2.0 * frames * valid_share * r.D * r.ncodes * K,
@@ -2285,6 +2287,16 @@ extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {
             e->graph_seen.clear();
         }
         e->stage0_fused = (int)value;
+        return MIMI_OK;
+    }
+    if (!strcmp(key, "rvq_form")) {
+        if (value < 0 || value > 3) return set_err(MIMI_ERR_INVALID_ARGUMENT, "rvq_form %lld (0..3)", (long long)value);
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->rvq_form != (int)value) {
+            drop_graphs(e);
+            e->graph_seen.clear();
+        }
+        e->rvq_form = (int)value;
         return MIMI_OK;
     }
     if (!strcmp(key, "ln_fused")) {

@@ -1442,26 +1442,33 @@ constexpr int RVQ_CAND = 2048;
 // large-batch form takes 64 (4 slices: 500 workgroups at B = 32 x 10 s -- one round of two per CU -- instead of 1000
 // in two rounds, each round paying the whole merge / residual / |r|^2 / plane prologue chain again).
 // NWV: waves per workgroup (8; 2 and 4 were timed for small grids, not kept: launch_rvq)
-template <int D, int PF = 4, int EX = 16, bool RG = false, int CW = 32, int NWV = 8>
+// FT: frames per workgroup (32, or 64: a workgroup streams its codebook slice once for twice the frames -- half the
+// L2 -> CU codebook bytes per level).  P1 (round 4): the approximate distance is ONE fp16 product (hi planes of r and
+// of the codebook, v_mfma_f32_32x32x16_f16) instead of three, with the window widened to that product's rigorous
+// error bound (below): a third of the MFMAs and half the codebook bytes; the exact re-score decides, so the codes are
+// the same bits.
+template <int D, int PF = 4, int EX = 16, bool RG = false, int CW = 32, int NWV = 8, int FT = 32, bool P1 = false>
 // (HIP's second launch bound is waves per SIMD: 4 = two 8-wave workgroups per CU, i.e. <= 128 VGPRs)
-__global__ __launch_bounds__(64 * NWV, PF <= 4 ? 4 : 2) void rvq_level_h16_kernel(RvqArgs p, int L0) {
+__global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_level_h16_kernel(RvqArgs p, int L0) {
     constexpr int NT = 64 * NWV;          // threads
     constexpr int TNC = CW / 32;          // 32-code MFMA tiles per wave
+    constexpr int RT = FT / 32;           // 32-frame MFMA row tiles
     constexpr int SLC = NWV * CW;         // codes per slice
     constexpr int NSL = 2048 / SLC;       // slices
+    constexpr int NPL = P1 ? 1 : 2;       // fp16 planes of r and of the codebook the approximation reads
     static_assert(NSL <= 32 && NSL % 4 == 0, "slices: rvq_work_bytes, rvq_merge");
+    static_assert(FT == 32 || FT == 64, "frame tile (RVQ_FT pads the work layout to 64)");
     // RG (a ragged batch: p.flen): a workgroup none of whose frames is valid has nothing to do -- no later level
     // reads what it would write (only valid frames' residuals and partial argmins are ever read)
     if constexpr (RG) {
-        if (!__syncthreads_or((int)threadIdx.x < 32 && rvq_valid(p, (long long)blockIdx.x * 32 + threadIdx.x))) return;
+        if (!__syncthreads_or((int)threadIdx.x < FT && rvq_valid(p, (long long)blockIdx.x * FT + threadIdx.x))) return;
     }
     const int L = L0 + (int)blockIdx.z;  // (grid.z = 2: the semantic and first acoustic levels together)
-    constexpr int FT = 32;
     constexpr int LDH = D / 2 + 4;
     constexpr int RLD = D + 8;  // fp16 plane rows: 528 B = 132 dwords (conflict-free b128 fragment reads)
     typedef _Float16 h8 __attribute__((ext_vector_type(8)));
     __shared__ __attribute__((aligned(16))) float img[2][FT][LDH];  // -2 r, split by k parity (exact chain)
-    __shared__ __attribute__((aligned(16))) _Float16 rpl[2][FT][RLD];  // fp16 planes of r * rs
+    __shared__ __attribute__((aligned(16))) _Float16 rpl[NPL][FT][RLD];  // fp16 planes of r * rs
     __shared__ float xn[FT], rus[FT], win[FT], smin[FT];
     __shared__ int prev[FT];
     __shared__ float redd[NWV][FT];
@@ -1543,7 +1550,7 @@ __global__ __launch_bounds__(64 * NWV, PF <= 4 ? 4 : 2) void rvq_level_h16_kerne
         }
     }
     __syncthreads();
-    // fp16 planes of r * rs
+    // fp16 planes of r * rs (P1: the hi plane only)
     for (int idx = tid; idx < FT * D / 2; idx += NT) {
         const int i = idx / (D / 2), k = (idx % (D / 2)) * 2;
         const float rs = -0.5f * win[i];
@@ -1551,8 +1558,10 @@ __global__ __launch_bounds__(64 * NWV, PF <= 4 ? 4 : 2) void rvq_level_h16_kerne
         const _Float16 a0 = (_Float16)t0, a1 = (_Float16)t1;
         rpl[0][i][k] = a0;
         rpl[0][i][k + 1] = a1;
-        rpl[1][i][k] = (_Float16)(t0 - (float)a0);
-        rpl[1][i][k + 1] = (_Float16)(t1 - (float)a1);
+        if constexpr (!P1) {
+            rpl[NPL - 1][i][k] = (_Float16)(t0 - (float)a0);
+            rpl[NPL - 1][i][k + 1] = (_Float16)(t1 - (float)a1);
+        }
     }
     __syncthreads();
 
@@ -1562,42 +1571,53 @@ __global__ __launch_bounds__(64 * NWV, PF <= 4 ? 4 : 2) void rvq_level_h16_kerne
     const h8* bp = reinterpret_cast<const h8*>(p.cb_h16) +
                    ((long long)L * (p.ncodes / 32) + code0 / 32) * (D / 16) * 2 * 64 + lane;
     constexpr int TST = (D / 16) * 2 * 64;  // h8 per 32-code block of the fragment image
-    f32x16 acc[TNC];
+    f32x16 acc[RT][TNC];
 #pragma unroll
-    for (int t = 0; t < TNC; ++t)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-    h8 bq[PF][TNC][2];
+        for (int t = 0; t < TNC; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.0f;
+    h8 bq[PF][TNC][NPL];
 #pragma unroll
     for (int q = 0; q < PF; ++q)
 #pragma unroll
-        for (int t = 0; t < TNC; ++t) {
-            bq[q][t][0] = bp[t * TST + q * 128];
-            bq[q][t][1] = bp[t * TST + q * 128 + 64];
-        }
+        for (int t = 0; t < TNC; ++t)
+#pragma unroll
+            for (int pl = 0; pl < NPL; ++pl) bq[q][t][pl] = bp[t * TST + q * 128 + pl * 64];
     auto kstep = [&](int ks) {
         const int cur = ks % PF;
-        h8 b0[TNC], b1[TNC];
+        h8 bb[TNC][NPL];
 #pragma unroll
-        for (int t = 0; t < TNC; ++t) {
-            b0[t] = bq[cur][t][0];
-            b1[t] = bq[cur][t][1];
-        }
+        for (int t = 0; t < TNC; ++t)
+#pragma unroll
+            for (int pl = 0; pl < NPL; ++pl) bb[t][pl] = bq[cur][t][pl];
         if (ks + PF < D / 16) {
 #pragma unroll
-            for (int t = 0; t < TNC; ++t) {
-                bq[cur][t][0] = bp[t * TST + (ks + PF) * 128];
-                bq[cur][t][1] = bp[t * TST + (ks + PF) * 128 + 64];
+            for (int t = 0; t < TNC; ++t)
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl) bq[cur][t][pl] = bp[t * TST + (ks + PF) * 128 + pl * 64];
+        }
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+            const h8 a0 = *reinterpret_cast<const h8*>(&rpl[0][i * 32 + (lane & 31)][ks * 16 + 8 * h]);
+            if constexpr (P1) {
+#pragma unroll
+                for (int t = 0; t < TNC; ++t)
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[t][0], acc[i][t], 0, 0, 0);
+            } else {
+                const h8 a1 = *reinterpret_cast<const h8*>(&rpl[NPL - 1][i * 32 + (lane & 31)][ks * 16 + 8 * h]);
+#pragma unroll
+                for (int t = 0; t < TNC; ++t) {
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bb[t][0], acc[i][t], 0, 0, 0);
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[t][NPL - 1], acc[i][t], 0, 0, 0);
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[t][0], acc[i][t], 0, 0, 0);
+                }
             }
         }
-        const h8 a0 = *reinterpret_cast<const h8*>(&rpl[0][lane & 31][ks * 16 + 8 * h]);
-        const h8 a1 = *reinterpret_cast<const h8*>(&rpl[1][lane & 31][ks * 16 + 8 * h]);
-#pragma unroll
-        for (int t = 0; t < TNC; ++t) {
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0[t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1[t], acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0[t], acc[t], 0, 0, 0);
-        }
+        // P1 with PF k-steps in flight: keep the scheduler from hoisting later k-steps' codebook loads above these
+        // MFMAs (with one product per k-step it did, holding every k-step's fragments live: 128-256 VGPRs, spills)
+        if constexpr (P1 && PF < 16) __builtin_amdgcn_sched_barrier(0);
     };
     // (a template-dependent `#pragma unroll PF` is not honoured by hipcc -- the loop is then fully unrolled and
     // the prefetch loads sunk to their uses -- so the depths spell their unroll factor out)
@@ -1613,26 +1633,28 @@ __global__ __launch_bounds__(64 * NWV, PF <= 4 ? 4 : 2) void rvq_level_h16_kerne
         for (int ks = 0; ks < D / 16; ++ks) kstep(ks);
     }
     const float cus = p.cb_unscale[L];
-    float ad[TNC][16];
-    float mrow[16];
 #pragma unroll
-    for (int t = 0; t < TNC; ++t) {
-        const int code = code0 + 32 * t + (lane & 31);
-        const float yn = p.cb_norm[(long long)L * p.ncodes + code];
+    for (int i = 0; i < RT; ++i) {
+        float mrow[16];
+#pragma unroll
+        for (int t = 0; t < TNC; ++t) {
+            const int code = code0 + 32 * t + (lane & 31);
+            const float yn = p.cb_norm[(long long)L * p.ncodes + code];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                acc[i][t][r] = (-2.0f * (acc[i][t][r] * (rus[row] * cus)) + xn[row]) + yn;  // approx d^2
+                mrow[r] = t == 0 ? acc[i][t][r] : fminf(mrow[r], acc[i][t][r]);
+            }
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            ad[t][r] = (-2.0f * (acc[t][r] * (rus[row] * cus)) + xn[row]) + yn;
-            mrow[r] = t == 0 ? ad[t][r] : fminf(mrow[r], ad[t][r]);
+            const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float m = mrow[r];
+#pragma unroll
+            for (int o = 16; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+            if ((lane & 31) == 0) redd[wave][row] = m;
         }
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        float m = mrow[r];
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o));
-        if ((lane & 31) == 0) redd[wave][row] = m;
     }
     __syncthreads();
     if (tid < FT) {
@@ -1641,23 +1663,37 @@ __global__ __launch_bounds__(64 * NWV, PF <= 4 ? 4 : 2) void rvq_level_h16_kerne
         for (int q = 1; q < NWV; ++q) m = fminf(m, redd[q][tid]);
         smin[tid] = m;
         const float emax = p.cb_emax[L];
-        const float rn = __builtin_sqrtf(fmaxf(xn[tid], 0.0f)) + emax;
-        win[tid] = ldexpf(rn * rn, -11) + ldexpf(fabsf(m), -20) + 1e-30f;
+        const float rnorm = __builtin_sqrtf(fmaxf(xn[tid], 0.0f));
+        const float rn = rnorm + emax;
+        if constexpr (P1) {
+            // one fp16 product: per element |r_k e_k - rh_k eh_k| <= (2 2^-11 + 2^-22) |r_k e_k| (fp16 unit roundoff; a
+            // subnormal rounding adds at most 2^-25 / scale per element, far below), so the approximate dot product is
+            // within (2^-10 + 2^-22) sum |r_k e_k| <= 1.0001 2^-10 |r| |e| of the true one, the MFMA's fp32 accumulation
+            // within 2^-19 |r| |e| more and the reference's fp32 chain within gamma_256 < 2^-15.9 |r| |e|.  A d^2 moves
+            // by twice the dot-product error: both the candidate and the slice minimum by <= 1.04 2^-9 |r| emax, so the
+            // exact argmin lies within 1.04 2^-8 |r| emax of the approximate minimum; plus the final adds' rounding
+            // (<= 2^-22 (|r| + emax)^2 each) and the sqrt / compare slack.
+            win[tid] = ldexpf(1.06f * rnorm * emax, -8) + ldexpf(rn * rn, -18) + ldexpf(fabsf(m), -20) + 1e-30f;
+        } else {
+            win[tid] = ldexpf(rn * rn, -11) + ldexpf(fabsf(m), -20) + 1e-30f;
+        }
     }
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < TNC; ++t) {
-        const int code = code0 + 32 * t + (lane & 31);
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            // NaN distances (a non-finite residual) are candidates too: the exact path decides
-            if (!(ad[t][r] > smin[row] + win[row]) && f0 + row < p.frames) {
-                const unsigned slot = atomicAdd(&ncand, 1u);
-                if (slot < RVQ_CAND) cand[slot] = ((unsigned)row << 16) | (unsigned)(code - slice * SLC);
+        for (int t = 0; t < TNC; ++t) {
+            const int code = code0 + 32 * t + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                // NaN distances (a non-finite residual) are candidates too: the exact path decides
+                if (!(acc[i][t][r] > smin[row] + win[row]) && f0 + row < p.frames) {
+                    const unsigned slot = atomicAdd(&ncand, 1u);
+                    if (slot < RVQ_CAND) cand[slot] = ((unsigned)row << 16) | (unsigned)(code - slice * SLC);
+                }
             }
         }
-    }
     __syncthreads();
     // ---- exact re-scoring: the candidates, or (degenerate: the list overflowed) every code of the slice
     const float* cbr = p.cb_rows + (long long)L * p.ncodes * D;
@@ -1670,6 +1706,8 @@ __global__ __launch_bounds__(64 * NWV, PF <= 4 ? 4 : 2) void rvq_level_h16_kerne
         if (f0 + row >= p.frames) continue;
         const f32x4* e = reinterpret_cast<const f32x4*>(cbr + (long long)c * D);
         float a = 0.0f;
+        // (not unrolled: unrolled, hipcc hoisted every round's loads -- the whole 1-KB row in 256 VGPRs -- and spilled)
+#pragma unroll 1
         for (int k0 = 0; k0 < D / 4; k0 += EX) {  // EX float4 of the code row in flight, then the in-order chain
             f32x4 ev[EX];
 #pragma unroll
@@ -1710,33 +1748,47 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
         // small batches (fewer 256-code-slice workgroups than CUs): 8 slices, every codebook k-step in flight at once
         // and half a code row per exact round -- the same arithmetic, latency-bound waves wait once instead of four
         // times; large batches: 4 slices of 512 codes (64 per wave, 2 k-steps in flight per 32-code tile)
-        const unsigned ftiles = (unsigned)((a.frames + 31) / 32);
-        const bool small = ftiles * 8 < 256;
+        const unsigned ftiles32 = (unsigned)((a.frames + 31) / 32);
+        const bool small = ftiles32 * 8 < 256;
         const bool split = a.sem_split != 0;  // levels 0 and 1 in one launch (rvq_sem_split)
         // (2- and 4-wave workgroups on small grids -- 32 / 16 slices, 4x / 2x the workgroups, each streaming a quarter /
         // half of the codebook bytes -- were slower at batch 1 and 4: rvq 0.14 -> 0.21 / 0.16 ms per batch-1 encode,
         // the per-workgroup prologue chain on fewer threads outweighs the shorter stream; profiles/r3j_ab_*)
+        // form: 1 = three fp16 products (round 3), 2 = one product (P1), 3 = one product, 64-frame tiles (large
+        // batches only); 0 = the default
+        const int form = a.form == 0 ? 1 : a.form;
+        const bool p1 = form >= 2;
+        const int ft = (!small && form == 3) ? 64 : 32;
+        const unsigned ftiles = (unsigned)((a.frames + ft - 1) / ft);
         constexpr int nwv = 8;
         const unsigned nsl = 2048 / (small ? nwv * 32 : 8 * 64);
-        static char kn[96];
-        snprintf(kn, sizeof kn, "mimi::rvq_level_h16_kernel<256, %d, %d, %s, %d, %d>", small ? 16 : 2, small ? 32 : 16,
-                 a.flen ? "true" : "false", small ? 32 : 64, nwv);
+        static char kn[112];
+        snprintf(kn, sizeof kn, "mimi::rvq_level_h16_kernel<256, %d, %d, %s, %d, %d, %d, %s>", small ? 16 : 2,
+                 small ? 32 : 16, a.flen ? "true" : "false", small ? 32 : 64, nwv, ft, p1 ? "true" : "false");
         *kname = kn;
         for (int L = 0; L < a.levels; L += (split && L == 0) ? 2 : 1) {
             const dim3 g(ftiles, nsl, (split && L == 0) ? 2 : 1);
             const dim3 blk(64 * nwv);
             // (ragged, RG: workgroups of invalid frames exit)
-#define RVQ_LAUNCH(PF_, EX_, CW_, NWV_)                                                                   \
-    do {                                                                                                  \
-        if (a.flen)                                                                                       \
-            hipLaunchKernelGGL((rvq_level_h16_kernel<256, PF_, EX_, true, CW_, NWV_>), g, blk, 0, s, a, L);  \
-        else                                                                                              \
-            hipLaunchKernelGGL((rvq_level_h16_kernel<256, PF_, EX_, false, CW_, NWV_>), g, blk, 0, s, a, L); \
+#define RVQ_LAUNCH(PF_, EX_, CW_, NWV_, FT_, P1_)                                                                   \
+    do {                                                                                                            \
+        if (a.flen)                                                                                                 \
+            hipLaunchKernelGGL((rvq_level_h16_kernel<256, PF_, EX_, true, CW_, NWV_, FT_, P1_>), g, blk, 0, s, a, L);  \
+        else                                                                                                        \
+            hipLaunchKernelGGL((rvq_level_h16_kernel<256, PF_, EX_, false, CW_, NWV_, FT_, P1_>), g, blk, 0, s, a, L); \
     } while (0)
-            if (!small)
-                RVQ_LAUNCH(2, 16, 64, 8);
-            else
-                RVQ_LAUNCH(16, 32, 32, 8);
+            if (small) {
+                if (p1)
+                    RVQ_LAUNCH(16, 32, 32, 8, 32, true);
+                else
+                    RVQ_LAUNCH(16, 32, 32, 8, 32, false);
+            } else if (!p1) {
+                RVQ_LAUNCH(2, 16, 64, 8, 32, false);
+            } else if (ft == 64) {
+                RVQ_LAUNCH(2, 16, 64, 8, 64, true);
+            } else {
+                RVQ_LAUNCH(2, 16, 64, 8, 32, true);
+            }
 #undef RVQ_LAUNCH
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
