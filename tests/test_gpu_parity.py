@@ -92,6 +92,20 @@ def test_quantizer_forms_bit_exact(engine, golden, form):
         engine.set_option("rvq_form", 0)
 
 
+def test_kernel_options_identical_codes(engine):
+    """Kernel-variant options change no bit: sc1 output stores on the transformer GEMMs (sc1_out, large-batch tiles)
+    and every RVQ form, on a B = 16 x 10 s batch at K = 32."""
+    x = torch.from_numpy(synthetic.clip_batch(16, 240000, seed=88))[:, None].cuda()
+    base = engine.encode(x, num_quantizers=32).audio_codes.cpu()
+    for key, val in (("sc1_out", 7), ("rvq_form", 1), ("rvq_form", 2), ("rvq_form", 3)):
+        engine.set_option(key, val)
+        try:
+            got = engine.encode(x, num_quantizers=32).audio_codes.cpu()
+        finally:
+            engine.set_option(key, 0)
+        assert torch.equal(got, base), (key, val, int((got != base).sum()))
+
+
 def test_stage_tensors_within_tolerance(engine, golden):
     arrays, meta = golden
     x = torch.from_numpy(synthetic.speech_like(12000, meta["audio_seed"], 100))[None, None].cuda()

@@ -330,6 +330,9 @@ struct mimi_engine {
     // 20.8 vs 10.4 + 5.2 us -- its one compute wave and 16-row tiles leave the prologue's chain exposed
     int ln_fused = 1;
     int rvq_form = 0;  // RVQ level-kernel form (mimi_set_option "rvq_form"; RvqArgs::form)
+    // transformer GEMMs with sc1 output stores (gemm_planes.h FL_SC1OUT; mimi_set_option "sc1_out"): bit 0 q/k/v,
+    // bit 1 fc1, bit 2 o_proj and fc2 (large batches; the same bits either way)
+    int sc1_out = 0;
     struct Tap {
         float* d = nullptr;
         size_t cap = 0;
@@ -1544,6 +1547,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                        "ln1");
             rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
         }
+        aq.sc1 = (e->sc1_out & 1) != 0;
         LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, prec), "qkv");
         rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
         if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, tapB, tapT, 3 * H * Dh, s))) return rc;
@@ -1565,6 +1569,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         ao.scale = x.ls1;
         if (ns) planes_in(ao, w.att, nact);
         use_h(ao, x.wo_h, x.wo_hs, atta);
+        ao.sc1 = (e->sc1_out & 4) != 0;
         LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
         rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
         if ((rc = save_tap(e, nmf("oproj%d", l).c_str(), w.t0, tapB, tapT, Hd, s))) return rc;
@@ -1587,6 +1592,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                        "ln2");
             rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
         }
+        a1.sc1 = (e->sc1_out & 2) != 0;
         LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, prec), "fc1");
         rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
         if ((rc = save_tap_planes(e, nmf("ff%d", l).c_str(), w.ff, ns, tapB, tapT, c.intermediate_size, s, ffa.scale)))
@@ -1603,6 +1609,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             dsin = new_act("ds.in");
             out_act(a2, dsin);
         }
+        a2.sc1 = (e->sc1_out & 4) != 0;
         LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname, prec), "fc2");
         rec.mark("fc2", gemm_flops(a2), gemm_bytes(a2, true), kname);
         snprintf(nm, sizeof nm, "xfmr%d", l);
@@ -2297,6 +2304,16 @@ extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {
             e->graph_seen.clear();
         }
         e->rvq_form = (int)value;
+        return MIMI_OK;
+    }
+    if (!strcmp(key, "sc1_out")) {
+        if (value < 0 || value > 7) return set_err(MIMI_ERR_INVALID_ARGUMENT, "sc1_out %lld (0..7)", (long long)value);
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->sc1_out != (int)value) {
+            drop_graphs(e);
+            e->graph_seen.clear();
+        }
+        e->sc1_out = (int)value;
         return MIMI_OK;
     }
     if (!strcmp(key, "ln_fused")) {

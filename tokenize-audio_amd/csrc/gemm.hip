@@ -91,6 +91,11 @@ static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
     const long long nwg = (long long)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.batch;
     if (nwg > 0x7fffffffLL) return hipErrorInvalidValue;
     if (F16 && ((OUTP & 7) ? a.out_scale <= 0.0f : false)) return hipErrorInvalidValue;
+    if constexpr ((FL & FL_SC1OUT) != 0) {  // 32-bit byte offsets from an item's output base (gemm_planes.h)
+        const long long rows = (FL & FL_RAGGED) ? (long long)a.M : (long long)a.M;
+        if ((rows * a.ldc + a.N) * 4 > 0x7fffffffLL || ((OUTP & 7) && (a.c_pstride + rows * a.ldc) * 2 > 0x7fffffffLL))
+            return run_planes<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL & ~FL_SC1OUT, F16>(a, s);
+    }
     auto kern = gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL, F16>;
     long long grid = nwg;
     if (FL & FL_PERSIST) {  // one workgroup per resident slot, a multiple of the 8 XCDs
@@ -140,7 +145,10 @@ static hipError_t run_planes_small_ld(const GemmArgs& a, hipStream_t s, int prec
     // fp16: 3 stages (o_proj / fc2 -2 %, final conv equal vs 4; profiles/r1l_ab_small_kernels.txt); 8 compute
     // waves instead of 4 (N = 512: 252 tiles, one round, so shorter per-tile chains win): o_proj -3 %, fc2 -1.4 %
     // (profiles/r2e_ab_8waves_oproj_fc2.log)
-    if (prec == PREC_F16X3) return run_planes<128, 128, 4, 2, 2, 3, EPI, 0, TAG, 4, 32, 16, 0, true>(a, s);
+    if (prec == PREC_F16X3) {
+        if (a.sc1) return run_planes<128, 128, 4, 2, 2, 3, EPI, 0, TAG, 4, 32, 16, FL_SC1OUT, true>(a, s);
+        return run_planes<128, 128, 4, 2, 2, 3, EPI, 0, TAG, 4, 32, 16, 0, true>(a, s);
+    }
     if (prec == PREC_BF16X6) return run_planes<128, 128, 2, 2, 3, 3, EPI, 0, TAG, 4>(a, s);
     return run_planes<128, 128, 2, 2, 2, 3, EPI, 0, TAG, 4>(a, s);
 }
@@ -303,6 +311,8 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
                         // non-persistent ring (profiles/r3c_ab_qkv_fc1.log; the same for fc1 measured +6 %)
             if (prec == PREC_F16X3) {
 #if MIMI_QKV_V == 1
+                if (a.sc1)
+                    return run_planes<128, 128, 4, 2, 2, 3, EPI_ROPE, 0, 5, 4, 32, 16, FL_PERSIST | FL_PF | FL_SC1OUT, true>(a, s);
                 return run_planes<128, 128, 4, 2, 2, 3, EPI_ROPE, 0, 5, 4, 32, 16, FL_PERSIST | FL_PF, true>(a, s);
 #elif MIMI_QKV_V == 2
                 return run_planes<128, 128, 4, 2, 2, 2, EPI_ROPE, 0, 5, 0, 32, 16, 0, true>(a, s);
@@ -321,6 +331,7 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
 #if MIMI_FC1_V == 1
                 return run_planes<128, 128, 4, 2, 2, 3, EPI_GELU, 2, 7, 4, 32, 16, FL_PERSIST | FL_PF, true>(a, s);
 #else
+                if (a.sc1) return run_planes<128, 128, 4, 2, 2, 2, EPI_GELU, 2, 7, 0, 32, 16, FL_SC1OUT, true>(a, s);
                 return run_planes<128, 128, 4, 2, 2, 2, EPI_GELU, 2, 7, 0, 32, 16, 0, true>(a, s);
 #endif
             }

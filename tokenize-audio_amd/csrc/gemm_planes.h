@@ -94,8 +94,12 @@ __device__ __forceinline__ int chunk_swz(int row) {
 //           image of the whole K = 512 (same rows, chunk swizzle and K-step layout as the DMA'd A images): the ring
 //           carries B only and the LayerNorm launch + its planes' HBM round trip are gone.  Small grids only (the
 //           LayerNorm is recomputed per N tile; a 512-wide A image is BM x 2 KiB of LDS).
+//           FL_SC1OUT -- the epilogue's output stores are `sc1` buffer stores (MI355X_MICROARCH.md: an sc1 store drops
+//           the line from the XCD's L2, a plain one keeps it): a large output stream then no longer evicts the weight
+//           planes every tile of the XCD re-reads from its L2.  Byte offsets from the item's C / planes base are 32-bit
+//           (run_planes checks).
 enum : int { FL_PRIO = 2, FL_PAIR = 4, FL_PERSIST = 8, FL_KG2 = 16, FL_KG4 = 32, FL_PF = 256, FL_RAGGED = 512,
-             FL_LNA = 2048 };
+             FL_LNA = 2048, FL_SC1OUT = 4096 };
 // tuning diagnostics (tools/gemm_bench.hip only; results are garbage): no DMA refills after the prologue / no MFMAs
 enum : int { FL_DIAG_NODMA = 64, FL_DIAG_NOMMA = 128 };
 // timing probe of an interleaved plane layout (tools/gemm_bench.hip only, results garbage): the loader waves fetch
@@ -638,6 +642,12 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     float* __restrict__ Cb = p.C ? p.C + c_base_of(b) : nullptr;
     static_assert(!F16 || ONS == 0 || ONS == 2, "fp16 output planes: 2");
     __bf16* __restrict__ Cpb = ONS ? reinterpret_cast<__bf16*>(p.Cp) + c_base_of(b) : nullptr;
+    constexpr bool SC1 = (FL & FL_SC1OUT) != 0;
+    static_assert(!SC1 || !ONS || F16, "sc1 output stores: fp32 and fp16 planes");
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    // (SC1: buffer resources over the item's output; a null base only ever meets a store that is not issued)
+    const __amdgpu_buffer_rsrc_t c_rs = make_rsrc(SC1 ? (void*)Cb : nullptr, SC1 ? 0x7fffffffLL : 0);
+    const __amdgpu_buffer_rsrc_t cp_rs = make_rsrc(SC1 ? (void*)Cpb : nullptr, SC1 ? 0x7fffffffLL : 0);
     constexpr int LPR = CWC / 8;  // lanes per row
     constexpr int RPS = 64 / LPR;  // rows per pass
     static_assert(RW % RPS == 0, "epilogue: a wave's tile holds whole passes of 64 lanes x 8 columns");
@@ -666,11 +676,31 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
 #pragma unroll
                 for (int e = 0; e < 8; ++e) pv[e] = elu1(pv[e]);
             }
-            store_act8(Cpb, p.c_pstride, ONS, off, pv, F16 ? p.out_scale : 0.0f, &omx);
+            if constexpr (SC1) {  // store_act8's fp16 split, stored sc1
+                typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+                f16x8_t ha, hb;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float t = pv[e] * p.out_scale;
+                    ha[e] = (_Float16)t;
+                    hb[e] = (_Float16)(t - (float)ha[e]);
+                    omx = fmaxf(omx, fabsf(pv[e]));
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ha), cp_rs, (int)(off * 2), 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hb), cp_rs,
+                                                       (int)((off + p.c_pstride) * 2), 0, 16);
+            } else {
+                store_act8(Cpb, p.c_pstride, ONS, off, pv, F16 ? p.out_scale : 0.0f, &omx);
+            }
         }
         if (Cb) {
-            *reinterpret_cast<f32x4*>(Cb + off) = v0;
-            *reinterpret_cast<f32x4*>(Cb + off + 4) = v1;
+            if constexpr (SC1) {
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), c_rs, (int)(off * 4), 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), c_rs, (int)(off * 4 + 16), 0, 16);
+            } else {
+                *reinterpret_cast<f32x4*>(Cb + off) = v0;
+                *reinterpret_cast<f32x4*>(Cb + off + 4) = v1;
+            }
         }
     }
     asm volatile("" ::: "memory");  // this pass's staging reads precede the next pass's writes (same wave)

@@ -226,6 +226,9 @@ struct GemmArgs {
     float ln_eps;
     float ln_scale;
     unsigned* ln_amax;
+    // host-side dispatch hint (not read by the kernels): 1 = take the FL_SC1OUT instantiation where the role has one
+    // (engine option sc1_out; the same bits either way)
+    int sc1;
 };
 // true when launch_gemm(role, a, precision) runs a tile with the LayerNorm prologue (a.ln_* then feed A)
 bool gemm_ln_prologue_ok(int role, const GemmArgs& a, int precision);
