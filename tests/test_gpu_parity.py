@@ -73,10 +73,11 @@ def test_quantizer_bit_exact_on_reference_embedding(engine, golden):
         assert np.array_equal(codes, ref), f"{tag}: {(codes != ref).sum()} of {ref.size} codes differ"
 
 
-@pytest.mark.parametrize("form", [1, 2, 3])
+@pytest.mark.parametrize("form", [1, 2, 3, 4, 5, 6])
 def test_quantizer_forms_bit_exact(engine, golden, form):
     """Every RVQ level-kernel form (engine option rvq_form: 1 = three fp16 products, 2 = one product with the widened
-    rigorous window, 3 = one product on 64-frame tiles) gives the reference quantizer's codes bit for bit, on the
+    rigorous window, 3 = one product on 64-frame tiles, 4 / 5 = 4 / 8 codebook k-steps in flight, 6 = the small-batch
+    form at every batch size) gives the reference quantizer's codes bit for bit, on the
     small-batch grid (one clip) and on the large-batch grid (4 x the 60 s embedding = 3000 frames), at K = 32."""
     arrays, _ = golden
     engine.set_option("rvq_form", form)
@@ -97,13 +98,39 @@ def test_kernel_options_identical_codes(engine):
     and every RVQ form, on a B = 16 x 10 s batch at K = 32."""
     x = torch.from_numpy(synthetic.clip_batch(16, 240000, seed=88))[:, None].cuda()
     base = engine.encode(x, num_quantizers=32).audio_codes.cpu()
-    for key, val in (("sc1_out", 7), ("rvq_form", 1), ("rvq_form", 2), ("rvq_form", 3)):
+    defaults = {"sc1_out": 2, "rvq_form": 0, "rvq_chain": 0}
+    cases = [("sc1_out", 0), ("sc1_out", 7), ("rvq_chain", 1)] + [("rvq_form", f) for f in range(1, 7)]
+    for key, val in cases:
         engine.set_option(key, val)
         try:
             got = engine.encode(x, num_quantizers=32).audio_codes.cpu()
         finally:
-            engine.set_option(key, 0)
+            engine.set_option(key, defaults[key])
         assert torch.equal(got, base), (key, val, int((got != base).sum()))
+
+
+@pytest.mark.parametrize("chain", [0, 1])
+def test_quantizer_chain_small_grids(engine, golden, chain):
+    """Small grids (up to 4 frame tiles = 128 frames per chain): the persistent all-levels RVQ (rvq_chain = 1) gives the
+    reference quantizer's codes bit for bit at K = 32, K = 8, K = 2 and K = 1 (semantic level only), and an end-to-end
+    batch-1 encode equals the per-level launches' codes."""
+    arrays, _ = golden
+    engine.set_option("rvq_chain", chain)
+    try:
+        for tag in ("speech10s", "noise5s"):
+            emb = torch.from_numpy(arrays[f"emb_{tag}"])[None].cuda()
+            ref = arrays[f"embcodes_{tag}"]
+            for K in (32, 8, 2, 1):
+                assert np.array_equal(engine.quantize(emb, K)[0].cpu().numpy(), ref[:K]), (chain, tag, K)
+        # 3 frames (a ragged-sized tail tile) and 1 frame
+        emb = torch.from_numpy(arrays["emb_speech10s"][:, :3])[None].cuda()
+        assert np.array_equal(engine.quantize(emb, 32)[0].cpu().numpy(), arrays["embcodes_speech10s"][:, :3])
+        x = torch.from_numpy(synthetic.speech_like(200000, 91, 0))[None, None].cuda()
+        got = engine.encode(x, num_quantizers=32).audio_codes.cpu()
+    finally:
+        engine.set_option("rvq_chain", 0)
+    base = engine.encode(x, num_quantizers=32).audio_codes.cpu()
+    assert torch.equal(got, base)
 
 
 def test_stage_tensors_within_tolerance(engine, golden):

@@ -330,9 +330,10 @@ struct mimi_engine {
     // 20.8 vs 10.4 + 5.2 us -- its one compute wave and 16-row tiles leave the prologue's chain exposed
     int ln_fused = 1;
     int rvq_form = 0;  // RVQ level-kernel form (mimi_set_option "rvq_form"; RvqArgs::form)
+    int rvq_chain = 0;  // small grids: the persistent all-levels RVQ (mimi_set_option "rvq_chain"; RvqArgs::chain)
     // transformer GEMMs with sc1 output stores (gemm_planes.h FL_SC1OUT; mimi_set_option "sc1_out"): bit 0 q/k/v,
     // bit 1 fc1, bit 2 o_proj and fc2 (large batches; the same bits either way)
-    int sc1_out = 0;
+    int sc1_out = 2;  // (A/B, round 4: fc1 0.594 -> 0.576 ms per B = 32 step; q/k/v, o_proj and fc2 slower with it)
     struct Tap {
         float* d = nullptr;
         size_t cap = 0;
@@ -1215,6 +1216,7 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     r.codes_ref = e->capturing ? reinterpret_cast<int32_t* const*>(e->io_dev + 1) : nullptr;
     r.frames_per_item = frames_per_item;
     r.form = e->rvq_form;
+    r.chain = e->rvq_chain;
     const char* kname = "?";
     LAUNCH_TRY(launch_rvq(r, s, &kname), "rvq");
     rec.mark("rvq", 2.0 * frames * valid_share * r.D * r.ncodes * K,
@@ -2297,13 +2299,23 @@ extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {
         return MIMI_OK;
     }
     if (!strcmp(key, "rvq_form")) {
-        if (value < 0 || value > 3) return set_err(MIMI_ERR_INVALID_ARGUMENT, "rvq_form %lld (0..3)", (long long)value);
+        if (value < 0 || value > 6) return set_err(MIMI_ERR_INVALID_ARGUMENT, "rvq_form %lld (0..6)", (long long)value);
         HIP_TRY(hipSetDevice(e->device));
         if (e->rvq_form != (int)value) {
             drop_graphs(e);
             e->graph_seen.clear();
         }
         e->rvq_form = (int)value;
+        return MIMI_OK;
+    }
+    if (!strcmp(key, "rvq_chain")) {
+        if (value < 0 || value > 1) return set_err(MIMI_ERR_INVALID_ARGUMENT, "rvq_chain %lld (0 or 1)", (long long)value);
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->rvq_chain != (int)value) {
+            drop_graphs(e);
+            e->graph_seen.clear();
+        }
+        e->rvq_chain = (int)value;
         return MIMI_OK;
     }
     if (!strcmp(key, "sc1_out")) {

@@ -377,8 +377,10 @@ struct RvqArgs {
     int sem_split;          // (set by launch_rvq) semantic + first acoustic level in one launch
     const int* flen;        // ragged batches: item b's valid frames (frame f of item f / frames_per_item); the
                             // others read a zero projection and their codes are unspecified.  null: all valid
-    int form;               // level-kernel form (engine option rvq_form; same codes): 0 default, 1 three-product
-                            // approximation (round 3), 2 one-product, 3 one-product with 64-frame tiles
+    int form;               // level-kernel form (engine option rvq_form; same codes): 0 default (2), 1 three-product
+                            // approximation (round 3), 2..6 one-product variants (launch_rvq)
+    int chain;              // small grids: all levels in one persistent launch (rvq_chain_h16_kernel; engine option
+                            // rvq_chain; same codes)
 };
 size_t rvq_work_bytes(long long frames);
 hipError_t launch_rvq(const RvqArgs& a, hipStream_t s, const char** kname = nullptr);  // kname: the level kernel's symbol

@@ -1735,6 +1735,295 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
     }
 }
 
+// ---- Persistent all-levels RVQ for small grids (round 4: the per-utterance callers at K = 32) ----
+// rvq_level_h16_kernel runs one launch per level; at batch 1 a level is a chain of dependent memory round trips (merge
+// of the slices' minima, residual and code-row gathers, the codebook stream, the exact re-score) plus a launch: 17 us
+// per level, 0.53 of a 1.51 ms K = 32 encode.  Here one launch runs every level.  Grid (frame tiles, 8 slices, chains):
+// chain 0 the acoustic levels [nsem, K), chain 1 the semantic levels [0, nsem).  A workgroup keeps its 32 frames'
+// residual in LDS across levels (as -2 r, the image the exact chain reads: r = -0.5 img and -2 (r - e) are exact) and
+// per level scores its 256-code slice with rvq_level_h16_kernel<..., P1>'s arithmetic (same approximate window, same
+// exact chain and (distance, code) minimum), publishes its 32 minima as tagged 8-byte granules (the data is the flag:
+// MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16 R2, tag = level + 1, two parity slots zeroed before the
+// launch), sweeps the granules of the frame tile's other 7 slices, merges the 8 slices in slice order with
+// rvq_merge's rule, stores the codes (slice 0) and subtracts the winning code rows.  The next level's codebook
+// fragments are loaded before the sweep, so they fly under it.  Same codes as the per-level launches.
+// Every workgroup of a launch must be resident at once: the host keeps the grid at <= 128 workgroups (2 fit a CU), and
+// every spin is bounded -- a sweep that times out (only possible if other persistent kernels hold the CUs) stores
+// code -1 for its frames, an impossible code.
+constexpr int RVQC_MAX_WG = 128;
+constexpr int RVQC_SPIN = 1 << 20;
+
+__device__ __forceinline__ unsigned long long rvqc_granule(unsigned epoch, unsigned long long best) {
+    // best = (distance bits << 32) | code (code 0xffffffff: none): tag 16 bits | code 16 bits | distance 32 bits
+    return ((unsigned long long)epoch << 48) | ((best & 0xffffull) << 32) | (best >> 32);
+}
+
+#if RVQC_STAMP  // tuning: per-phase cycle sums of wave 0 of workgroup (0, 0, 0), printed at its end
+#define RVQC_T0() unsigned long long st_last = __builtin_readcyclecounter(), st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define RVQC_T(i)                                                     \
+    do {                                                              \
+        const unsigned long long now_ = __builtin_readcyclecounter(); \
+        st_acc[i] += now_ - st_last;                                  \
+        st_last = now_;                                               \
+    } while (0)
+#define RVQC_TPRINT()                                                                                              \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid == 0)                                       \
+    printf("rvqc levels %d: r2 %llu planes %llu mfma %llu cand %llu exact %llu sweep %llu merge %llu resid %llu\n", \
+           Le - Lb, st_acc[0], st_acc[1], st_acc[2], st_acc[3], st_acc[4], st_acc[5], st_acc[6], st_acc[7])
+#else
+#define RVQC_T0()
+#define RVQC_T(i)
+#define RVQC_TPRINT()
+#endif
+template <int D, int EX>
+__global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsigned long long* __restrict__ gran) {
+    constexpr int NWV = 8, NT = 512, FT = 32, CW = 32, SLC = NWV * CW, NSL = 2048 / SLC;
+    constexpr int LDH = D / 2 + 4, RLD = D + 8, KS = D / 16;
+    static_assert(NSL == 8, "8 slices of 256 codes");
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    typedef __attribute__((address_space(1))) unsigned long long gu64;
+    __shared__ __attribute__((aligned(16))) float img[2][FT][LDH];  // -2 r (the residual, kept across levels)
+    __shared__ __attribute__((aligned(16))) _Float16 rpl[FT][RLD];  // hi fp16 plane of r * rs
+    __shared__ float xn[FT], rus[FT], win[FT], smin[FT];
+    __shared__ float redd[NWV][FT];
+    __shared__ unsigned cand[RVQ_CAND];
+    __shared__ unsigned ncand;
+    __shared__ unsigned long long best[FT];
+    __shared__ int prev[FT];
+    __shared__ float gd[NSL][FT];
+    __shared__ int gi[NSL][FT];
+    __shared__ int tmo;
+    const int chain = blockIdx.z;
+    const int Lb = chain ? 0 : p.nsem, Le = chain ? min(p.nsem, p.levels) : p.levels;
+    if (Lb >= Le) return;  // (workgroup-uniform)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+    const long long f0 = (long long)blockIdx.x * FT;
+    const int slice = blockIdx.y;
+    const int code0 = slice * SLC + wave * CW;
+    const unsigned ftiles = gridDim.x;
+    // granules [parity 2][chain 2][frame tile][slice 8][32 frames]
+    auto gslot = [&](int par, int sl) {
+        return gran + ((((long long)par * 2 + chain) * ftiles + blockIdx.x) * NSL + sl) * FT;
+    };
+    // the chain's first residual: the projection (as rvq_level_h16_kernel's fresh levels), zero for invalid frames
+    const int coff = chain ? 0 : D;
+#pragma unroll 4
+    for (int idx = tid; idx < FT * D / 4; idx += NT) {
+        const int i = idx / (D / 4), k = (idx % (D / 4)) * 4;
+        const long long f = f0 + i;
+        f32x4 r = {0.f, 0.f, 0.f, 0.f};
+        if (rvq_valid(p, f)) r = *reinterpret_cast<const f32x4*>(p.proj + f * (2 * D) + coff + k);
+        img[0][i][k >> 1] = -2.0f * r.x;
+        img[1][i][k >> 1] = -2.0f * r.y;
+        img[0][i][(k >> 1) + 1] = -2.0f * r.z;
+        img[1][i][(k >> 1) + 1] = -2.0f * r.w;
+    }
+    h8 bq[KS];  // this wave's 32 codes' hi-plane fragments of the level's codebook, every k-step
+    auto load_cb = [&](int L) {
+        const h8* bp = reinterpret_cast<const h8*>(p.cb_h16) +
+                       ((long long)L * (p.ncodes / 32) + code0 / 32) * KS * 2 * 64 + lane;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) bq[ks] = bp[ks * 128];
+    };
+    load_cb(Lb);
+    if (tid == 0) tmo = 0;
+    RVQC_T0();
+    for (int L = Lb; L < Le; ++L) {
+        if (tid < FT) best[tid] = ~0ull;
+        if (tid == 0) ncand = 0;
+        __syncthreads();  // the residual image is complete
+        RVQC_T(7);
+        // |r|^2 in torch's order and max|r| per frame (rvq_level_h16_kernel)
+        for (int fi = tid >> 4; fi < FT; fi += NT / 16) {
+            const int l = tid & 15;
+            if (l < 8) {
+                float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+                for (int blk = 0; blk < D / 8; ++blk) {
+                    const int k = blk * 8 + l;
+                    const float v = img[k & 1][fi][k >> 1];
+                    a[blk & 3] = a[blk & 3] + v * v;
+                }
+                const float part = ((a[0] + a[1]) + a[2]) + a[3];
+                float tot = __shfl(part, (lane & ~15));
+#pragma unroll
+                for (int q = 1; q < 8; ++q) tot = tot + __shfl(part, (lane & ~15) + q);
+                if (l == 0) xn[fi] = tot * 0.25f;
+            }
+            float mx = 0.0f;
+            for (int k = l; k < D; k += 16) mx = fmaxf(mx, fabsf(img[k & 1][fi][k >> 1]));
+#pragma unroll
+            for (int o = 8; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            if (l == 0) {
+                mx *= 0.5f;
+                const float rs = mx > 0.0f && mx < INFINITY ? ldexpf(1.0f, 13 - ilogbf(mx)) : 1.0f;
+                rus[fi] = 1.0f / rs;
+                win[fi] = rs;
+            }
+        }
+        __syncthreads();
+        RVQC_T(0);
+        for (int idx = tid; idx < FT * D / 2; idx += NT) {
+            const int i = idx / (D / 2), k = (idx % (D / 2)) * 2;
+            const float rs = -0.5f * win[i];
+            rpl[i][k] = (_Float16)(img[0][i][k >> 1] * rs);
+            rpl[i][k + 1] = (_Float16)(img[1][i][k >> 1] * rs);
+        }
+        __syncthreads();
+        RVQC_T(1);
+        // approximate r.e: one fp16 product per k-step (P1)
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const h8 a0 = *reinterpret_cast<const h8*>(&rpl[lane & 31][ks * 16 + 8 * h]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq[ks], acc, 0, 0, 0);
+        }
+        const float cus = p.cb_unscale[L];
+        {
+            const int code = code0 + (lane & 31);
+            const float yn = p.cb_norm[(long long)L * p.ncodes + code];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                acc[r] = (-2.0f * (acc[r] * (rus[row] * cus)) + xn[row]) + yn;
+                float m = acc[r];
+#pragma unroll
+                for (int o = 16; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o));
+                if ((lane & 31) == 0) redd[wave][row] = m;
+            }
+        }
+        __syncthreads();
+        RVQC_T(2);
+        if (tid < FT) {
+            float m = redd[0][tid];
+#pragma unroll
+            for (int q = 1; q < NWV; ++q) m = fminf(m, redd[q][tid]);
+            smin[tid] = m;
+            const float emax = p.cb_emax[L];
+            const float rnorm = __builtin_sqrtf(fmaxf(xn[tid], 0.0f));
+            const float rn = rnorm + emax;
+            // rvq_level_h16_kernel's P1 window (its derivation is there)
+            win[tid] = ldexpf(1.06f * rnorm * emax, -8) + ldexpf(rn * rn, -18) + ldexpf(fabsf(m), -20) + 1e-30f;
+        }
+        __syncthreads();
+        {
+            const int code = code0 + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (!(acc[r] > smin[row] + win[row]) && f0 + row < p.frames) {
+                    const unsigned sl = atomicAdd(&ncand, 1u);
+                    if (sl < RVQ_CAND) cand[sl] = ((unsigned)row << 16) | (unsigned)(code - slice * SLC);
+                }
+            }
+        }
+        __syncthreads();
+        RVQC_T(3);
+        // exact re-score (the reference's fp32 chain), as rvq_level_h16_kernel
+        {
+            const float* cbr = p.cb_rows + (long long)L * p.ncodes * D;
+            const unsigned nc = ncand;
+            const bool all = nc > RVQ_CAND;
+            const unsigned total = all ? FT * SLC : nc;
+            for (unsigned i = tid; i < total; i += NT) {
+                const int row = all ? (int)(i % FT) : (int)(cand[i] >> 16);
+                const int c = slice * SLC + (all ? (int)(i / FT) : (int)(cand[i] & 0xffff));
+                if (f0 + row >= p.frames) continue;
+                const f32x4* e = reinterpret_cast<const f32x4*>(cbr + (long long)c * D);
+                float a = 0.0f;
+#pragma unroll 1
+                for (int k0 = 0; k0 < D / 4; k0 += EX) {
+                    f32x4 ev[EX];
+#pragma unroll
+                    for (int j = 0; j < EX; ++j) ev[j] = e[k0 + j];
+#pragma unroll
+                    for (int j = 0; j < EX; ++j) {
+                        const int k4 = k0 + j;
+                        a = __builtin_fmaf(img[0][row][2 * k4], ev[j].x, a);
+                        a = __builtin_fmaf(img[1][row][2 * k4], ev[j].y, a);
+                        a = __builtin_fmaf(img[0][row][2 * k4 + 1], ev[j].z, a);
+                        a = __builtin_fmaf(img[1][row][2 * k4 + 1], ev[j].w, a);
+                    }
+                }
+                float d2 = a + xn[row];
+                d2 = d2 + p.cb_norm[(long long)L * p.ncodes + c];
+                const float d = __builtin_sqrtf(fmaxf(d2, 0.0f));
+                atomicMin(&best[row], ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)c);
+            }
+        }
+        __syncthreads();
+        RVQC_T(4);
+        // publish this slice's 32 minima (one 8-byte agent-scope store each: the granule is its own flag)
+        const unsigned epoch = (unsigned)L + 1;
+        if (tid < FT)
+            __hip_atomic_store((gu64*)(gslot(L & 1, slice) + tid), rvqc_granule(epoch, best[tid]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (L + 1 < Le) load_cb(L + 1);  // the next level's codebook: in flight under the sweep
+        // sweep the frame tile's 8 slices (wave 0, 4 granules per lane) until every tag is this level's
+        if (wave == 0) {
+            unsigned long long v[4];
+            for (unsigned spins = 0;; ++spins) {
+                bool ok = true;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int j = lane + 64 * q;
+                    v[q] = __hip_atomic_load((gu64*)(gslot(L & 1, j >> 5) + (j & 31)), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                    ok = ok && (unsigned)(v[q] >> 48) == epoch;
+                }
+                if (__all(ok)) break;
+                if (spins >= RVQC_SPIN) {
+                    if (lane == 0) tmo = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = lane + 64 * q;
+                gd[j >> 5][j & 31] = __uint_as_float((unsigned)(v[q] & 0xffffffffu));
+                gi[j >> 5][j & 31] = (int)(short)(unsigned short)((v[q] >> 32) & 0xffffu);
+            }
+        }
+        __syncthreads();
+        RVQC_T(5);
+        if (tid < FT) {  // rvq_merge's rule over the slices in order
+            float d = gd[0][tid];
+            int ix = gi[0][tid];
+#pragma unroll
+            for (int q = 1; q < NSL; ++q)
+                if (gd[q][tid] < d || (gd[q][tid] == d && gi[q][tid] < ix)) {
+                    d = gd[q][tid];
+                    ix = gi[q][tid];
+                }
+            ix = (ix < 0 || ix >= p.ncodes) ? 0 : ix;
+            const long long f = f0 + tid;
+            if (slice == 0 && f < p.frames) rvq_store_code(p, L, f, tmo ? -1 : ix);
+            prev[tid] = ix;
+        }
+        __syncthreads();
+        RVQC_T(6);
+        if (L + 1 < Le) {  // r_{L+1} = r_L - embed_L[idx] (fp32), kept as -2 r; invalid frames stay 0
+            const float* rows = p.cb_rows + (long long)L * p.ncodes * D;
+#pragma unroll 4
+            for (int idx = tid; idx < FT * D / 4; idx += NT) {
+                const int i = idx / (D / 4), k = (idx % (D / 4)) * 4;
+                if (!rvq_valid(p, f0 + i)) continue;
+                const f32x4 e = *reinterpret_cast<const f32x4*>(rows + (long long)prev[i] * D + k);
+                const float r0 = -0.5f * img[0][i][k >> 1], r1 = -0.5f * img[1][i][k >> 1];
+                const float r2 = -0.5f * img[0][i][(k >> 1) + 1], r3 = -0.5f * img[1][i][(k >> 1) + 1];
+                img[0][i][k >> 1] = -2.0f * (r0 - e.x);
+                img[1][i][k >> 1] = -2.0f * (r1 - e.y);
+                img[0][i][(k >> 1) + 1] = -2.0f * (r2 - e.z);
+                img[1][i][(k >> 1) + 1] = -2.0f * (r3 - e.w);
+            }
+        }
+    }
+    RVQC_TPRINT();
+}
+
 hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
     const char* kn_dummy = nullptr;
     if (!kname) kname = &kn_dummy;
@@ -1754,17 +2043,36 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
         // (2- and 4-wave workgroups on small grids -- 32 / 16 slices, 4x / 2x the workgroups, each streaming a quarter /
         // half of the codebook bytes -- were slower at batch 1 and 4: rvq 0.14 -> 0.21 / 0.16 ms per batch-1 encode,
         // the per-workgroup prologue chain on fewer threads outweighs the shorter stream; profiles/r3j_ab_*)
-        // form: 1 = three fp16 products (round 3), 2 = one product (P1), 3 = one product, 64-frame tiles (large
-        // batches only); 0 = the default
-        const int form = a.form == 0 ? 1 : a.form;
+        // form: 1 = three fp16 products (round 3); one product (P1): 2 = 2 k-steps in flight per 32-code tile, 3 = the
+        // same on 64-frame tiles, 4 / 5 = 4 / 8 k-steps in flight, 6 = the small-batch form (8 slices of 256 codes,
+        // every k-step in flight) at every batch size; 0 = the default.  Small batches: the small-batch form, P1 from 2 on
+        const int form = a.form == 0 ? 5 : a.form;
+        // small grids: every level in one persistent launch (rvq_chain_h16_kernel), unless the form asks otherwise
+        const int nchain = (a.levels > a.nsem ? 1 : 0) + (a.nsem > 0 ? 1 : 0);
+        if (small && a.chain && form != 1 && ftiles32 * 8 * 2 <= (unsigned)RVQC_MAX_WG && a.nsem <= 1) {
+            const size_t gbytes = (size_t)2 * 2 * ftiles32 * 8 * 32 * 8;
+            const size_t pd_off = (size_t)2 * ((a.frames + RVQ_FT - 1) / RVQ_FT * RVQ_FT) * a.D * 4;
+            if (gbytes > rvq_work_bytes(a.frames) - pd_off) return hipErrorInvalidValue;
+            unsigned long long* gran = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.work) + pd_off);
+            const hipError_t me = hipMemsetAsync(gran, 0, gbytes, s);
+            if (me != hipSuccess) return me;
+            static char knc[96];
+            snprintf(knc, sizeof knc, "mimi::rvq_chain_h16_kernel<256, 16>");
+            *kname = knc;
+            (void)nchain;
+            hipLaunchKernelGGL((rvq_chain_h16_kernel<256, 16>), dim3(ftiles32, 8, 2), dim3(512), 0, s, a, gran);
+            return hipGetLastError();
+        }
         const bool p1 = form >= 2;
-        const int ft = (!small && form == 3) ? 64 : 32;
+        const bool scfg = small || form == 6;
+        const int ft = (!scfg && form == 3) ? 64 : 32;
+        const int pf = scfg ? 16 : form == 4 ? 4 : form == 5 ? 8 : 2;
         const unsigned ftiles = (unsigned)((a.frames + ft - 1) / ft);
         constexpr int nwv = 8;
-        const unsigned nsl = 2048 / (small ? nwv * 32 : 8 * 64);
+        const unsigned nsl = 2048 / (scfg ? nwv * 32 : 8 * 64);
         static char kn[112];
-        snprintf(kn, sizeof kn, "mimi::rvq_level_h16_kernel<256, %d, %d, %s, %d, %d, %d, %s>", small ? 16 : 2,
-                 small ? 32 : 16, a.flen ? "true" : "false", small ? 32 : 64, nwv, ft, p1 ? "true" : "false");
+        snprintf(kn, sizeof kn, "mimi::rvq_level_h16_kernel<256, %d, %d, %s, %d, %d, %d, %s>", pf, scfg ? 32 : 16,
+                 a.flen ? "true" : "false", scfg ? 32 : 64, nwv, ft, p1 ? "true" : "false");
         *kname = kn;
         for (int L = 0; L < a.levels; L += (split && L == 0) ? 2 : 1) {
             const dim3 g(ftiles, nsl, (split && L == 0) ? 2 : 1);
@@ -1777,7 +2085,7 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
         else                                                                                                        \
             hipLaunchKernelGGL((rvq_level_h16_kernel<256, PF_, EX_, false, CW_, NWV_, FT_, P1_>), g, blk, 0, s, a, L); \
     } while (0)
-            if (small) {
+            if (scfg) {
                 if (p1)
                     RVQ_LAUNCH(16, 32, 32, 8, 32, true);
                 else
@@ -1786,6 +2094,10 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
                 RVQ_LAUNCH(2, 16, 64, 8, 32, false);
             } else if (ft == 64) {
                 RVQ_LAUNCH(2, 16, 64, 8, 64, true);
+            } else if (pf == 4) {
+                RVQ_LAUNCH(4, 16, 64, 8, 32, true);
+            } else if (pf == 8) {
+                RVQ_LAUNCH(8, 16, 64, 8, 32, true);
             } else {
                 RVQ_LAUNCH(2, 16, 64, 8, 32, true);
             }
