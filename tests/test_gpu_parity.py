@@ -98,8 +98,8 @@ def test_kernel_options_identical_codes(engine):
     and every RVQ form, on a B = 16 x 10 s batch at K = 32."""
     x = torch.from_numpy(synthetic.clip_batch(16, 240000, seed=88))[:, None].cuda()
     base = engine.encode(x, num_quantizers=32).audio_codes.cpu()
-    defaults = {"sc1_out": 2, "rvq_form": 0, "rvq_chain": 0}
-    cases = [("sc1_out", 0), ("sc1_out", 7), ("rvq_chain", 1)] + [("rvq_form", f) for f in range(1, 7)]
+    defaults = {"sc1_out": 2, "rvq_form": 0, "rvq_chain": 1}
+    cases = [("sc1_out", 0), ("sc1_out", 7), ("rvq_chain", 0)] + [("rvq_form", f) for f in range(1, 7)]
     for key, val in cases:
         engine.set_option(key, val)
         try:
@@ -127,10 +127,11 @@ def test_quantizer_chain_small_grids(engine, golden, chain):
         assert np.array_equal(engine.quantize(emb, 32)[0].cpu().numpy(), arrays["embcodes_speech10s"][:, :3])
         x = torch.from_numpy(synthetic.speech_like(200000, 91, 0))[None, None].cuda()
         got = engine.encode(x, num_quantizers=32).audio_codes.cpu()
+        engine.set_option("rvq_chain", 1 - chain)
+        other = engine.encode(x, num_quantizers=32).audio_codes.cpu()
     finally:
-        engine.set_option("rvq_chain", 0)
-    base = engine.encode(x, num_quantizers=32).audio_codes.cpu()
-    assert torch.equal(got, base)
+        engine.set_option("rvq_chain", 1)  # (the default)
+    assert torch.equal(got, other)
 
 
 def test_stage_tensors_within_tolerance(engine, golden):

@@ -330,7 +330,7 @@ struct mimi_engine {
     // 20.8 vs 10.4 + 5.2 us -- its one compute wave and 16-row tiles leave the prologue's chain exposed
     int ln_fused = 1;
     int rvq_form = 0;  // RVQ level-kernel form (mimi_set_option "rvq_form"; RvqArgs::form)
-    int rvq_chain = 0;  // small grids: the persistent all-levels RVQ (mimi_set_option "rvq_chain"; RvqArgs::chain)
+    int rvq_chain = 1;  // small grids: the persistent all-levels RVQ (mimi_set_option "rvq_chain"; RvqArgs::chain)
     // transformer GEMMs with sc1 output stores (gemm_planes.h FL_SC1OUT; mimi_set_option "sc1_out"): bit 0 q/k/v,
     // bit 1 fc1, bit 2 o_proj and fc2 (large batches; the same bits either way)
     int sc1_out = 2;  // (A/B, round 4: fc1 0.594 -> 0.576 ms per B = 32 step; q/k/v, o_proj and fc2 slower with it)

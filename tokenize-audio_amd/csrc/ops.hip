@@ -1447,6 +1447,78 @@ constexpr int RVQ_CAND = 2048;
 // of the codebook, v_mfma_f32_32x32x16_f16) instead of three, with the window widened to that product's rigorous
 // error bound (below): a third of the MFMAs and half the codebook bytes; the exact re-score decides, so the codes are
 // the same bits.
+// |r|^2 in torch's order (x.pow(2).sum(-1): 8 lanes x 4 accumulators, each accumulator over blocks blk = j, j + 4, ..,
+// the 4 combined as ((a0 + a1) + a2) + a3, the 8 lanes summed in order) and the fp16 scale of max |r|, from the -2 r
+// image (4 r^2 summed, then * 0.25: power-of-two scalings, exact).  32 threads per frame, one accumulator chain of 8
+// each (round 4; 16 threads per frame with chains of 32 before: the same sums in the same order).  NT >= 32 threads.
+template <int FT, int D, int LDH, int NT>
+__device__ __forceinline__ void rvq_norms(const float (*img)[FT][LDH], float* xn, float* rus, float* win, int tid) {
+    static_assert(D == 256, "8 lanes x 4 accumulators x 8 blocks");
+    const int lane = tid & 63, sub = tid & 31, l = sub & 7, j = sub >> 3, gb = lane & 32;
+    for (int fi = tid >> 5; fi < FT; fi += NT / 32) {
+        float a = 0.0f, mx = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int k = 8 * (j + 4 * t) + l;
+            const float v = img[k & 1][fi][k >> 1];
+            a = a + v * v;
+            mx = fmaxf(mx, fabsf(v));
+        }
+        const float part = ((__shfl(a, gb + l) + __shfl(a, gb + l + 8)) + __shfl(a, gb + l + 16)) + __shfl(a, gb + l + 24);
+        float tot = __shfl(part, gb);
+#pragma unroll
+        for (int q = 1; q < 8; ++q) tot = tot + __shfl(part, gb + q);
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        if (sub == 0) {
+            xn[fi] = tot * 0.25f;
+            mx *= 0.5f;  // max |r|
+            const float rs = mx > 0.0f && mx < INFINITY ? ldexpf(1.0f, 13 - ilogbf(mx)) : 1.0f;
+            rus[fi] = 1.0f / rs;
+            win[fi] = rs;  // (the scale, until the window replaces it)
+        }
+    }
+}
+
+// Exact re-score of the candidates (the reference's fp32 chain: fmaf over k = 0..255 in order of -2 r_k e_k, + |r|^2,
+// + |e|^2, clamp, sqrt; (distance, code) minimum per frame by a 64-bit LDS atomicMin), one thread per candidate with EX
+// float4 of its code row in flight, or every code of the slice when the list overflowed (degenerate codebooks).  (Staging
+// the rows in LDS 32 at a time -- one memory round trip per 32 candidates -- was slower: the chains then wait on an LDS
+// read per 4 FMAs, rvq 0.21 -> 0.36 ms per B = 32 step, 0.50 -> 0.58 ms at batch 1 K = 32.)
+template <int FT, int D, int LDH, int NT, int SLC, int EX>
+__device__ __forceinline__ void rvq_exact(const float (*img)[FT][LDH], const float* xn, const unsigned* cand,
+                                          unsigned nc, unsigned long long* best, const float* cbr, const float* cnorm,
+                                          int cbase, long long f0, long long frames, int tid) {
+    const bool all = nc > RVQ_CAND;
+    const unsigned total = all ? FT * SLC : nc;
+    for (unsigned i = tid; i < total; i += NT) {
+        const int row = all ? (int)(i % FT) : (int)(cand[i] >> 16);
+        const int c = cbase + (all ? (int)(i / FT) : (int)(cand[i] & 0xffff));
+        if (f0 + row >= frames) continue;
+        const f32x4* e = reinterpret_cast<const f32x4*>(cbr + (long long)c * D);
+        float a = 0.0f;
+        // (not unrolled: unrolled, hipcc hoisted every round's loads -- the whole 1-KB row in 256 VGPRs -- and spilled)
+#pragma unroll 1
+        for (int k0 = 0; k0 < D / 4; k0 += EX) {  // EX float4 of the code row in flight, then the in-order chain
+            f32x4 ev[EX];
+#pragma unroll
+            for (int j = 0; j < EX; ++j) ev[j] = e[k0 + j];
+#pragma unroll
+            for (int j = 0; j < EX; ++j) {
+                const int k4 = k0 + j;
+                a = __builtin_fmaf(img[0][row][2 * k4], ev[j].x, a);
+                a = __builtin_fmaf(img[1][row][2 * k4], ev[j].y, a);
+                a = __builtin_fmaf(img[0][row][2 * k4 + 1], ev[j].z, a);
+                a = __builtin_fmaf(img[1][row][2 * k4 + 1], ev[j].w, a);
+            }
+        }
+        float d2 = a + xn[row];
+        d2 = d2 + cnorm[c];
+        const float d = __builtin_sqrtf(fmaxf(d2, 0.0f));
+        atomicMin(&best[row], ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)c);
+    }
+}
+
 template <int D, int PF = 4, int EX = 16, bool RG = false, int CW = 32, int NWV = 8, int FT = 32, bool P1 = false>
 // (HIP's second launch bound is waves per SIMD: 4 = two 8-wave workgroups per CU, i.e. <= 128 VGPRs)
 __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_level_h16_kernel(RvqArgs p, int L0) {
@@ -1475,10 +1547,16 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
     __shared__ unsigned cand[RVQ_CAND];
     __shared__ unsigned ncand;
     __shared__ unsigned long long best[FT];
+    __shared__ float ynl[SLC];  // |e|^2 of the slice's codes
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
     const long long f0 = (long long)blockIdx.x * FT;
     const int slice = blockIdx.y;
     const RvqWork w = rvq_work(p, NSL);
+    // the level's scalars and this lane's code norms, loaded here so the barriers below wait for them (used after the
+    // MFMA loop, where a load is a whole exposed memory round trip)
+    const int code0 = slice * SLC + wave * CW;
+    const float cus = p.cb_unscale[L], emax_l = p.cb_emax[L];
+    for (int c = tid; c < SLC; c += NT) ynl[c] = p.cb_norm[(long long)L * p.ncodes + slice * SLC + c];
 
     // ---- prologue (as rvq_level_kernel): finish level L-1, form r_L
     // (the first acoustic level of a combined launch, blockIdx.z = 1, does not merge the semantic level running beside
@@ -1521,34 +1599,7 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
         img[1][i][(k >> 1) + 1] = -2.0f * r.w;
     }
     __syncthreads();
-    // |r|^2 in torch's order (rvq_level_kernel) and max|r| per frame (16 threads per frame)
-    for (int fi = tid >> 4; fi < FT; fi += NT / 16) {
-        const int l = tid & 15;
-        if (l < 8) {
-            float a[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-            for (int blk = 0; blk < D / 8; ++blk) {
-                const int k = blk * 8 + l;
-                const float v = img[k & 1][fi][k >> 1];
-                a[blk & 3] = a[blk & 3] + v * v;
-            }
-            const float part = ((a[0] + a[1]) + a[2]) + a[3];
-            float tot = __shfl(part, (lane & ~15));
-#pragma unroll
-            for (int q = 1; q < 8; ++q) tot = tot + __shfl(part, (lane & ~15) + q);
-            if (l == 0) xn[fi] = tot * 0.25f;
-        }
-        float mx = 0.0f;
-        for (int k = l; k < D; k += 16) mx = fmaxf(mx, fabsf(img[k & 1][fi][k >> 1]));
-#pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-        if (l == 0) {
-            mx *= 0.5f;  // max |r|
-            const float rs = mx > 0.0f && mx < INFINITY ? ldexpf(1.0f, 13 - ilogbf(mx)) : 1.0f;
-            rus[fi] = 1.0f / rs;
-            win[fi] = rs;  // (the scale, until the window replaces it below)
-        }
-    }
+    rvq_norms<FT, D, LDH, NT>(img, xn, rus, win, tid);
     __syncthreads();
     // fp16 planes of r * rs (P1: the hi plane only)
     for (int idx = tid; idx < FT * D / 2; idx += NT) {
@@ -1567,7 +1618,6 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
 
     // ---- approximate r.e for FT frames x this wave's CW codes; the wave's codebook planes stream from L2 with PF
     // k-steps in flight
-    const int code0 = slice * SLC + wave * CW;
     const h8* bp = reinterpret_cast<const h8*>(p.cb_h16) +
                    ((long long)L * (p.ncodes / 32) + code0 / 32) * (D / 16) * 2 * 64 + lane;
     constexpr int TST = (D / 16) * 2 * 64;  // h8 per 32-code block of the fragment image
@@ -1601,17 +1651,20 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
             const h8 a0 = *reinterpret_cast<const h8*>(&rpl[0][i * 32 + (lane & 31)][ks * 16 + 8 * h]);
+            // transposed: the codebook fragment is the A operand (rows = codes), r the B operand (columns = frames), so
+            // a lane holds ONE frame and 16 codes per tile -- the minimum over codes is in-register, not 5 shuffles per
+            // frame row (a fragment serves as either operand: lane (j, h) holds row / column j, k = 8 h .. 8 h + 7)
             if constexpr (P1) {
 #pragma unroll
                 for (int t = 0; t < TNC; ++t)
-                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[t][0], acc[i][t], 0, 0, 0);
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bb[t][0], a0, acc[i][t], 0, 0, 0);
             } else {
                 const h8 a1 = *reinterpret_cast<const h8*>(&rpl[NPL - 1][i * 32 + (lane & 31)][ks * 16 + 8 * h]);
 #pragma unroll
                 for (int t = 0; t < TNC; ++t) {
-                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bb[t][0], acc[i][t], 0, 0, 0);
-                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[t][NPL - 1], acc[i][t], 0, 0, 0);
-                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[t][0], acc[i][t], 0, 0, 0);
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bb[t][0], a1, acc[i][t], 0, 0, 0);
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bb[t][NPL - 1], a0, acc[i][t], 0, 0, 0);
+                    acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bb[t][0], a0, acc[i][t], 0, 0, 0);
                 }
             }
         }
@@ -1632,29 +1685,23 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) kstep(ks);
     }
-    const float cus = p.cb_unscale[L];
+    // approximate d^2 (transposed layout: frame i * 32 + (lane & 31), code 32 t + (r & 3) + 8 (r >> 2) + 4 h of the
+    // wave's CW) and each frame's minimum over the wave's codes
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
-        float mrow[16];
+        const int fr = i * 32 + (lane & 31);
+        const float ur = rus[fr] * cus, xr = xn[fr];
+        float m = INFINITY;
 #pragma unroll
-        for (int t = 0; t < TNC; ++t) {
-            const int code = code0 + 32 * t + (lane & 31);
-            const float yn = p.cb_norm[(long long)L * p.ncodes + code];
+        for (int t = 0; t < TNC; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                acc[i][t][r] = (-2.0f * (acc[i][t][r] * (rus[row] * cus)) + xn[row]) + yn;  // approx d^2
-                mrow[r] = t == 0 ? acc[i][t][r] : fminf(mrow[r], acc[i][t][r]);
+                const float yn = ynl[wave * CW + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h];
+                acc[i][t][r] = (-2.0f * (acc[i][t][r] * ur) + xr) + yn;
+                m = fminf(m, acc[i][t][r]);
             }
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            float m = mrow[r];
-#pragma unroll
-            for (int o = 16; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o));
-            if ((lane & 31) == 0) redd[wave][row] = m;
-        }
+        m = fminf(m, __shfl_xor(m, 32));
+        if (h == 0) redd[wave][fr] = m;
     }
     __syncthreads();
     if (tid < FT) {
@@ -1662,7 +1709,7 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
 #pragma unroll
         for (int q = 1; q < NWV; ++q) m = fminf(m, redd[q][tid]);
         smin[tid] = m;
-        const float emax = p.cb_emax[L];
+        const float emax = emax_l;
         const float rnorm = __builtin_sqrtf(fmaxf(xn[tid], 0.0f));
         const float rn = rnorm + emax;
         if constexpr (P1) {
@@ -1680,52 +1727,26 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < RT; ++i)
+    for (int i = 0; i < RT; ++i) {
+        const int fr = i * 32 + (lane & 31);
+        const float lim = smin[fr] + win[fr];
+        const bool fin = f0 + fr < p.frames;
 #pragma unroll
-        for (int t = 0; t < TNC; ++t) {
-            const int code = code0 + 32 * t + (lane & 31);
+        for (int t = 0; t < TNC; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 // NaN distances (a non-finite residual) are candidates too: the exact path decides
-                if (!(acc[i][t][r] > smin[row] + win[row]) && f0 + row < p.frames) {
+                if (!(acc[i][t][r] > lim) && fin) {
                     const unsigned slot = atomicAdd(&ncand, 1u);
-                    if (slot < RVQ_CAND) cand[slot] = ((unsigned)row << 16) | (unsigned)(code - slice * SLC);
+                    if (slot < RVQ_CAND)
+                        cand[slot] = ((unsigned)fr << 16) | (unsigned)(wave * CW + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h);
                 }
             }
-        }
-    __syncthreads();
-    // ---- exact re-scoring: the candidates, or (degenerate: the list overflowed) every code of the slice
-    const float* cbr = p.cb_rows + (long long)L * p.ncodes * D;
-    const unsigned nc = ncand;
-    const bool all = nc > RVQ_CAND;
-    const unsigned total = all ? FT * SLC : nc;
-    for (unsigned i = tid; i < total; i += NT) {
-        const int row = all ? (int)(i % FT) : (int)(cand[i] >> 16);
-        const int c = slice * SLC + (all ? (int)(i / FT) : (int)(cand[i] & 0xffff));
-        if (f0 + row >= p.frames) continue;
-        const f32x4* e = reinterpret_cast<const f32x4*>(cbr + (long long)c * D);
-        float a = 0.0f;
-        // (not unrolled: unrolled, hipcc hoisted every round's loads -- the whole 1-KB row in 256 VGPRs -- and spilled)
-#pragma unroll 1
-        for (int k0 = 0; k0 < D / 4; k0 += EX) {  // EX float4 of the code row in flight, then the in-order chain
-            f32x4 ev[EX];
-#pragma unroll
-            for (int j = 0; j < EX; ++j) ev[j] = e[k0 + j];
-#pragma unroll
-            for (int j = 0; j < EX; ++j) {
-                const int k4 = k0 + j;
-                a = __builtin_fmaf(img[0][row][2 * k4], ev[j].x, a);
-                a = __builtin_fmaf(img[1][row][2 * k4], ev[j].y, a);
-                a = __builtin_fmaf(img[0][row][2 * k4 + 1], ev[j].z, a);
-                a = __builtin_fmaf(img[1][row][2 * k4 + 1], ev[j].w, a);
-            }
-        }
-        float d2 = a + xn[row];
-        d2 = d2 + p.cb_norm[(long long)L * p.ncodes + c];
-        const float d = __builtin_sqrtf(fmaxf(d2, 0.0f));
-        atomicMin(&best[row], ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)c);
     }
+    __syncthreads();
+    // ---- exact re-scoring (rvq_exact): the candidates, or every code of the slice when the list overflowed
+    rvq_exact<FT, D, LDH, NT, SLC, EX>(img, xn, cand, ncand, best, p.cb_rows + (long long)L * p.ncodes * D,
+                                       p.cb_norm + (long long)L * p.ncodes, slice * SLC, f0, p.frames, tid);
     __syncthreads();
     if (tid < FT && f0 + tid < p.frames) {
         const unsigned long long b = best[tid];
@@ -1793,6 +1814,8 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
     __shared__ float gd[NSL][FT];
     __shared__ int gi[NSL][FT];
     __shared__ int tmo;
+    __shared__ int codes_l[FT][32];  // this tile's codes per level, stored at the end (slice 0)
+    __shared__ float ynl[SLC];       // |e|^2 of the slice's codes at this level
     const int chain = blockIdx.z;
     const int Lb = chain ? 0 : p.nsem, Le = chain ? min(p.nsem, p.levels) : p.levels;
     if (Lb >= Le) return;  // (workgroup-uniform)
@@ -1819,11 +1842,15 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
         img[1][i][(k >> 1) + 1] = -2.0f * r.w;
     }
     h8 bq[KS];  // this wave's 32 codes' hi-plane fragments of the level's codebook, every k-step
+    float yn = 0.0f, cus = 0.0f, emax = 0.0f;  // ... and the norm of the slice's code tid, the level's scalars
     auto load_cb = [&](int L) {
         const h8* bp = reinterpret_cast<const h8*>(p.cb_h16) +
                        ((long long)L * (p.ncodes / 32) + code0 / 32) * KS * 2 * 64 + lane;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) bq[ks] = bp[ks * 128];
+        if (tid < SLC) yn = p.cb_norm[(long long)L * p.ncodes + slice * SLC + tid];
+        cus = p.cb_unscale[L];
+        emax = p.cb_emax[L];
     };
     load_cb(Lb);
     if (tid == 0) tmo = 0;
@@ -1831,36 +1858,10 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
     for (int L = Lb; L < Le; ++L) {
         if (tid < FT) best[tid] = ~0ull;
         if (tid == 0) ncand = 0;
+        if (tid < SLC) ynl[tid] = yn;
         __syncthreads();  // the residual image is complete
         RVQC_T(7);
-        // |r|^2 in torch's order and max|r| per frame (rvq_level_h16_kernel)
-        for (int fi = tid >> 4; fi < FT; fi += NT / 16) {
-            const int l = tid & 15;
-            if (l < 8) {
-                float a[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-                for (int blk = 0; blk < D / 8; ++blk) {
-                    const int k = blk * 8 + l;
-                    const float v = img[k & 1][fi][k >> 1];
-                    a[blk & 3] = a[blk & 3] + v * v;
-                }
-                const float part = ((a[0] + a[1]) + a[2]) + a[3];
-                float tot = __shfl(part, (lane & ~15));
-#pragma unroll
-                for (int q = 1; q < 8; ++q) tot = tot + __shfl(part, (lane & ~15) + q);
-                if (l == 0) xn[fi] = tot * 0.25f;
-            }
-            float mx = 0.0f;
-            for (int k = l; k < D; k += 16) mx = fmaxf(mx, fabsf(img[k & 1][fi][k >> 1]));
-#pragma unroll
-            for (int o = 8; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-            if (l == 0) {
-                mx *= 0.5f;
-                const float rs = mx > 0.0f && mx < INFINITY ? ldexpf(1.0f, 13 - ilogbf(mx)) : 1.0f;
-                rus[fi] = 1.0f / rs;
-                win[fi] = rs;
-            }
-        }
+        rvq_norms<FT, D, LDH, NT>(img, xn, rus, win, tid);
         __syncthreads();
         RVQC_T(0);
         for (int idx = tid; idx < FT * D / 2; idx += NT) {
@@ -1878,21 +1879,19 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const h8 a0 = *reinterpret_cast<const h8*>(&rpl[lane & 31][ks * 16 + 8 * h]);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq[ks], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq[ks], a0, acc, 0, 0, 0);  // transposed (level kernel)
         }
-        const float cus = p.cb_unscale[L];
-        {
-            const int code = code0 + (lane & 31);
-            const float yn = p.cb_norm[(long long)L * p.ncodes + code];
+        {  // lane: frame lane & 31, codes (r & 3) + 8 (r >> 2) + 4 h of the wave's 32
+            const int fr = lane & 31;
+            const float ur = rus[fr] * cus, xr = xn[fr];
+            float m = INFINITY;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                acc[r] = (-2.0f * (acc[r] * (rus[row] * cus)) + xn[row]) + yn;
-                float m = acc[r];
-#pragma unroll
-                for (int o = 16; o >= 1; o >>= 1) m = fminf(m, __shfl_xor(m, o));
-                if ((lane & 31) == 0) redd[wave][row] = m;
+                acc[r] = (-2.0f * (acc[r] * ur) + xr) + ynl[wave * CW + (r & 3) + 8 * (r >> 2) + 4 * h];
+                m = fminf(m, acc[r]);
             }
+            m = fminf(m, __shfl_xor(m, 32));
+            if (h == 0) redd[wave][fr] = m;
         }
         __syncthreads();
         RVQC_T(2);
@@ -1901,7 +1900,6 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
 #pragma unroll
             for (int q = 1; q < NWV; ++q) m = fminf(m, redd[q][tid]);
             smin[tid] = m;
-            const float emax = p.cb_emax[L];
             const float rnorm = __builtin_sqrtf(fmaxf(xn[tid], 0.0f));
             const float rn = rnorm + emax;
             // rvq_level_h16_kernel's P1 window (its derivation is there)
@@ -1909,50 +1907,21 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
         }
         __syncthreads();
         {
-            const int code = code0 + (lane & 31);
+            const int fr = lane & 31;
+            const float lim = smin[fr] + win[fr];
+            const bool fin = f0 + fr < p.frames;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (!(acc[r] > smin[row] + win[row]) && f0 + row < p.frames) {
+            for (int r = 0; r < 16; ++r)
+                if (!(acc[r] > lim) && fin) {
                     const unsigned sl = atomicAdd(&ncand, 1u);
-                    if (sl < RVQ_CAND) cand[sl] = ((unsigned)row << 16) | (unsigned)(code - slice * SLC);
+                    if (sl < RVQ_CAND) cand[sl] = ((unsigned)fr << 16) | (unsigned)(wave * CW + (r & 3) + 8 * (r >> 2) + 4 * h);
                 }
-            }
         }
         __syncthreads();
         RVQC_T(3);
-        // exact re-score (the reference's fp32 chain), as rvq_level_h16_kernel
-        {
-            const float* cbr = p.cb_rows + (long long)L * p.ncodes * D;
-            const unsigned nc = ncand;
-            const bool all = nc > RVQ_CAND;
-            const unsigned total = all ? FT * SLC : nc;
-            for (unsigned i = tid; i < total; i += NT) {
-                const int row = all ? (int)(i % FT) : (int)(cand[i] >> 16);
-                const int c = slice * SLC + (all ? (int)(i / FT) : (int)(cand[i] & 0xffff));
-                if (f0 + row >= p.frames) continue;
-                const f32x4* e = reinterpret_cast<const f32x4*>(cbr + (long long)c * D);
-                float a = 0.0f;
-#pragma unroll 1
-                for (int k0 = 0; k0 < D / 4; k0 += EX) {
-                    f32x4 ev[EX];
-#pragma unroll
-                    for (int j = 0; j < EX; ++j) ev[j] = e[k0 + j];
-#pragma unroll
-                    for (int j = 0; j < EX; ++j) {
-                        const int k4 = k0 + j;
-                        a = __builtin_fmaf(img[0][row][2 * k4], ev[j].x, a);
-                        a = __builtin_fmaf(img[1][row][2 * k4], ev[j].y, a);
-                        a = __builtin_fmaf(img[0][row][2 * k4 + 1], ev[j].z, a);
-                        a = __builtin_fmaf(img[1][row][2 * k4 + 1], ev[j].w, a);
-                    }
-                }
-                float d2 = a + xn[row];
-                d2 = d2 + p.cb_norm[(long long)L * p.ncodes + c];
-                const float d = __builtin_sqrtf(fmaxf(d2, 0.0f));
-                atomicMin(&best[row], ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)c);
-            }
-        }
+        // exact re-score (the reference's fp32 chain), rvq_exact as in rvq_level_h16_kernel
+        rvq_exact<FT, D, LDH, NT, SLC, EX>(img, xn, cand, ncand, best, p.cb_rows + (long long)L * p.ncodes * D,
+                                           p.cb_norm + (long long)L * p.ncodes, slice * SLC, f0, p.frames, tid);
         __syncthreads();
         RVQC_T(4);
         // publish this slice's 32 minima (one 8-byte agent-scope store each: the granule is its own flag)
@@ -1999,8 +1968,7 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
                     ix = gi[q][tid];
                 }
             ix = (ix < 0 || ix >= p.ncodes) ? 0 : ix;
-            const long long f = f0 + tid;
-            if (slice == 0 && f < p.frames) rvq_store_code(p, L, f, tmo ? -1 : ix);
+            codes_l[tid][L] = tmo ? -1 : ix;
             prev[tid] = ix;
         }
         __syncthreads();
@@ -2022,6 +1990,14 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
         }
     }
     RVQC_TPRINT();
+    if (slice == 0) {  // the tile's codes, every level (stores deferred: a barrier after each would wait for them)
+        __syncthreads();
+        for (int i = tid; i < FT * (Le - Lb); i += NT) {
+            const int fr = i % FT, L = Lb + i / FT;
+            const long long f = f0 + fr;
+            if (f < p.frames) rvq_store_code(p, L, f, codes_l[fr][L]);
+        }
+    }
 }
 
 hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
