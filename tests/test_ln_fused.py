@@ -5,8 +5,8 @@ On small grids (batch 1-4 of 10 s) every q/k/v and fc1 tile computes LayerNorm (
 `input_layernorm` / `post_attention_layernorm` in MimiTransformerLayer.forward :851-869) of its own rows with the
 LayerNorm kernel's arithmetic (kernels.h ln_row_coeffs) and feeds its fp16 planes to the MFMAs from LDS.  The
 q/k/v outputs of every layer (taps "qkv0".."qkv7", fp32 after RoPE), the transformer output and all 32 codebooks
-must be equal BITWISE across the "ln_fused" option (0: LayerNorm launches, 1: fc1 prologue, 2: fc1 and q/k/v
-prologues), for every small-grid tile
+must be equal BITWISE across the "ln_fused" option (0: LayerNorm launches, 1: fc1 prologue, 2 / 3 / 4: fc1 and q/k/v
+prologues, q/k/v on 16x64 / 32x64 / 16x128 tiles), for every small-grid tile
 (16-, 32- and 64-row tiles: B = 1, 2, 4 at 10 s, a 1-sample clip, a length that leaves a partial tile), and the
 graph-replayed encode must give the same codes.  The ragged batch (LayerNorm kernel on packed rows, large grid)
 must equal per-utterance encodes (which take the prologue) -- the batch-invariance contract of
@@ -47,7 +47,7 @@ def run(engine, variant, xt, K=32):
 def test_ln_prologue_bitwise(engine, B, L):
     x = torch.from_numpy(np.stack([synthetic.speech_like(L, 71, i) for i in range(B)])).cuda()
     c0, t0 = run(engine, 0, x)
-    for v in (1, 2):
+    for v in (1, 2, 3, 4):
         c1, t1 = run(engine, v, x)
         for name in TAPS:
             assert np.array_equal(t0[name], t1[name]), (v, name, int((t0[name] != t1[name]).sum()), t0[name].size)
@@ -85,4 +85,4 @@ def test_ln_prologue_ragged_equals_single(engine):
 def test_ln_option_rejects_bad_value(engine):
     from mimi_hip._lib import MimiHipError
     with pytest.raises(MimiHipError):
-        engine.set_option("ln_fused", 3)
+        engine.set_option("ln_fused", 5)

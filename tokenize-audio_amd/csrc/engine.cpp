@@ -330,6 +330,7 @@ struct mimi_engine {
     // 20.8 vs 10.4 + 5.2 us -- its one compute wave and 16-row tiles leave the prologue's chain exposed
     int ln_fused = 1;
     int rvq_form = 0;  // RVQ level-kernel form (mimi_set_option "rvq_form"; RvqArgs::form)
+    int ln_rpw = 1;  // LayerNorm rows per wave (mimi_set_option "ln_rpw": 1 (A/B r4h: 0.186 vs 0.200 ms per B = 32 step for 2), 2, 4, 8; the same bits)
     int rvq_chain = 1;  // small grids: the persistent all-levels RVQ (mimi_set_option "rvq_chain"; RvqArgs::chain)
     // transformer GEMMs with sc1 output stores (gemm_planes.h FL_SC1OUT; mimi_set_option "sc1_out"): bit 0 q/k/v,
     // bit 1 fc1, bit 2 o_proj and fc2 (large batches; the same bits either way)
@@ -1195,6 +1196,15 @@ static GemmArgs linear_args(const float* in, int64_t rows, int K, const float* W
         if (_e != hipSuccess) return set_err(MIMI_ERR_HIP, "launch %s: %s", what, hipGetErrorString(_e)); \
     } while (0)
 
+static const char* ln_kname(int rpw) {
+    switch (rpw) {
+        case 1: return "mimi::layernorm_kernel<512, 1>";
+        case 4: return "mimi::layernorm_kernel<512, 4>";
+        case 8: return "mimi::layernorm_kernel<512, 8>";
+        default: return "mimi::layernorm_kernel<512, 2>";
+    }
+}
+
 static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int32_t* codes, int frames_per_item,
                    void* work, hipStream_t s, Recorder& rec, const int* flen = nullptr, double valid_share = 1.0) {
     RvqArgs r{};
@@ -1517,6 +1527,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         // rows' LayerNorm (the same bits as the LayerNorm kernel's planes, gemm_planes.h FL_LNA)
         auto ln_into = [&](GemmArgs& g, int role, const float* lw, const float* lb, const Act& act) {
             if (!h16 || e->ln_fused < (role == ROLE_QKV ? 2 : 1) || !gemm_ln_prologue_ok(role, g, prec)) return false;
+            if (role == ROLE_QKV) g.ln_tile = e->ln_fused - 2;  // (2: 16x64, 3: 32x64, 4: 16x128 tiles)
             g.ln_x = w.t0;
             g.ln_g = lw;
             g.ln_b = lb;
@@ -1545,9 +1556,9 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         use_h(aq, x.wqkv_h, x.wqkv_hs, t1a);
         if (!ln_into(aq, ROLE_QKV, x.ln1_w, x.ln1_b, t1a)) {
             LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1a.scale,
-                                        t1a.amax),
+                                        t1a.amax, nullptr, 0, e->ln_rpw),
                        "ln1");
-            rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
+            rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, ln_kname(e->ln_rpw));
         }
         aq.sc1 = (e->sc1_out & 1) != 0;
         LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, prec), "qkv");
@@ -1590,9 +1601,9 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         }
         if (!ln_into(a1, ROLE_FC1, x.ln2_w, x.ln2_b, t1b)) {
             LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1b.scale,
-                                        t1b.amax),
+                                        t1b.amax, nullptr, 0, e->ln_rpw),
                        "ln2");
-            rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, "mimi::layernorm_kernel<512, 2>");
+            rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, ln_kname(e->ln_rpw));
         }
         a1.sc1 = (e->sc1_out & 2) != 0;
         LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, prec), "fc1");
@@ -2308,6 +2319,17 @@ extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {
         e->rvq_form = (int)value;
         return MIMI_OK;
     }
+    if (!strcmp(key, "ln_rpw")) {
+        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
+            return set_err(MIMI_ERR_INVALID_ARGUMENT, "ln_rpw %lld (0, 1, 2, 4 or 8)", (long long)value);
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->ln_rpw != (int)value) {
+            drop_graphs(e);
+            e->graph_seen.clear();
+        }
+        e->ln_rpw = (int)value;
+        return MIMI_OK;
+    }
     if (!strcmp(key, "rvq_chain")) {
         if (value < 0 || value > 1) return set_err(MIMI_ERR_INVALID_ARGUMENT, "rvq_chain %lld (0 or 1)", (long long)value);
         HIP_TRY(hipSetDevice(e->device));
@@ -2329,7 +2351,7 @@ extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {
         return MIMI_OK;
     }
     if (!strcmp(key, "ln_fused")) {
-        if (value < 0 || value > 2) return set_err(MIMI_ERR_INVALID_ARGUMENT, "ln_fused %lld (0, 1 or 2)", (long long)value);
+        if (value < 0 || value > 4) return set_err(MIMI_ERR_INVALID_ARGUMENT, "ln_fused %lld (0 .. 4)", (long long)value);
         HIP_TRY(hipSetDevice(e->device));
         if (e->ln_fused != (int)value) {
             drop_graphs(e);

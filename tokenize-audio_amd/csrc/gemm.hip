@@ -260,6 +260,8 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         // the tile rule of run_small_h16 (q/k/v never reaches its 64-row tile on a small grid)
         if (role == ROLE_QKV) {
             if (tiles(a, 32, 128) >= 256) return run_planes<32, 128, 2, 2, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
+            if (a.ln_tile == 1) return run_planes<32, 64, 2, 1, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
+            if (a.ln_tile == 2) return run_planes<16, 128, 1, 2, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
             return run_planes<16, 64, 1, 1, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
         }
         if (tiles(a, 64, 64) >= 256) return run_planes<64, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);

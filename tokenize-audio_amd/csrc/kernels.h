@@ -229,6 +229,7 @@ struct GemmArgs {
     // host-side dispatch hint (not read by the kernels): 1 = take the FL_SC1OUT instantiation where the role has one
     // (engine option sc1_out; the same bits either way)
     int sc1;
+    int ln_tile;  // host-side hint: the q/k/v LayerNorm-prologue tile on small grids (0 16x64, 1 32x64, 2 16x128)
 };
 // true when launch_gemm(role, a, precision) runs a tile with the LayerNorm prologue (a.ln_* then feed A)
 bool gemm_ln_prologue_ok(int role, const GemmArgs& a, int precision);
@@ -320,7 +321,7 @@ hipError_t launch_conv0(const float* x, long long L, int batch, const float* w /
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* y, long long rows,
                             int C, float eps, hipStream_t s, void* yp = nullptr, long long y_pstride = 0,
                             int yns = 0, float yscale = 0.0f, unsigned* yamax = nullptr, const int* row_len = nullptr,
-                            int row_T = 0);
+                            int row_T = 0, int rpw = 0);
 
 // Sliding-window causal attention on the fused qkv tensor [B][T][3*H*D] (q, k already rotated);
 // output [B][T][H*D].  h16: the fp16-plane kernels (PREC_F16X3; T <= 256 needs fp16-plane output), else fp32.

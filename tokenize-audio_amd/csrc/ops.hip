@@ -146,13 +146,21 @@ __global__ __launch_bounds__(512) void layernorm_kernel(const float* __restrict_
 
 hipError_t launch_layernorm(const float* x, const float* g, const float* b, float* y, long long rows, int C,
                             float eps, hipStream_t s, void* yp, long long y_pstride, int yns, float yscale,
-                            unsigned* yamax, const int* row_len, int row_T) {
+                            unsigned* yamax, const int* row_len, int row_T, int rpw) {
     if (row_len && row_T <= 0) return hipErrorInvalidValue;
     if (C != 512 || (yns != 0 && !yp) || (yscale > 0.0f && yns != 2)) return hipErrorInvalidValue;
-    constexpr int RPW = 2;  // 16 rows per workgroup
-    hipLaunchKernelGGL((layernorm_kernel<512, RPW>), dim3((unsigned)((rows + 8 * RPW - 1) / (8 * RPW))), dim3(512), 0, s,
-                       x, g, b, y,
-                       rows, eps, reinterpret_cast<__bf16*>(yp), y_pstride, yns, yscale, yamax, row_len, row_T);
+    // rpw rows per wave (8 waves per workgroup): 2 by default (16 rows per workgroup); 1, 4, 8 for A/B
+#define LN_LAUNCH(R_)                                                                                                \
+    hipLaunchKernelGGL((layernorm_kernel<512, R_>), dim3((unsigned)((rows + 8 * (R_) - 1) / (8 * (R_)))), dim3(512), 0, \
+                       s, x, g, b, y, rows, eps, reinterpret_cast<__bf16*>(yp), y_pstride, yns, yscale, yamax, row_len,  \
+                       row_T)
+    switch (rpw) {
+        case 1: LN_LAUNCH(1); break;
+        case 4: LN_LAUNCH(4); break;
+        case 8: LN_LAUNCH(8); break;
+        default: LN_LAUNCH(2); break;
+    }
+#undef LN_LAUNCH
     return hipGetLastError();
 }
 
