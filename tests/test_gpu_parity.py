@@ -98,8 +98,8 @@ def test_kernel_options_identical_codes(engine):
     and every RVQ form, on a B = 16 x 10 s batch at K = 32."""
     x = torch.from_numpy(synthetic.clip_batch(16, 240000, seed=88))[:, None].cuda()
     base = engine.encode(x, num_quantizers=32).audio_codes.cpu()
-    defaults = {"sc1_out": 2, "rvq_form": 0, "rvq_chain": 1}
-    cases = [("sc1_out", 0), ("sc1_out", 7), ("rvq_chain", 0)] + [("rvq_form", f) for f in range(1, 7)]
+    defaults = {"sc1_out": 2, "rvq_form": 0, "rvq_chain": 1, "rvq_xcd": 1}
+    cases = [("sc1_out", 0), ("sc1_out", 7), ("rvq_chain", 0), ("rvq_xcd", 0)] + [("rvq_form", f) for f in range(1, 7)]
     for key, val in cases:
         engine.set_option(key, val)
         try:

@@ -331,6 +331,7 @@ struct mimi_engine {
     int ln_fused = 1;
     int rvq_form = 0;  // RVQ level-kernel form (mimi_set_option "rvq_form"; RvqArgs::form)
     int ln_rpw = 1;  // LayerNorm rows per wave (mimi_set_option "ln_rpw": 1 (A/B r4h: 0.186 vs 0.200 ms per B = 32 step for 2), 2, 4, 8; the same bits)
+    int rvq_xcd = 1;  // large grids: a frame tile's RVQ slices on one XCD (mimi_set_option "rvq_xcd"; same bits)
     int rvq_chain = 1;  // small grids: the persistent all-levels RVQ (mimi_set_option "rvq_chain"; RvqArgs::chain)
     // transformer GEMMs with sc1 output stores (gemm_planes.h FL_SC1OUT; mimi_set_option "sc1_out"): bit 0 q/k/v,
     // bit 1 fc1, bit 2 o_proj and fc2 (large batches; the same bits either way)
@@ -1227,6 +1228,7 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     r.frames_per_item = frames_per_item;
     r.form = e->rvq_form;
     r.chain = e->rvq_chain;
+    r.xcd_group_ok = e->rvq_xcd;
     const char* kname = "?";
     LAUNCH_TRY(launch_rvq(r, s, &kname), "rvq");
     rec.mark("rvq", 2.0 * frames * valid_share * r.D * r.ncodes * K,
@@ -2328,6 +2330,16 @@ extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {
             e->graph_seen.clear();
         }
         e->ln_rpw = (int)value;
+        return MIMI_OK;
+    }
+    if (!strcmp(key, "rvq_xcd")) {
+        if (value < 0 || value > 1) return set_err(MIMI_ERR_INVALID_ARGUMENT, "rvq_xcd %lld (0 or 1)", (long long)value);
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->rvq_xcd != (int)value) {
+            drop_graphs(e);
+            e->graph_seen.clear();
+        }
+        e->rvq_xcd = (int)value;
         return MIMI_OK;
     }
     if (!strcmp(key, "rvq_chain")) {

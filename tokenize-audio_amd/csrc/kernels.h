@@ -382,6 +382,8 @@ struct RvqArgs {
                             // approximation (round 3), 2..6 one-product variants (launch_rvq)
     int chain;              // small grids: all levels in one persistent launch (rvq_chain_h16_kernel; engine option
                             // rvq_chain; same codes)
+    int xcd_group_ok;       // large grids: the slices of a frame tile on one XCD (engine option rvq_xcd; speed only)
+    int xcd_group;          // (set by launch_rvq)
 };
 size_t rvq_work_bytes(long long frames);
 hipError_t launch_rvq(const RvqArgs& a, hipStream_t s, const char** kname = nullptr);  // kname: the level kernel's symbol

@@ -1540,8 +1540,18 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
     static_assert(FT == 32 || FT == 64, "frame tile (RVQ_FT pads the work layout to 64)");
     // RG (a ragged batch: p.flen): a workgroup none of whose frames is valid has nothing to do -- no later level
     // reads what it would write (only valid frames' residuals and partial argmins are ever read)
+    // p.xcd_group (large grids, round 4): a 1-D grid whose workgroup b runs slice (b >> 3) % NSL of frame tile
+    // (b & 7) + 8 ((b >> 3) / NSL) -- the slices of a frame tile land on one XCD (workgroups are dealt round-robin over
+    // the 8 XCDs; speed only), so its L2 serves the residual and code-row reads the NSL slices share
+    unsigned ftile = blockIdx.x, slc = blockIdx.y;
+    if (p.xcd_group) {
+        const unsigned q = blockIdx.x >> 3;
+        slc = q % NSL;
+        ftile = (blockIdx.x & 7) + 8 * (q / NSL);
+        if ((long long)ftile * FT >= p.frames) return;  // (padding of the grid to whole groups of 8 frame tiles)
+    }
     if constexpr (RG) {
-        if (!__syncthreads_or((int)threadIdx.x < FT && rvq_valid(p, (long long)blockIdx.x * FT + threadIdx.x))) return;
+        if (!__syncthreads_or((int)threadIdx.x < FT && rvq_valid(p, (long long)ftile * FT + threadIdx.x))) return;
     }
     const int L = L0 + (int)blockIdx.z;  // (grid.z = 2: the semantic and first acoustic levels together)
     constexpr int LDH = D / 2 + 4;
@@ -1557,8 +1567,8 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
     __shared__ unsigned long long best[FT];
     __shared__ float ynl[SLC];  // |e|^2 of the slice's codes
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-    const long long f0 = (long long)blockIdx.x * FT;
-    const int slice = blockIdx.y;
+    const long long f0 = (long long)ftile * FT;
+    const int slice = (int)slc;
     const RvqWork w = rvq_work(p, NSL);
     // the level's scalars and this lane's code norms, loaded here so the barriers below wait for them (used after the
     // MFMA loop, where a load is a whole exposed memory round trip)
@@ -2059,7 +2069,9 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
                  a.flen ? "true" : "false", scfg ? 32 : 64, nwv, ft, p1 ? "true" : "false");
         *kname = kn;
         for (int L = 0; L < a.levels; L += (split && L == 0) ? 2 : 1) {
-            const dim3 g(ftiles, nsl, (split && L == 0) ? 2 : 1);
+            a.xcd_group = (!scfg && a.xcd_group_ok) ? 1 : 0;
+            const dim3 g = a.xcd_group ? dim3((ftiles + 7) / 8 * 8 * nsl, 1, (split && L == 0) ? 2 : 1)
+                                       : dim3(ftiles, nsl, (split && L == 0) ? 2 : 1);
             const dim3 blk(64 * nwv);
             // (ragged, RG: workgroups of invalid frames exit)
 #define RVQ_LAUNCH(PF_, EX_, CW_, NWV_, FT_, P1_)                                                                   \
