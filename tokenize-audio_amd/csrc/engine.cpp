@@ -333,6 +333,10 @@ struct mimi_engine {
     int ln_rpw = 1;  // LayerNorm rows per wave (mimi_set_option "ln_rpw": 1 (A/B r4h: 0.186 vs 0.200 ms per B = 32 step for 2), 2, 4, 8; the same bits)
     int rvq_xcd = 1;  // large grids: a frame tile's RVQ slices on one XCD (mimi_set_option "rvq_xcd"; same bits)
     int rvq_chain = 1;  // small grids: the persistent all-levels RVQ (mimi_set_option "rvq_chain"; RvqArgs::chain)
+    // q/k/v + attention as one kernel (qkv_attn.hip) for items of <= 256 frames: 0 off, 1 when the batch has at least
+    // 256 (item, head) pairs (one workgroup per CU), 2 whenever the items fit (mimi_set_option "qkv_attn"; same bits)
+    int qkv_attn = 1;
+    int qkv_attn_xcd = 1;  // its workgroups: an item's heads on one XCD (mimi_set_option "qkv_attn_xcd"; same bits)
     // transformer GEMMs with sc1 output stores (gemm_planes.h FL_SC1OUT; mimi_set_option "sc1_out"): bit 0 q/k/v,
     // bit 1 fc1, bit 2 o_proj and fc2 (large batches; the same bits either way)
     int sc1_out = 2;  // (A/B, round 4: fc1 0.594 -> 0.576 ms per B = 32 step; q/k/v, o_proj and fc2 slower with it)
@@ -1556,27 +1560,58 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         }
         if (ns) planes_in(aq, w.t1, nact);
         use_h(aq, x.wqkv_h, x.wqkv_hs, t1a);
-        if (!ln_into(aq, ROLE_QKV, x.ln1_w, x.ln1_b, t1a)) {
+        // q/k/v + attention in one kernel (qkv_attn.hip): large batches of items <= 256 frames, fp16 planes
+        const bool fuse_qa = h16 && ns && e->qkv_attn && Dh == 64 && (rg ? rg->maxT25 <= 256 : T <= 256) &&
+                             (e->qkv_attn == 2 || (long long)B * H >= 256);
+        if (fuse_qa || !ln_into(aq, ROLE_QKV, x.ln1_w, x.ln1_b, t1a)) {
             LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1a.scale,
                                         t1a.amax, nullptr, 0, e->ln_rpw),
                        "ln1");
             rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, ln_kname(e->ln_rpw));
         }
-        aq.sc1 = (e->sc1_out & 1) != 0;
-        LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, prec), "qkv");
-        rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
-        if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, tapB, tapT, 3 * H * Dh, s))) return rc;
         const Act atta = new_act(nmf("xf%d.att", l));
-        // fp16-plane attention in f16x3 mode (also for the no-plane long clips: the same arithmetic as their
-        // prefixes); true fp32 in f32 mode and the bf16 modes
-        const bool ah16 = prec == PREC_F16X3;
-        LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh), s,
-                                    w.att, nact, ns, atta.scale, atta.amax, ah16, rg ? dT25 : nullptr,
-                                    rg ? rg->maxT25 : 0, rg ? rg->minT25 : 0, dToff),
-                   "attention");
-        rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4,
-                 ah16 ? (T <= 256 ? "mimi::attention_t256_h16_kernel" : "mimi::attention_band_h16_kernel")
-                     : (T <= 256 ? "mimi::attention_t256_kernel" : "mimi::attention_kernel"));
+        if (fuse_qa) {
+            QkvAttnArgs qa{};
+            qa.Ap = aq.Ap;
+            qa.a_pstride = aq.a_pstride;
+            qa.a_rows = rows;
+            qa.Wp = aq.Wsplit;
+            qa.unscale = aq.unscale;
+            qa.rope_cos = e->rope_cos;
+            qa.rope_sin = e->rope_sin;
+            qa.K = Hd;
+            qa.Ts = (int)T;
+            qa.H = H;
+            qa.window = c.sliding_window;
+            qa.scale = 1.0f / std::sqrt((float)Dh);
+            qa.outp = w.att;
+            qa.out_pstride = nact;
+            qa.oscale = atta.scale;
+            qa.oamax = atta.amax;
+            qa.tlen = rg ? dT25 : nullptr;
+            qa.toff = rg ? dToff : nullptr;
+            qa.qkv = e->taps ? w.qkv : nullptr;  // (the q/k/v tap, as the GEMM would have stored it)
+            qa.xcd = e->qkv_attn_xcd;
+            LAUNCH_TRY(launch_qkv_attention(qa, B, s), "qkv_attention");
+            rec.mark("qkv_attention", gemm_flops(aq) + att_flops, (double)rows * Hd * 4 * 2 + 3.0 * H * Dh * Hd * 4,
+                     "mimi::qkv_attention_h16_kernel");
+            if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, tapB, tapT, 3 * H * Dh, s))) return rc;
+        } else {
+            aq.sc1 = (e->sc1_out & 1) != 0;
+            LAUNCH_TRY(launch_gemm(ROLE_QKV, aq, s, &kname, prec), "qkv");
+            rec.mark("qkv", gemm_flops(aq), gemm_bytes(aq, false), kname);
+            if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, tapB, tapT, 3 * H * Dh, s))) return rc;
+            // fp16-plane attention in f16x3 mode (also for the no-plane long clips: the same arithmetic as their
+            // prefixes); true fp32 in f32 mode and the bf16 modes
+            const bool ah16 = prec == PREC_F16X3;
+            LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh),
+                                        s, w.att, nact, ns, atta.scale, atta.amax, ah16, rg ? dT25 : nullptr,
+                                        rg ? rg->maxT25 : 0, rg ? rg->minT25 : 0, dToff),
+                       "attention");
+            rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4,
+                     ah16 ? (T <= 256 ? "mimi::attention_t256_h16_kernel" : "mimi::attention_band_h16_kernel")
+                         : (T <= 256 ? "mimi::attention_t256_kernel" : "mimi::attention_kernel"));
+        }
         if ((rc = save_tap_planes(e, nmf("att%d", l).c_str(), w.att, ns, tapB, tapT, H * Dh, s, atta.scale))) return rc;
         GemmArgs ao = linear_args(w.att, rows, H * Dh, x.wo, Hd, w.t0);
         ao.Wsplit = x.wo_s;
@@ -2298,78 +2333,39 @@ extern "C" int mimi_set_graphs(mimi_engine* e, int32_t enable) {
 
 extern "C" int64_t mimi_graph_replays(const mimi_engine* e) { return e ? e->graph_replays : -1; }
 
+// mimi_set_option keys: engine field, allowed values (bit v of `allowed` set: value v accepted), what they select.
+// Every key changes the kernel sequence (never the bits an encode produces), so a change drops captured graphs.
+struct EngineOption {
+    const char* key;
+    int mimi_engine::*field;
+    unsigned allowed;
+    const char* values;
+};
+static const EngineOption kEngineOptions[] = {
+    {"stage0_fused", &mimi_engine::stage0_fused, 0x3u, "0 or 1"},
+    {"rvq_form", &mimi_engine::rvq_form, 0x7fu, "0..6"},
+    {"ln_rpw", &mimi_engine::ln_rpw, 0x117u, "0, 1, 2, 4 or 8"},
+    {"rvq_xcd", &mimi_engine::rvq_xcd, 0x3u, "0 or 1"},
+    {"rvq_chain", &mimi_engine::rvq_chain, 0x3u, "0 or 1"},
+    {"sc1_out", &mimi_engine::sc1_out, 0xffu, "0..7"},
+    {"ln_fused", &mimi_engine::ln_fused, 0x1fu, "0 .. 4"},
+    {"qkv_attn", &mimi_engine::qkv_attn, 0x7u, "0, 1 or 2"},
+    {"qkv_attn_xcd", &mimi_engine::qkv_attn_xcd, 0x3u, "0 or 1"},
+};
+
 extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {
     if (!e || !key) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine or key");
     std::lock_guard<std::mutex> lk(e->mu);
-    if (!strcmp(key, "stage0_fused")) {
-        if (value < 0 || value > 1) return set_err(MIMI_ERR_INVALID_ARGUMENT, "stage0_fused %lld (0 or 1)", (long long)value);
+    for (const EngineOption& o : kEngineOptions) {
+        if (strcmp(key, o.key)) continue;
+        if (value < 0 || value > 31 || !((o.allowed >> value) & 1u))
+            return set_err(MIMI_ERR_INVALID_ARGUMENT, "%s %lld (%s)", key, (long long)value, o.values);
         HIP_TRY(hipSetDevice(e->device));
-        if (e->stage0_fused != (int)value) {  // captured graphs hold the other kernel sequence
+        if (e->*o.field != (int)value) {  // captured graphs hold the other kernel sequence
             drop_graphs(e);
             e->graph_seen.clear();
         }
-        e->stage0_fused = (int)value;
-        return MIMI_OK;
-    }
-    if (!strcmp(key, "rvq_form")) {
-        if (value < 0 || value > 6) return set_err(MIMI_ERR_INVALID_ARGUMENT, "rvq_form %lld (0..6)", (long long)value);
-        HIP_TRY(hipSetDevice(e->device));
-        if (e->rvq_form != (int)value) {
-            drop_graphs(e);
-            e->graph_seen.clear();
-        }
-        e->rvq_form = (int)value;
-        return MIMI_OK;
-    }
-    if (!strcmp(key, "ln_rpw")) {
-        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
-            return set_err(MIMI_ERR_INVALID_ARGUMENT, "ln_rpw %lld (0, 1, 2, 4 or 8)", (long long)value);
-        HIP_TRY(hipSetDevice(e->device));
-        if (e->ln_rpw != (int)value) {
-            drop_graphs(e);
-            e->graph_seen.clear();
-        }
-        e->ln_rpw = (int)value;
-        return MIMI_OK;
-    }
-    if (!strcmp(key, "rvq_xcd")) {
-        if (value < 0 || value > 1) return set_err(MIMI_ERR_INVALID_ARGUMENT, "rvq_xcd %lld (0 or 1)", (long long)value);
-        HIP_TRY(hipSetDevice(e->device));
-        if (e->rvq_xcd != (int)value) {
-            drop_graphs(e);
-            e->graph_seen.clear();
-        }
-        e->rvq_xcd = (int)value;
-        return MIMI_OK;
-    }
-    if (!strcmp(key, "rvq_chain")) {
-        if (value < 0 || value > 1) return set_err(MIMI_ERR_INVALID_ARGUMENT, "rvq_chain %lld (0 or 1)", (long long)value);
-        HIP_TRY(hipSetDevice(e->device));
-        if (e->rvq_chain != (int)value) {
-            drop_graphs(e);
-            e->graph_seen.clear();
-        }
-        e->rvq_chain = (int)value;
-        return MIMI_OK;
-    }
-    if (!strcmp(key, "sc1_out")) {
-        if (value < 0 || value > 7) return set_err(MIMI_ERR_INVALID_ARGUMENT, "sc1_out %lld (0..7)", (long long)value);
-        HIP_TRY(hipSetDevice(e->device));
-        if (e->sc1_out != (int)value) {
-            drop_graphs(e);
-            e->graph_seen.clear();
-        }
-        e->sc1_out = (int)value;
-        return MIMI_OK;
-    }
-    if (!strcmp(key, "ln_fused")) {
-        if (value < 0 || value > 4) return set_err(MIMI_ERR_INVALID_ARGUMENT, "ln_fused %lld (0 .. 4)", (long long)value);
-        HIP_TRY(hipSetDevice(e->device));
-        if (e->ln_fused != (int)value) {
-            drop_graphs(e);
-            e->graph_seen.clear();
-        }
-        e->ln_fused = (int)value;
+        e->*o.field = (int)value;
         return MIMI_OK;
     }
     return set_err(MIMI_ERR_INVALID_ARGUMENT, "unknown option '%s'", key);

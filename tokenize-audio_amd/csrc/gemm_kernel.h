@@ -14,6 +14,12 @@ __device__ __forceinline__ float gelu_erf(float x) {
     return (x * 0.5f) * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
+// RoPE rotate-half of the pair (x1 = dim d, x2 = dim d + 32), d < 32 (TF/modeling_mimi.py:384-404): the q/k/v
+// GEMM epilogue (gemm_planes.h EPI_ROPE) and the fused q/k/v + attention kernel (qkv_attn.hip) form it with
+// these two expressions, so both give the same bits
+__device__ __forceinline__ float rope_lo(float x1, float x2, float c, float sn) { return x1 * c + (-x2) * sn; }
+__device__ __forceinline__ float rope_hi(float x2, float x1, float c, float sn) { return x2 * c + x1 * sn; }
+
 template <int BM, int BN, int WM, int WN, int BK, int NBUF, bool NFAST, bool ELU_IN, int PAD, int EPI, int TAG>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_f32_kernel(GemmArgs p) {
     constexpr int NT = WM * WN * 64;

@@ -628,10 +628,10 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                         const float sn = p.rope_sin[(long long)pos * 32 + (d & 31)];
                         if (((j / PJ) & 1) == 0) {
                             const float x2 = F16 ? acc[i][j + PJ][r] * us : acc[i][j + PJ][r];
-                            v = v * c + (-x2) * sn;
+                            v = rope_lo(v, x2, c, sn);
                         } else {
                             const float x1 = F16 ? acc[i][j - PJ][r] * us : acc[i][j - PJ][r];
-                            v = v * c + x1 * sn;
+                            v = rope_hi(v, x1, c, sn);
                         }
                     }
                 }

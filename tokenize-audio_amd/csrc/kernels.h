@@ -348,6 +348,35 @@ hipError_t launch_ragged_rows(const int* tlen, const int* toff, int B, int* rpos
 hipError_t launch_attention_band(const float* qkv, int batch, int T, int H, int window, float scale,
                                  hipStream_t s, void* outp, long long out_pstride, float oscale, unsigned* oamax);
 
+// Fused q/k/v projection + RoPE + attention for items of at most 256 frames (qkv_attn.hip): one workgroup per
+// (item, head) computes the head's 192 q/k/v columns of the item's rows on the fp16 planes (the q/k/v GEMM's
+// instruction sequence per output element) and runs attention_t256_h16_kernel's arithmetic on them in LDS -- the
+// fp32 q/k/v tensor never goes to HBM.  Bitwise the same attention output as launch_gemm(ROLE_QKV) +
+// launch_attention.
+struct QkvAttnArgs {
+    const void* Ap;            // LayerNorm output, 2 fp16 planes [rows][K] (plane 1 at + a_pstride elements)
+    long long a_pstride;
+    long long a_rows;          // rows in the planes buffer (range of the A loads)
+    const void* Wp;            // q/k/v weights, 2 fp16 planes [3 H 64][K]
+    float unscale;             // 1 / (activation scale x weight scale)
+    const float* rope_cos;     // [pos][32]
+    const float* rope_sin;
+    int K;                     // hidden size (multiple of 32)
+    int Ts;                    // uniform batches: frames per item (row stride)
+    int H;                     // heads (head_dim 64)
+    int window;
+    float scale;               // 1 / sqrt(64)
+    void* outp;                // attention output planes [rows][H 64], plane stride out_pstride
+    long long out_pstride;
+    float oscale;
+    unsigned* oamax;
+    const int* tlen;           // ragged batches: frames per item and first packed row (else null)
+    const int* toff;
+    float* qkv;                // optional: the fp32 q/k/v rows as the GEMM would store them (taps)
+    int xcd;                   // 1: an item's heads on one XCD (workgroup order; speed only)
+};
+hipError_t launch_qkv_attention(const QkvAttnArgs& a, int items, hipStream_t s);
+
 // planes -> fp32 (x0 + x1 [+ x2], or (h0 + h1) / hscale for fp16 planes); used only to materialise per-stage
 // taps of plane-format activations.
 hipError_t launch_planes_to_f32(const void* planes, long long pstride, int ns, float* out, long long n,
