@@ -337,6 +337,9 @@ struct mimi_engine {
     // 256 (item, head) pairs (one workgroup per CU), 2 whenever the items fit (mimi_set_option "qkv_attn"; same bits)
     int qkv_attn = 1;
     int qkv_attn_xcd = 1;  // its workgroups: an item's heads on one XCD (mimi_set_option "qkv_attn_xcd"; same bits)
+    // row-slab GEMM (gemm_rows.h) for the large-batch transformer linears: bit 0 fc1, bit 1 fc2, bit 2 o_proj
+    // (mimi_set_option "gemm_rows"; same bits)
+    int gemm_rows = 0;  // (A/B r4p, B = 32: fc1 0.587 -> 0.645-0.651 ms, fc2 0.50 -> 0.536-0.54, o_proj 0.204 -> 0.198-0.203: off)
     // transformer GEMMs with sc1 output stores (gemm_planes.h FL_SC1OUT; mimi_set_option "sc1_out"): bit 0 q/k/v,
     // bit 1 fc1, bit 2 o_proj and fc2 (large batches; the same bits either way)
     int sc1_out = 2;  // (A/B, round 4: fc1 0.594 -> 0.576 ms per B = 32 step; q/k/v, o_proj and fc2 slower with it)
@@ -1620,6 +1623,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         if (ns) planes_in(ao, w.att, nact);
         use_h(ao, x.wo_h, x.wo_hs, atta);
         ao.sc1 = (e->sc1_out & 4) != 0;
+        ao.rows_form = (e->gemm_rows & 4) != 0;
         LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
         rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
         if ((rc = save_tap(e, nmf("oproj%d", l).c_str(), w.t0, tapB, tapT, Hd, s))) return rc;
@@ -1643,6 +1647,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, ln_kname(e->ln_rpw));
         }
         a1.sc1 = (e->sc1_out & 2) != 0;
+        a1.rows_form = (e->gemm_rows & 1) != 0;
         LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, prec), "fc1");
         rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
         if ((rc = save_tap_planes(e, nmf("ff%d", l).c_str(), w.ff, ns, tapB, tapT, c.intermediate_size, s, ffa.scale)))
@@ -1660,6 +1665,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             out_act(a2, dsin);
         }
         a2.sc1 = (e->sc1_out & 4) != 0;
+        a2.rows_form = (e->gemm_rows & 2) != 0;
         LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname, prec), "fc2");
         rec.mark("fc2", gemm_flops(a2), gemm_bytes(a2, true), kname);
         snprintf(nm, sizeof nm, "xfmr%d", l);
@@ -2351,6 +2357,7 @@ static const EngineOption kEngineOptions[] = {
     {"ln_fused", &mimi_engine::ln_fused, 0x1fu, "0 .. 4"},
     {"qkv_attn", &mimi_engine::qkv_attn, 0x7u, "0, 1 or 2"},
     {"qkv_attn_xcd", &mimi_engine::qkv_attn_xcd, 0x3u, "0 or 1"},
+    {"gemm_rows", &mimi_engine::gemm_rows, 0xffu, "0..7"},
 };
 
 extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {

@@ -230,6 +230,8 @@ struct GemmArgs {
     // (engine option sc1_out; the same bits either way)
     int sc1;
     int ln_tile;  // host-side hint: the q/k/v LayerNorm-prologue tile on small grids (0 16x64, 1 32x64, 2 16x128)
+    int rows_form;  // host-side hint: 1 = the row-slab kernel (gemm_rows.h) where the role has one (fc1 / fc2 / o_proj,
+                    // large grids, f16x3; engine option gemm_rows; the same bits either way)
 };
 // true when launch_gemm(role, a, precision) runs a tile with the LayerNorm prologue (a.ln_* then feed A)
 bool gemm_ln_prologue_ok(int role, const GemmArgs& a, int precision);

@@ -10,7 +10,7 @@
 //      order, the 3 plane products in mma_split's order), so every fp32 q/k/v value is bitwise the one the GEMM
 //      stores.  Wave w owns 16 rows and all 192 columns, the RoPE pairs (d, d + 32) in one lane (gemm_kernel.h
 //      rope_lo / rope_hi).  A fragments load straight into registers two K steps ahead; the W planes stream through
-//      a 4-deep LDS-DMA ring (the first form, both operands through a 2-stage ring of 56 KiB, kept one stage in
+//      a 5-deep LDS-DMA ring (the first form, both operands through a 2-stage ring of 56 KiB, kept one stage in
 //      flight: ~13 GB/s per CU of ingest and 0.87 ms per B = 32 step, slower than the two kernels' 0.74).
 //   2. Epilogue in registers: unscale, RoPE on q and k; q goes to an fp32 LDS image (the attention tasks' queries
 //      belong to other waves), k / v stay in the accumulators; the head's max |k|, |v| over the item's frames.
@@ -18,7 +18,7 @@
 //      head's power-of-two scales, per-task Q planes, the chunk loops, the two-half merge and the planes store.
 // Every value is computed as on the unfused path, so an item's codes do not depend on which path its batch took
 // (the engine runs this kernel only for large batches; batch 1 keeps the small-grid GEMM + attention).
-#include "gemm_planes.h"
+#include "gemm_rows.h"
 #include "attn_h16.h"
 
 #ifndef QA_DIAG
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
     constexpr int KLD = 72, KPL = TM * KLD;  // K planes: [256][72 halves]
     constexpr int VPL = TM * D;              // V planes: [256 keys][64 dims] (attn_vrow_off)
     constexpr int BK = 32, NC = 3 * D;       // K step; the head's q/k/v columns
-    constexpr int S = 4;                                 // W ring stages
+    constexpr int S = 5;                                 // W ring stages
     constexpr int BIMG = NC * BK, BSTG = 2 * BIMG;       // halves per W plane image / stage
     constexpr int NPB = 2 * NC / 16;                     // 1-KiB DMA pieces per stage: 24
     constexpr int QLD = D + 4;                           // q image row (floats)
@@ -110,21 +110,18 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
 #pragma unroll
     for (int j = 0; j < 12; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     bf16x8 a[3][2];  // A fragments of K steps kt, kt + 1, kt + 2 (slot kt % 3)
-    // issue order (vmcnt counts this wave's loads in order): W(0) .. W(S-3), A(0), W(S-2), A(1), then per K step kt
-    // W(kt + S - 1), A(kt + 2) -- at step kt the ops issued after A(kt) are those of step kt - 1
+    // W(0) .. W(S-2) and A(0), A(1) ahead; per K step kt: W(kt + S - 1), A(kt + 2).  The wait before step kt's
+    // barrier counts only the DMA pieces certainly behind W(kt) -- those of W(kt + 1) .. W(kt + S - 2), 2 per wave
+    // each: the compiler keeps the DMA issues in order against the waits but places the A register loads freely
+    // (and inserts their waits itself), see gemm_rows.h rows_dma_after
 #pragma unroll
-    for (int k = 0; k < S - 2; ++k)
+    for (int k = 0; k < S - 1; ++k)
         if (k < KT) issueB(k);
     loadA(0, a[0]);
-    if (S - 2 < KT) issueB(S - 2);
     if (1 < KT) loadA(1, a[1]);
     // one K step with the A fragments in `a`; refills go to `an` (the step two ahead)
     auto step = [&](int kt, bf16x8 (&a)[2], bf16x8 (&an)[2]) __attribute__((always_inline)) {
-        if (kt + S - 2 < KT) {  // step kt - 1 issued W(kt + S - 2) (2 pieces) and A(kt + 1) (2 loads) after A(kt)
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        vm_wait(rows_dma_after<S, KT, 2>(kt));
         __builtin_amdgcn_s_barrier();  // every wave's W pieces of stage kt landed; stage kt - 1 is free
         if (!(QA_DIAG & 2)) {
             if (kt + S - 1 < KT) issueB(kt + S - 1);
