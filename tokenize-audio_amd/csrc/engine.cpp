@@ -340,6 +340,10 @@ struct mimi_engine {
     // row-slab GEMM (gemm_rows.h) for the large-batch transformer linears: bit 0 fc1, bit 1 fc2, bit 2 o_proj
     // (mimi_set_option "gemm_rows"; same bits)
     int gemm_rows = 0;  // (A/B r4p, B = 32: fc1 0.587 -> 0.645-0.651 ms, fc2 0.50 -> 0.536-0.54, o_proj 0.204 -> 0.198-0.203: off)
+    // stage-2 residual block as one kernel (resblock_rows.hip) on large grids: 0 off, 1 on (mimi_set_option
+    // "res_rows"; same bits).  Off: 0.535-0.568 ms against 0.47 for the two planes GEMMs, the down conv before it
+    // 0.72 -> 0.67 (profiles/r4q_ab_res_rows.txt)
+    int res_rows = 0;
     // transformer GEMMs with sc1 output stores (gemm_planes.h FL_SC1OUT; mimi_set_option "sc1_out"): bit 0 q/k/v,
     // bit 1 fc1, bit 2 o_proj and fc2 (large batches; the same bits either way)
     int sc1_out = 2;  // (A/B, round 4: fc1 0.594 -> 0.576 ms per B = 32 step; q/k/v, o_proj and fc2 slower with it)
@@ -1335,6 +1339,12 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         snprintf(b, sizeof b, fmt, i);
         return std::string(b);
     };
+    // stage si's residual block as the one-kernel form (resblock_rows.hip): f16x3 planes, C = 256, >= 256 tiles of 128
+    // frames (smaller batches keep the two planes GEMMs: the same bits)
+    auto res_rows_on = [&](int si, int Cs) {
+        return h16 && ns && e->res_rows && si == 2 && Cs == 256 && c.compress == 2 && c.residual_kernel_size == 3 &&
+               (long long)B * ((p.T[si] + 127) / 128) >= 256;
+    };
     for (int si = 0; si < c.num_ratios; ++si) {
         const int64_t T = p.T[si];
         const bool unf = ns && si > 0 && si >= mimi_engine::kUnfuseFrom;
@@ -1428,6 +1438,35 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             snprintf(nm, sizeof nm, "res_s%d", si);
             const double by = BT * 4 * (si == 0 ? 1 + C : 2 * C) + (3.0 * C * H + H * C) * 4;
             rec.mark(nm, fl, by, kname);
+        } else if (res_rows_on(si, C)) {
+            // one kernel: k3 from the fp32 x (ELU(x) planes built in registers), h in LDS, k1 + skip + ELU -> y planes
+            const int Hh = C / c.compress;
+            hact = new_act(nmf("h%d", si));
+            yact = new_act(nmf("y%d", si));
+            ResRowsArgs rr{};
+            rr.x = w.x;
+            rr.T = (int)T;
+            rr.batch = B;
+            rr.tlen = rg ? dT[si] : nullptr;
+            rr.w3 = e->res3[si].wh;
+            rr.us3 = 1.0f / (xeact.scale * e->res3[si].wscale);
+            rr.b3 = e->res3[si].b;
+            rr.xscale = xeact.scale;
+            rr.xamax = xeact.amax;
+            rr.hscale = hact.scale;
+            rr.hamax = hact.amax;
+            rr.w1 = e->res1[si].wh;
+            rr.us1 = 1.0f / (hact.scale * e->res1[si].wscale);
+            rr.b1 = e->res1[si].b;
+            rr.yp = w.y;
+            rr.y_pstride = (long long)B * T * C;
+            rr.yscale = yact.scale;
+            rr.yamax = yact.amax;
+            LAUNCH_TRY(launch_resblock_rows(C, rr, s, &kname), "resblock rows");
+            const double BT = rows_of(si, (double)B * T);
+            snprintf(nm, sizeof nm, "res_s%d", si);
+            rec.mark(nm, 2.0 * BT * (3.0 * C * Hh + (double)Hh * C), BT * C * 4 * 2 + (3.0 * C * Hh + (double)Hh * C) * 4,
+                     kname);
         } else {
             // two plane GEMMs: h = ELU(b3 + W3 (*) ELU(x)) from the ELU(x) planes the down conv wrote, then
             // y = ELU(x + b1 + W1 . h) with the fp32 x as the skip
@@ -1471,6 +1510,8 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                 ad.C = nullptr;
                 xact = new_act("x_last");
                 out_act(ad, xact);
+            } else if (next_unf && res_rows_on(si + 1, 2 * C)) {  // fp32 x only: the block kernel splits ELU(x) itself
+                xeact = new_act(nmf("xe%d", si + 1));
             } else if (next_unf) {  // fp32 x (the skip) + ELU(x) planes (the next k3 conv's input)
                 ad.Cp = w.xe;
                 ad.c_pstride = (long long)B * p.T[si + 1] * 2 * C;
@@ -2358,6 +2399,7 @@ static const EngineOption kEngineOptions[] = {
     {"qkv_attn", &mimi_engine::qkv_attn, 0x7u, "0, 1 or 2"},
     {"qkv_attn_xcd", &mimi_engine::qkv_attn_xcd, 0x3u, "0 or 1"},
     {"gemm_rows", &mimi_engine::gemm_rows, 0xffu, "0..7"},
+    {"res_rows", &mimi_engine::res_rows, 0x3u, "0 or 1"},
 };
 
 extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {

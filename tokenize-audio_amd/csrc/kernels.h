@@ -379,6 +379,30 @@ struct QkvAttnArgs {
 };
 hipError_t launch_qkv_attention(const QkvAttnArgs& a, int items, hipStream_t s);
 
+// Stage-2 residual block (C = 256, H = 128) in one kernel on fp16 planes (resblock_rows.hip): the k3 conv's A
+// fragments built in registers from the fp32 x (ELU + the ELU(x) planes' split), h in LDS, the k1 conv + skip + ELU
+// -> y planes.  Bitwise the unfused path's y (down conv ELU(x) planes -> k3 planes GEMM -> k1 planes GEMM).
+struct ResRowsArgs {
+    const float* x;        // [batch][T][C] fp32 (the down conv's output: block input and skip)
+    int T, batch;
+    const int* tlen;       // ragged: valid frames per item (null: T)
+    const void* w3;        // k3 weight planes [2][H][3 C] (tap-major K), 1 / (ELU(x) scale x weight scale) in us3
+    float us3;
+    const float* b3;
+    float xscale;          // the ELU(x) planes' scale and max slot (the act slot the down conv would have filled)
+    unsigned* xamax;
+    float hscale;          // h planes (LDS only): scale and max slot
+    unsigned* hamax;
+    const void* w1;        // k1 weight planes [2][C][H]
+    float us1;
+    const float* b1;
+    void* yp;              // y planes [batch][T][C], plane stride y_pstride, scale yscale, max slot yamax
+    long long y_pstride;
+    float yscale;
+    unsigned* yamax;
+};
+hipError_t launch_resblock_rows(int C, const ResRowsArgs& a, hipStream_t s, const char** kname);
+
 // planes -> fp32 (x0 + x1 [+ x2], or (h0 + h1) / hscale for fp16 planes); used only to materialise per-stage
 // taps of plane-format activations.
 hipError_t launch_planes_to_f32(const void* planes, long long pstride, int ns, float* out, long long n,
