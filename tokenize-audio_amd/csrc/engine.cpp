@@ -1638,7 +1638,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             qa.xcd = e->qkv_attn_xcd;
             LAUNCH_TRY(launch_qkv_attention(qa, B, s), "qkv_attention");
             rec.mark("qkv_attention", gemm_flops(aq) + att_flops, (double)rows * Hd * 4 * 2 + 3.0 * H * Dh * Hd * 4,
-                     "mimi::qkv_attention_h16_kernel");
+                     "mimi::qkv_attention_h16_kernel<512>");
             if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, tapB, tapT, 3 * H * Dh, s))) return rc;
         } else {
             aq.sc1 = (e->sc1_out & 1) != 0;
