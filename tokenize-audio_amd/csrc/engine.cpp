@@ -337,6 +337,10 @@ struct mimi_engine {
     // 256 (item, head) pairs (one workgroup per CU), 2 whenever the items fit (mimi_set_option "qkv_attn"; same bits)
     int qkv_attn = 1;
     int qkv_attn_xcd = 1;  // its workgroups: an item's heads on one XCD (mimi_set_option "qkv_attn_xcd"; same bits)
+    // ... forming the input LayerNorm itself from the residual stream (mimi_set_option "qkv_attn_ln"; same bits).  Off:
+    // the per-step LayerNorm + split beside 48 accumulators spills (128 VGPRs at 16 waves): 0.47 -> 0.82 ms against
+    // the 0.09 ms of LayerNorm launches it saves (profiles/r4t_ab_qkv_attn_ln.txt)
+    int qkv_attn_ln = 0;
     // row-slab GEMM (gemm_rows.h) for the large-batch transformer linears: bit 0 fc1, bit 1 fc2, bit 2 o_proj
     // (mimi_set_option "gemm_rows"; same bits)
     int gemm_rows = 0;  // (A/B r4p, B = 32: fc1 0.587 -> 0.645-0.651 ms, fc2 0.50 -> 0.536-0.54, o_proj 0.204 -> 0.198-0.203: off)
@@ -1607,7 +1611,8 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         // q/k/v + attention in one kernel (qkv_attn.hip): large batches of items <= 256 frames, fp16 planes
         const bool fuse_qa = h16 && ns && e->qkv_attn && Dh == 64 && (rg ? rg->maxT25 <= 256 : T <= 256) &&
                              (e->qkv_attn == 2 || (long long)B * H >= 256);
-        if (fuse_qa || !ln_into(aq, ROLE_QKV, x.ln1_w, x.ln1_b, t1a)) {
+        const bool fuse_ln = fuse_qa && e->qkv_attn_ln;  // the fused kernel forms the LayerNorm itself
+        if (!fuse_ln && (fuse_qa || !ln_into(aq, ROLE_QKV, x.ln1_w, x.ln1_b, t1a))) {
             LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1a.scale,
                                         t1a.amax, nullptr, 0, e->ln_rpw),
                        "ln1");
@@ -1636,9 +1641,17 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             qa.toff = rg ? dToff : nullptr;
             qa.qkv = e->taps ? w.qkv : nullptr;  // (the q/k/v tap, as the GEMM would have stored it)
             qa.xcd = e->qkv_attn_xcd;
+            if (fuse_ln) {
+                qa.ln_x = w.t0;
+                qa.ln_g = x.ln1_w;
+                qa.ln_b = x.ln1_b;
+                qa.ln_eps = c.norm_eps;
+                qa.ln_scale = t1a.scale;
+                qa.ln_amax = t1a.amax;
+            }
             LAUNCH_TRY(launch_qkv_attention(qa, B, s), "qkv_attention");
             rec.mark("qkv_attention", gemm_flops(aq) + att_flops, (double)rows * Hd * 4 * 2 + 3.0 * H * Dh * Hd * 4,
-                     "mimi::qkv_attention_h16_kernel<512>");
+                     fuse_ln ? "mimi::qkv_attention_h16_kernel<512, true>" : "mimi::qkv_attention_h16_kernel<512, false>");
             if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, tapB, tapT, 3 * H * Dh, s))) return rc;
         } else {
             aq.sc1 = (e->sc1_out & 1) != 0;
@@ -2398,6 +2411,7 @@ static const EngineOption kEngineOptions[] = {
     {"ln_fused", &mimi_engine::ln_fused, 0x1fu, "0 .. 4"},
     {"qkv_attn", &mimi_engine::qkv_attn, 0x7u, "0, 1 or 2"},
     {"qkv_attn_xcd", &mimi_engine::qkv_attn_xcd, 0x3u, "0 or 1"},
+    {"qkv_attn_ln", &mimi_engine::qkv_attn_ln, 0x3u, "0 or 1"},
     {"gemm_rows", &mimi_engine::gemm_rows, 0xffu, "0..7"},
     {"res_rows", &mimi_engine::res_rows, 0x3u, "0 or 1"},
 };

@@ -376,6 +376,14 @@ struct QkvAttnArgs {
     const int* toff;
     float* qkv;                // optional: the fp32 q/k/v rows as the GEMM would store them (taps)
     int xcd;                   // 1: an item's heads on one XCD (workgroup order; speed only)
+    // optional: A = LayerNorm(ln_x) formed in-kernel with layernorm_kernel's arithmetic (its planes at ln_scale, max
+    // |out| to ln_amax) instead of read from Ap -- the input LayerNorm launch and its planes' HBM round trip go away
+    const float* ln_x;         // residual stream [rows][K] fp32
+    const float* ln_g;
+    const float* ln_b;
+    float ln_eps;
+    float ln_scale;
+    unsigned* ln_amax;
 };
 hipError_t launch_qkv_attention(const QkvAttnArgs& a, int items, hipStream_t s);
 
