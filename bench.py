@@ -240,7 +240,7 @@ def north_star_groups(prof, steps, pmc, pmc_note=None):
     base = lambda s: s.split("#")[0]  # noqa: E731  ("fc2#2": the same stage on a second kernel symbol)
     groups = {
         "conv_stack": [s for s in prof if base(s).startswith(("res", "down_s", "final"))],
-        "transformer": [s for s in prof if base(s) in ("layernorm", "qkv", "attention", "qkv_attention", "o_proj", "fc1", "fc2")],
+        "transformer": [s for s in prof if base(s) in ("layernorm", "qkv", "attention", "qkv_attention", "o_proj", "o_proj_ln", "fc1", "fc2")],
         "quantizer": [s for s in prof if base(s) in ("downsample", "input_proj", "rvq")],
     }
     out = {}

@@ -341,6 +341,10 @@ struct mimi_engine {
     // the per-step LayerNorm + split beside 48 accumulators spills (128 VGPRs at 16 waves): 0.47 -> 0.82 ms against
     // the 0.09 ms of LayerNorm launches it saves (profiles/r4t_ab_qkv_attn_ln.txt)
     int qkv_attn_ln = 0;
+    // o_proj + residual + the post-attention LayerNorm as one kernel (oproj_ln.hip) when the rows give >= 128 slabs
+    // of 32 (mimi_set_option "oproj_ln"; same bits).  Off: every 32-row slab streams all of W_o (1 MB of planes) through
+    // a 2-stage ring at ~20 GB/s per CU, 0.405 ms against 0.20 + 0.093 for the two kernels (profiles/r4v_ab_oproj_ln.txt)
+    int oproj_ln = 0;
     // row-slab GEMM (gemm_rows.h) for the large-batch transformer linears: bit 0 fc1, bit 1 fc2, bit 2 o_proj
     // (mimi_set_option "gemm_rows"; same bits)
     int gemm_rows = 0;  // (A/B r4p, B = 32: fc1 0.587 -> 0.645-0.651 ms, fc2 0.50 -> 0.536-0.54, o_proj 0.204 -> 0.198-0.203: off)
@@ -1678,10 +1682,35 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         use_h(ao, x.wo_h, x.wo_hs, atta);
         ao.sc1 = (e->sc1_out & 4) != 0;
         ao.rows_form = (e->gemm_rows & 4) != 0;
-        LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
-        rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
-        if ((rc = save_tap(e, nmf("oproj%d", l).c_str(), w.t0, tapB, tapT, Hd, s))) return rc;
         const Act t1b = new_act(nmf("xf%d.ln2", l));
+        // o_proj + residual + post-attention LayerNorm in one kernel (oproj_ln.hip) on large batches
+        const bool fuse_oln = h16 && ns && e->oproj_ln && Hd == 512 && H * Dh == 512 && (rows + 31) / 32 >= 128;
+        if (fuse_oln) {
+            OprojLnArgs ol{};
+            ol.Ap = ao.Ap;
+            ol.a_pstride = ao.a_pstride;
+            ol.Wp = ao.Wsplit;
+            ol.M = (int)rows;
+            ol.N = Hd;
+            ol.K = H * Dh;
+            ol.unscale = ao.unscale;
+            ol.scale = x.ls1;
+            ol.R = w.t0;
+            ol.C = w.t0;
+            ol.ln_g = x.ln2_w;
+            ol.ln_b = x.ln2_b;
+            ol.ln_eps = c.norm_eps;
+            ol.ln_scale = t1b.scale;
+            ol.ln_out = w.t1;
+            ol.ln_pstride = nact;
+            ol.ln_amax = t1b.amax;
+            LAUNCH_TRY(launch_oproj_ln(ol, s, &kname), "o_proj + LayerNorm");
+            rec.mark("o_proj_ln", gemm_flops(ao), gemm_bytes(ao, true) + (double)rows * Hd * 4, kname);
+        } else {
+            LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
+            rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
+        }
+        if ((rc = save_tap(e, nmf("oproj%d", l).c_str(), w.t0, tapB, tapT, Hd, s))) return rc;
         GemmArgs a1 = linear_args(w.t1, rows, Hd, x.w1, c.intermediate_size, w.ff);
         a1.Wsplit = x.w1_s;
         Act ffa;
@@ -1694,7 +1723,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             ffa = new_act(nmf("xf%d.ff", l));
             out_act(a1, ffa);
         }
-        if (!ln_into(a1, ROLE_FC1, x.ln2_w, x.ln2_b, t1b)) {
+        if (!fuse_oln && !ln_into(a1, ROLE_FC1, x.ln2_w, x.ln2_b, t1b)) {
             LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1b.scale,
                                         t1b.amax, nullptr, 0, e->ln_rpw),
                        "ln2");
@@ -2412,6 +2441,7 @@ static const EngineOption kEngineOptions[] = {
     {"qkv_attn", &mimi_engine::qkv_attn, 0x7u, "0, 1 or 2"},
     {"qkv_attn_xcd", &mimi_engine::qkv_attn_xcd, 0x3u, "0 or 1"},
     {"qkv_attn_ln", &mimi_engine::qkv_attn_ln, 0x3u, "0 or 1"},
+    {"oproj_ln", &mimi_engine::oproj_ln, 0x3u, "0 or 1"},
     {"gemm_rows", &mimi_engine::gemm_rows, 0xffu, "0..7"},
     {"res_rows", &mimi_engine::res_rows, 0x3u, "0 or 1"},
 };

@@ -411,6 +411,28 @@ struct ResRowsArgs {
 };
 hipError_t launch_resblock_rows(int C, const ResRowsArgs& a, hipStream_t s, const char** kname);
 
+// o_proj + layer scale + residual and the post-attention LayerNorm in one kernel (oproj_ln.hip): workgroups of 32
+// rows x all 512 columns; C (= R, in place) bitwise the o_proj planes GEMM's, the LayerNorm planes the LayerNorm
+// kernel's.
+struct OprojLnArgs {
+    const void* Ap;        // attention output planes [M][K] (plane 1 at + a_pstride)
+    long long a_pstride;
+    const void* Wp;        // o_proj weight planes [2][N][K]
+    int M, N, K;
+    float unscale;         // 1 / (activation scale x weight scale)
+    const float* scale;    // layer scale [N]
+    const float* R;        // residual stream [M][N] (read) ...
+    float* C;              // ... and the updated stream (may equal R)
+    const float* ln_g;
+    const float* ln_b;
+    float ln_eps;
+    float ln_scale;        // LayerNorm planes: out * ln_scale as 2 fp16 planes at ln_out (plane stride ln_pstride)
+    void* ln_out;
+    long long ln_pstride;
+    unsigned* ln_amax;
+};
+hipError_t launch_oproj_ln(const OprojLnArgs& a, hipStream_t s, const char** kname);
+
 // planes -> fp32 (x0 + x1 [+ x2], or (h0 + h1) / hscale for fp16 planes); used only to materialise per-stage
 // taps of plane-format activations.
 hipError_t launch_planes_to_f32(const void* planes, long long pstride, int ns, float* out, long long n,

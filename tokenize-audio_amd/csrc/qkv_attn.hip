@@ -23,7 +23,8 @@
 
 #ifndef QA_DIAG
 #define QA_DIAG 0  // timing diagnostics (tools/qa_diag.sh builds only; results garbage): 1 return after the q/k/v
-#endif             // epilogue, 2 no DMA refills in the K loop, 4 no MFMAs in the K loop
+#endif             // epilogue, 2 no DMA refills in the K loop, 4 no MFMAs in the K loop, 8 no chunk loop, 16 no K / V
+                   // plane writes
 
 namespace mimi {
 
@@ -322,6 +323,7 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
     _Float16* Vt = lds + 2 * KPL;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+        if (QA_DIAG & 16) break;
         const int row = wave * 16 + 4 * hsel + r;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
@@ -350,9 +352,11 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
         const int kstart = max(0, qw - p.window + 1) & ~31;
         const int n = (kend - kstart) / 32 + 1, n0 = (n + 1) >> 1;
         const int cb = kstart + (kh ? 32 * n0 : 0), ce = kstart + 32 * (kh ? n : n0);
-        for (int c0 = cb; c0 < ce; c0 += 32)
+        for (int c0 = cb; c0 < ce; c0 += 32) {
+            if (QA_DIAG & 8) break;
             attn_chunk_h16<KLD, KPL, D, VPL, true>(o, m, l, qf, Ks + c0 * KLD, Vt, c0, qw, qi, kend, p.window, hf, col,
                                                    usa, 1.0f, 16384.0f, vlb0, vlb1);
+        }
     }
     __syncthreads();  // K / V dead: the merge and the output staging reuse the LDS
     float* mo = reinterpret_cast<float*>(lds);
