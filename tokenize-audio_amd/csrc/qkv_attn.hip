@@ -26,6 +26,10 @@
 #endif             // epilogue, 2 no DMA refills in the K loop, 4 no MFMAs in the K loop, 8 no chunk loop, 16 no K / V
                    // plane writes
 
+#ifndef QA_KG
+#define QA_KG 1  // W ring stages retired per barrier (2: 0.468 -> 0.494 ms per B = 32 step, profiles/r4w_ab_kg.txt)
+#endif
+
 namespace mimi {
 
 template <int K, bool LN>
@@ -36,6 +40,8 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
     constexpr int VPL = TM * D;              // V planes: [256 keys][64 dims] (attn_vrow_off)
     constexpr int BK = 32, NC = 3 * D;       // K step; the head's q/k/v columns
     constexpr int S = 5;                                 // W ring stages
+    constexpr int KG = QA_KG;                            // ring stages retired per barrier
+    static_assert(S >= 2 * KG + 1 && KG >= 1, "ring");
     constexpr int BIMG = NC * BK, BSTG = 2 * BIMG;       // halves per W plane image / stage
     constexpr int NPB = 2 * NC / 16;                     // 1-KiB DMA pieces per stage: 24
     constexpr int QLD = D + 4;                           // q image row (floats)
@@ -128,12 +134,11 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
     // conversion temporaries need the registers of the third slot: two steps ahead spilled)
     constexpr int PA = LN ? 1 : 2;
     bf16x8 a[PA + 1][2];
-    // W(0) .. W(S-2) and A(0), A(1) ahead; per K step kt: W(kt + S - 1), A(kt + 2).  The wait before step kt's
-    // barrier counts only the DMA pieces certainly behind W(kt) -- those of W(kt + 1) .. W(kt + S - 2), 2 per wave
-    // each: the compiler keeps the DMA issues in order against the waits but places the A register loads freely
-    // (and inserts their waits itself), see gemm_rows.h rows_dma_after
+    // W(0) .. W(S - KG - 1) and A(0) .. A(PA - 1) ahead; per K step kt: A(kt + PA); per group of KG steps the W refills
+    // (below).  The compiler keeps the DMA issues in order against the waits but places the A register loads freely
+    // (and inserts their waits itself), so the ring waits count DMA pieces only (gemm_rows.h rows_dma_after)
 #pragma unroll
-    for (int k = 0; k < S - 1; ++k)
+    for (int k = 0; k < S - KG; ++k)
         if (k < KT) issueB(k);
 #pragma unroll
     for (int k = 0; k < PA; ++k)
@@ -202,14 +207,12 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
             a[1] = __builtin_bit_cast(bf16x8, lo);
         }
     };
-    // one K step with the A fragments in `a`; refills go to `an` (the step two ahead)
+    // one K step with the A fragments in `a`; refills go to `an` (the step PA ahead).  The W ring is retired KG
+    // stages per barrier: before group kt0's barrier every wave waits for its pieces of W(kt0 .. kt0 + KG - 1) (the
+    // DMA pieces certainly behind them: W(kt0 + KG .. kt0 + S - KG - 1), 2 per wave each), after it refills the KG
+    // slots the previous group freed
     auto step = [&](int kt, bf16x8 (&a)[2], bf16x8 (&an)[2]) __attribute__((always_inline)) {
-        vm_wait(rows_dma_after<S, KT, 2>(kt));
-        __builtin_amdgcn_s_barrier();  // every wave's W pieces of stage kt landed; stage kt - 1 is free
-        if (!(QA_DIAG & 2)) {
-            if (kt + S - 1 < KT) issueB(kt + S - 1);
-            if (kt + PA < KT) loadA(kt + PA, an);
-        }
+        if (!(QA_DIAG & 2) && kt + PA < KT) loadA(kt + PA, an);
         operand(kt, a);
         const __bf16* Bs = reinterpret_cast<const __bf16*>(lds + (kt % S) * BSTG);
 #pragma unroll
@@ -228,8 +231,27 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
             if (LN && (j & 3) == 3) asm volatile("" ::: "memory");
         }
     };
+    auto dma_after_group = [&](int kt0) {
+        int n = 0;
+        for (int w = kt0 + KG; w <= kt0 + S - KG - 1; ++w) n += w < KT ? 2 : 0;
+        return n;
+    };
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) step(kt, a[kt % (PA + 1)], a[(kt + PA) % (PA + 1)]);
+    for (int kt0 = 0; kt0 < KT; kt0 += KG) {
+        vm_wait(dma_after_group(kt0));
+        __builtin_amdgcn_s_barrier();  // every wave's W pieces of stages kt0 .. kt0 + KG - 1 landed; the previous
+                                       // group's slots are free
+        if (!(QA_DIAG & 2)) {
+#pragma unroll
+            for (int i = 0; i < KG; ++i)
+                if (kt0 + S - KG + i < KT) issueB(kt0 + S - KG + i);
+        }
+#pragma unroll
+        for (int i = 0; i < KG; ++i) {
+            const int kt = kt0 + i;
+            if (kt < KT) step(kt, a[kt % (PA + 1)], a[(kt + PA) % (PA + 1)]);
+        }
+    }
     __syncthreads();  // every wave is done with the ring
     if (LN && h == 0) amax_commit(p.ln_amax, lnmx);  // (the item's 8 head workgroups form the same LayerNorm)
 
