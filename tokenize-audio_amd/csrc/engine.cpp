@@ -355,6 +355,10 @@ struct mimi_engine {
     // transformer GEMMs with sc1 output stores (gemm_planes.h FL_SC1OUT; mimi_set_option "sc1_out"): bit 0 q/k/v,
     // bit 1 fc1, bit 2 o_proj and fc2 (large batches; the same bits either way)
     int sc1_out = 2;  // (A/B, round 4: fc1 0.594 -> 0.576 ms per B = 32 step; q/k/v, o_proj and fc2 slower with it)
+    // fc1's tile order in XCD column groups (GemmArgs::ncg, gemm_planes.h; mimi_set_option "fc1_cg": 0 / 1 none, 2, 4;
+    // same bits): each XCD re-serves 1 / fc1_cg of W1 from its L2.  (A/B r4y: 2 groups cut fc1's fetch 85 -> 54 MB per
+    // launch but not its time, 0.59-0.60 vs 0.61-0.62 ms per step; profiles/r4y_ab_fc1_cg.txt)
+    int fc1_cg = 1;
     struct Tap {
         float* d = nullptr;
         size_t cap = 0;
@@ -1731,6 +1735,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         }
         a1.sc1 = (e->sc1_out & 2) != 0;
         a1.rows_form = (e->gemm_rows & 1) != 0;
+        a1.ncg = e->fc1_cg;
         LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, prec), "fc1");
         rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
         if ((rc = save_tap_planes(e, nmf("ff%d", l).c_str(), w.ff, ns, tapB, tapT, c.intermediate_size, s, ffa.scale)))
@@ -2444,6 +2449,7 @@ static const EngineOption kEngineOptions[] = {
     {"oproj_ln", &mimi_engine::oproj_ln, 0x3u, "0 or 1"},
     {"gemm_rows", &mimi_engine::gemm_rows, 0xffu, "0..7"},
     {"res_rows", &mimi_engine::res_rows, 0x3u, "0 or 1"},
+    {"fc1_cg", &mimi_engine::fc1_cg, 0x17u, "0, 1, 2 or 4"},
 };
 
 extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {

@@ -190,11 +190,22 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     }
     float omx = 0.0f;  // max|planes value| (fp16 planes: the engine's range check), over this workgroup's tiles
     const int KT = K / BK / NB;
-    // tile -> (item, M tile, N tile)
+    // tile -> (item, M tile, N tile).  p.ncg > 1 (XCD column groups): the logical order is column group outermost, so
+    // the XCD-contiguous runs of xcd_remap cover 8 / ncg of the M tiles x N / ncg of the N tiles each -- an XCD's L2
+    // then re-serves 1 / ncg of W to all its M tiles instead of streaming all of W past its 4 MB once per M-tile wave
+    const int ncg = (p.ncg > 1 && NTn % p.ncg == 0) ? p.ncg : 1;
     auto decode = [&](int tile, int& b, int& mt, int& nt) {
         const int logical = xcd_remap(tile, ntiles);
-        nt = logical % NTn;
-        int rest = logical / NTn;
+        int rest;
+        if (ncg > 1) {
+            const int NG = NTn / ncg, per = ntiles / ncg;
+            const int cg = logical / per, w = logical - cg * per;
+            nt = cg * NG + w % NG;
+            rest = w / NG;
+        } else {
+            nt = logical % NTn;
+            rest = logical / NTn;
+        }
         if constexpr (RG) {
             b = 0;
             for (; b < p.batch - 1; ++b) {

@@ -232,6 +232,8 @@ struct GemmArgs {
     int ln_tile;  // host-side hint: the q/k/v LayerNorm-prologue tile on small grids (0 16x64, 1 32x64, 2 16x128)
     int rows_form;  // host-side hint: 1 = the row-slab kernel (gemm_rows.h) where the role has one (fc1 / fc2 / o_proj,
                     // large grids, f16x3; engine option gemm_rows; the same bits either way)
+    int ncg;  // planes kernels: XCD column groups of the tile order (0 / 1 none; must divide the N tiles, else none;
+              // engine option fc1_cg; which workgroup computes a tile only, the same bits either way)
 };
 // true when launch_gemm(role, a, precision) runs a tile with the LayerNorm prologue (a.ln_* then feed A)
 bool gemm_ln_prologue_ok(int role, const GemmArgs& a, int precision);
