@@ -179,7 +179,8 @@ int64_t mimi_graph_replays(const mimi_engine* e);
  * small grids, default 1), "rvq_xcd" 0/1.  "sc1_out" 0-7 (sc1 output stores: bit 0 q/k/v, 1 fc1 (default 2),
  * 2 o_proj + fc2), "ln_rpw" 0/1/2/4/8 (LayerNorm rows per wave), "gemm_rows" 0-7 (row-slab GEMM for fc1 / fc2 /
  * o_proj, default 0), "res_rows" 0/1 (stage-2 residual block as one kernel, default 0), "fc1_cg" 0/1/2/4 (fc1's
- * tile order in XCD column groups, default 1 = none).  Unknown keys and values:
+ * tile order in XCD column groups, default 1 = none), "res1_form" 0/1 (stage-1 block as one 8-wave or two 4-wave
+ * workgroups per CU, default 1).  Unknown keys and values:
  * MIMI_ERR_INVALID_ARGUMENT.  A change drops the captured graphs. */
 int mimi_set_option(mimi_engine* e, const char* key, int64_t value);
 /* MIMI_PRECISION_F16X3 diagnostics: per plane tensor (64-char names), its fixed activation scale and the max|x|

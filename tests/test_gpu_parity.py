@@ -96,12 +96,13 @@ def test_quantizer_forms_bit_exact(engine, golden, form):
 def test_kernel_options_identical_codes(engine):
     """Kernel-variant options change no bit: sc1 output stores on the transformer GEMMs (sc1_out, large-batch tiles),
     the row-slab GEMMs (gemm_rows), the fused q/k/v + attention (qkv_attn; B = 16 is below its automatic threshold,
-    2 forces it), fc1's XCD column groups (fc1_cg) and every RVQ form, on a B = 16 x 10 s batch at K = 32."""
+    2 forces it), fc1's XCD column groups (fc1_cg), the stage-1 block's
+    workgroup form (res1_form) and every RVQ form, on a B = 16 x 10 s batch at K = 32."""
     x = torch.from_numpy(synthetic.clip_batch(16, 240000, seed=88))[:, None].cuda()
     base = engine.encode(x, num_quantizers=32).audio_codes.cpu()
     defaults = {"sc1_out": 2, "rvq_form": 0, "rvq_chain": 1, "rvq_xcd": 1, "gemm_rows": 0, "qkv_attn": 1, "res_rows": 0, "oproj_ln": 0,
-                "fc1_cg": 1}
-    cases = [("fc1_cg", 2), ("fc1_cg", 4), ("sc1_out", 0), ("sc1_out", 7), ("rvq_chain", 0), ("rvq_xcd", 0), ("gemm_rows", 7), ("qkv_attn", 0), ("res_rows", 1), ("oproj_ln", 1),
+                "fc1_cg": 1, "res1_form": 1}
+    cases = [("res1_form", 0), ("fc1_cg", 2), ("fc1_cg", 4), ("sc1_out", 0), ("sc1_out", 7), ("rvq_chain", 0), ("rvq_xcd", 0), ("gemm_rows", 7), ("qkv_attn", 0), ("res_rows", 1), ("oproj_ln", 1),
              ("qkv_attn", 2)] + [("rvq_form", f) for f in range(1, 7)]
     for key, val in cases:
         engine.set_option(key, val)

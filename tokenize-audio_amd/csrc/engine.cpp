@@ -359,6 +359,10 @@ struct mimi_engine {
     // same bits): each XCD re-serves 1 / fc1_cg of W1 from its L2.  (A/B r4y: 2 groups cut fc1's fetch 85 -> 54 MB per
     // launch but not its time, 0.59-0.60 vs 0.61-0.62 ms per step; profiles/r4y_ab_fc1_cg.txt)
     int fc1_cg = 1;
+    // stage-1 fp16 block form (resblock.hip resblock128_h16_kernel; mimi_set_option "res1_form"; same bits): 0 one
+    // 8-wave workgroup per CU, 1 two 4-wave workgroups per CU (each wave both 16-step tiles of its M tile; their block
+    // chains interleave on the SIMDs: 0.59 -> 0.555 ms per B = 32 step, profiles/r4aa_ab_res1_form.txt)
+    int res1_form = 1;
     struct Tap {
         float* d = nullptr;
         size_t cap = 0;
@@ -1417,6 +1421,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                 ra.unscale2 = 1.0f / (ha.scale * e->res1_wsc[1]);
                 ra.xamax = xa.amax;
                 ra.hamax = ha.amax;
+                ra.form = e->res1_form;
             }
             if (rg && !(h16 && (si == 0 || si == 1))) return set_err(MIMI_ERR_UNSUPPORTED, "ragged: fp16 blocks only");
             const double H = C / c.compress;
@@ -2450,6 +2455,7 @@ static const EngineOption kEngineOptions[] = {
     {"gemm_rows", &mimi_engine::gemm_rows, 0xffu, "0..7"},
     {"res_rows", &mimi_engine::res_rows, 0x3u, "0 or 1"},
     {"fc1_cg", &mimi_engine::fc1_cg, 0x17u, "0, 1, 2 or 4"},
+    {"res1_form", &mimi_engine::res1_form, 0x3u, "0 or 1"},
 };
 
 extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {

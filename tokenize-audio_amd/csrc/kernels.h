@@ -306,6 +306,9 @@ struct ResArgs {
     float unscale_d;
     float* xout;
     long long T1;
+    // stage 1 fp16 block (resblock128_h16_kernel): 0 = one 8-wave workgroup per CU, 1 = two 4-wave workgroups per CU
+    // (engine option res1_form; which wave computes a tile only, the same bits)
+    int form;
 };
 hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** kname);
 // stage 0 + down conv 0 in one kernel (PREC_F16X3)

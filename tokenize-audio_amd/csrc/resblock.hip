@@ -781,8 +781,14 @@ __device__ __forceinline__ int r1h_swz(int row, int ld, int ch) {
     return row * ld + 8 * ((ch >> 3) ^ ((row >> 2) & 1)) + (ch & 7);
 }
 
-__global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
+// NN = 1: one workgroup of 8 waves per CU, wave w the 16-step N tile w & 1 of M tile w >> 1.  NN = 2: two
+// workgroups of 4 waves per CU, wave w both N tiles of M tile w (the W3 fragments it holds serve both), so the two
+// workgroups' block chains (barriers, VALU epilogues, MFMA phases) interleave on every SIMD instead of running in
+// lockstep; each output element sees the same MFMA sequence and epilogue arithmetic either way (the same bits).
+template <int NN>
+__global__ __launch_bounds__(512 / NN) __attribute__((amdgpu_waves_per_eu(NN))) void resblock128_h16_kernel(ResArgs p) {
     using namespace r1h;
+    constexpr int NWW = NW / NN;  // waves per workgroup
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -792,7 +798,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
     {
         const uint4* src = reinterpret_cast<const uint4*>(p.wh16) + FR_W1 * 64;  // W1's fragments
         uint4* dst = reinterpret_cast<uint4*>(lds);
-        for (int i = tid; i < LFRAG * 64; i += NW * 64) dst[i] = src[i];
+        for (int i = tid; i < LFRAG * 64; i += NWW * 64) dst[i] = src[i];
         if (tid < H) bl[tid] = p.b3[tid];
         if (tid < C) bl[H + tid] = p.b1[tid];
     }
@@ -806,8 +812,9 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
     static_assert(BM == 32, "TileWalk steps 32");
     TileWalk tw(p, tpi, g0);
     const int li = lane & 15, lq = lane >> 4;
-    const int n = wave & 1, mp = wave >> 1;  // N-tile (16 steps), M-tile pair
-    const int t = 16 * n + li;                // this lane's step inside a block (E layout)
+    const int n0 = NN == 1 ? (wave & 1) : 0;    // this wave's first N tile (16 steps)
+    const int mp = NN == 1 ? wave >> 1 : wave;  // its M tile (GEMM1) / M-tile pair (GEMM2)
+    auto tof = [&](int nn) { return 16 * (n0 + nn) + li; };  // this lane's step inside a block (E layout), tile nn
     const float sx = p.xscale, sh = p.hscale, sy = p.yscale;
     const float u1 = p.unscale1, u2 = p.unscale2;
     float mxx = 0.0f, mxh = 0.0f, mxy = 0.0f;
@@ -852,33 +859,47 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
         }
     };
 
-    uint2 hhi[2], hlo[2];  // lanes with t >= 30: the halo planes for the next block
-    f32x4 xn[2];
-    if (g0 < g1) xload(tw.b, tw.Tb, tw.t0, t, xn);
+    uint2 hhi[2], hlo[2];  // lanes with t >= 30 (the last N tile): the halo planes for the next block
+    f32x4 xn[NN][2];
+    if (g0 < g1) {
+#pragma unroll
+        for (int nn = 0; nn < NN; ++nn) xload(tw.b, tw.Tb, tw.t0, tof(nn), xn[nn]);
+    }
     __syncthreads();  // weights and biases resident
     for (unsigned g = g0; g < g1; ++g) {
         const unsigned b = tw.b;
         const long long t0 = tw.t0;
         const long long Tb = tw.Tb;
-        f32x4 xc[2] = {xn[0], xn[1]};
+        f32x4 xc[NN][2];
+#pragma unroll
+        for (int nn = 0; nn < NN; ++nn) {
+            xc[nn][0] = xn[nn][0];
+            xc[nn][1] = xn[nn][1];
+        }
         tw.next();
-        if (g + 1 < g1) xload(tw.b, tw.Tb, tw.t0, t, xn);  // flies under this block
+        if (g + 1 < g1) {  // flies under this block
+#pragma unroll
+            for (int nn = 0; nn < NN; ++nn) xload(tw.b, tw.Tb, tw.t0, tof(nn), xn[nn]);
+        }
         // ---- slab: halo rows 0, 1 (lanes t = 30, 31), rows 2 + t
-        if (t >= BM - 2) {
+        const int tl = tof(NN - 1);  // the last tile's step (the halo lanes live there)
+        if (tl >= BM - 2) {
             if (t0 == 0) {
                 hhi[0] = hhi[1] = hlo[0] = hlo[1] = make_uint2(0u, 0u);
             } else if (g == g0) {
                 f32x4 xh[2];
-                xload(b, Tb, t0, t - BM, xh);  // steps t0 - 2, t0 - 1
+                xload(b, Tb, t0, tl - BM, xh);  // steps t0 - 2, t0 - 1
                 xsplit(xh, hhi, hlo);
             }
-            slab_row_put(t - (BM - 2), hhi, hlo);
+            slab_row_put(tl - (BM - 2), hhi, hlo);
         }
-        {
+#pragma unroll
+        for (int nn = 0; nn < NN; ++nn) {
+            const int t = tof(nn);
             uint2 hi[2], lo[2];
-            xsplit(xc, hi, lo);
+            xsplit(xc[nn], hi, lo);
             slab_row_put(2 + t, hi, lo);
-            if (t >= BM - 2) {
+            if (nn == NN - 1 && t >= BM - 2) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     hhi[i] = hi[i];
@@ -889,49 +910,64 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
         lds_barrier();  // B1: slab complete
 
         // ---- GEMM1: tile (hch 16 mp, steps 16 n); k = 32 ks + 8 lq + e -> tap ks / 4, channel 32 (ks % 4) + 8 lq + e
-        f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+        f32x4 acc1[NN];
+#pragma unroll
+        for (int nn = 0; nn < NN; ++nn) acc1[nn] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 12; ++ks) {
-            const int o = r1h_swz(16 * n + li + (ks >> 2), SLD, (ks & 3) * 32 + 8 * lq);
-            const f16x8 bx0 = *reinterpret_cast<const f16x8*>(slab + o);
-            const f16x8 bx1 = *reinterpret_cast<const f16x8*>(slab + SPL + o);
-            acc1 = mfma_h16(w3r[ks][1], bx0, acc1);
-            acc1 = mfma_h16(w3r[ks][0], bx1, acc1);
-            acc1 = mfma_h16(w3r[ks][0], bx0, acc1);
+#pragma unroll
+            for (int nn = 0; nn < NN; ++nn) {
+                const int o = r1h_swz(16 * (n0 + nn) + li + (ks >> 2), SLD, (ks & 3) * 32 + 8 * lq);
+                const f16x8 bx0 = *reinterpret_cast<const f16x8*>(slab + o);
+                const f16x8 bx1 = *reinterpret_cast<const f16x8*>(slab + SPL + o);
+                acc1[nn] = mfma_h16(w3r[ks][1], bx0, acc1[nn]);
+                acc1[nn] = mfma_h16(w3r[ks][0], bx1, acc1[nn]);
+                acc1[nn] = mfma_h16(w3r[ks][0], bx0, acc1[nn]);
+            }
         }
         {  // h = ELU(acc + b3): step t, hch 16 mp + 4 lq .. +3
             const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 16 * mp + 4 * lq);
-            float z[4], tt[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) z[q] = __builtin_fmaf(acc1[q], u1, bb[q]);
-            elu_s4(z, sh, tt, mxh);
-            uint2 hi, lo;
-            split4_t(tt, hi, lo);
-            const int o = r1h_swz(t, HLD, 16 * mp + 4 * lq);
-            *reinterpret_cast<uint2*>(hb + o) = hi;
-            *reinterpret_cast<uint2*>(hb + HPL + o) = lo;
+            for (int nn = 0; nn < NN; ++nn) {
+                float z[4], tt[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) z[q] = __builtin_fmaf(acc1[nn][q], u1, bb[q]);
+                elu_s4(z, sh, tt, mxh);
+                uint2 hi, lo;
+                split4_t(tt, hi, lo);
+                const int o = r1h_swz(tof(nn), HLD, 16 * mp + 4 * lq);
+                *reinterpret_cast<uint2*>(hb + o) = hi;
+                *reinterpret_cast<uint2*>(hb + HPL + o) = lo;
+            }
         }
         lds_barrier();  // B2: h complete, every wave done reading the slab
 
         // ---- GEMM2: tiles (channels 16 (2 mp + i), steps 16 n), K = 64
-        f32x4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+        f32x4 acc2[NN][2];
+#pragma unroll
+        for (int nn = 0; nn < NN; ++nn) acc2[nn][0] = acc2[nn][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            const int o = r1h_swz(16 * n + li, HLD, ks * 32 + 8 * lq);
-            const f16x8 bh0 = *reinterpret_cast<const f16x8*>(hb + o);
-            const f16x8 bh1 = *reinterpret_cast<const f16x8*>(hb + HPL + o);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int m = 2 * mp + i;
-                const f16x8 aw0 = wf[(FR_W1 + (m * 2 + ks) * 2) * 64 + lane];
-                const f16x8 aw1 = wf[(FR_W1 + (m * 2 + ks) * 2 + 1) * 64 + lane];
-                acc2[i] = mfma_h16(aw1, bh0, acc2[i]);
-                acc2[i] = mfma_h16(aw0, bh1, acc2[i]);
-                acc2[i] = mfma_h16(aw0, bh0, acc2[i]);
+            for (int nn = 0; nn < NN; ++nn) {
+                const int o = r1h_swz(16 * (n0 + nn) + li, HLD, ks * 32 + 8 * lq);
+                const f16x8 bh0 = *reinterpret_cast<const f16x8*>(hb + o);
+                const f16x8 bh1 = *reinterpret_cast<const f16x8*>(hb + HPL + o);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int m = 2 * mp + i;
+                    const f16x8 aw0 = wf[(FR_W1 + (m * 2 + ks) * 2) * 64 + lane];
+                    const f16x8 aw1 = wf[(FR_W1 + (m * 2 + ks) * 2 + 1) * 64 + lane];
+                    acc2[nn][i] = mfma_h16(aw1, bh0, acc2[nn][i]);
+                    acc2[nn][i] = mfma_h16(aw0, bh1, acc2[nn][i]);
+                    acc2[nn][i] = mfma_h16(aw0, bh0, acc2[nn][i]);
+                }
             }
         }
         // ---- y = ELU(x + (acc + b1)) -> planes, staged over slab rows 2..33
-        {
+#pragma unroll
+        for (int nn = 0; nn < NN; ++nn) {
+            const int t = tof(nn);
             float tmy = 0.0f;
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
@@ -939,7 +975,7 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
                 const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + H + ch);
                 float z[4], tt[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) z[q] = xc[i][q] + __builtin_fmaf(acc2[i][q], u2, bb[q]);
+                for (int q = 0; q < 4; ++q) z[q] = xc[nn][i][q] + __builtin_fmaf(acc2[nn][i][q], u2, bb[q]);
                 elu_s4(z, sy, tt, tmy);
                 uint2 hi, lo;
                 split4_t(tt, hi, lo);
@@ -950,10 +986,10 @@ __global__ __launch_bounds__(512) void resblock128_h16_kernel(ResArgs p) {
             if (t0 + t < Tb) mxy = fmaxf(mxy, tmy);  // steps past the end are not stored, not in max|y|
         }
         lds_barrier();  // B3: staging complete
-        {  // 2 planes x 32 rows x 16 chunks of 16 B = 1024 chunks, 2 per thread
+        {  // 2 planes x 32 rows x 16 chunks of 16 B = 1024 chunks, 2 NN per thread
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int idx = tid + k * NW * 64;
+            for (int k = 0; k < 2 * NN; ++k) {
+                const int idx = tid + k * NWW * 64;
                 const int pl = idx >> 9, r = (idx >> 4) & 31, c = (idx & 15) * 8;
                 const uint4 v = *reinterpret_cast<const uint4*>(slab + pl * SPL + r1h_swz(2 + r, SLD, c));
                 if (t0 + r < Tb)
@@ -1008,13 +1044,21 @@ hipError_t launch_resblock(int C, const ResArgs& a, hipStream_t s, const char** 
             return run_res<64, 128, true, false, 4, 1, 4, 1, 64>(a, s, kname);
         case 128:
             if (a.wh16) {
-                static const char* nm = "mimi::resblock128_h16_kernel(mimi::ResArgs)";
-                if (kname) *kname = nm;
-                // persistent: one workgroup (8 waves, 157.9 KB of LDS) per CU, each a range of 32-step blocks
+                // persistent: one workgroup of 8 waves (form 0) or two of 4 waves (form 1) per CU, each workgroup a
+                // range of 32-step blocks (62.6 KB of LDS per workgroup)
                 int dev = 0, ncu = 256;
                 (void)hipGetDevice(&dev);
                 (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-                hipLaunchKernelGGL(resblock128_h16_kernel, dim3((unsigned)ncu), dim3(64 * r1h::NW), 0, s, a);
+                if (a.form == 1) {
+                    static const char* nm2 = "mimi::resblock128_h16_kernel<2>(mimi::ResArgs)";
+                    if (kname) *kname = nm2;
+                    hipLaunchKernelGGL(resblock128_h16_kernel<2>, dim3((unsigned)(2 * ncu)), dim3(64 * r1h::NW / 2), 0,
+                                       s, a);
+                    return hipGetLastError();
+                }
+                static const char* nm = "mimi::resblock128_h16_kernel<1>(mimi::ResArgs)";
+                if (kname) *kname = nm;
+                hipLaunchKernelGGL(resblock128_h16_kernel<1>, dim3((unsigned)ncu), dim3(64 * r1h::NW), 0, s, a);
                 return hipGetLastError();
             }
             return run_res<128, 64, true, false, 2, 2, 2, 2, 128>(a, s, kname);
