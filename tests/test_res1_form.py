@@ -51,7 +51,7 @@ def test_res1_form_ragged_bitwise(engine):
         try:
             got.append(engine.encode_ragged(xt, lengths, 32).cpu().numpy())
         finally:
-            engine.set_option("res1_form", 0)
+            engine.set_option("res1_form", 1)
     assert np.array_equal(got[0], got[1]), int((got[0] != got[1]).sum())
 
 
