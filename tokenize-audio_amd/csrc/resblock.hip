@@ -733,11 +733,11 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
 
 
 // ------------------------------------------------------------------------------------------------
-// Stage 1 (C = 128, H = 64) on the fp16 matrix cores (PREC_F16X3): residual block + ELU, persistent, one
-// workgroup of 8 waves per CU walking a contiguous range of 32-step blocks.  Both weight images stay resident
-// in LDS (W3 96 KB + W1 32 KB, 16x16x32 A fragments); per block:
-// W3 (96 KB) is register-resident instead: each wave holds the 24 fragments of its M tile (96 VGPRs, loaded once), so
-// GEMM1 reads only the slab from LDS -- with W3 in LDS every block re-read 192 KB of fragments per CU.
+// Stage 1 (C = 128, H = 64) on the fp16 matrix cores (PREC_F16X3): residual block + ELU, persistent, workgroups
+// walking contiguous ranges of 32-step blocks -- one of 8 waves per CU, or (the default) two of 4 waves per CU
+// (template NN below).  W1 (32 KB of 16x16x32 A fragments) is resident in LDS; W3 (96 KB) is register-resident: each
+// wave holds the 24 fragments of its M tile (96 VGPRs, loaded once), so GEMM1 reads only the slab from LDS -- with W3
+// in LDS every block re-read 192 KB of fragments per CU.  Per block (the 8-wave form's wave roles shown):
 //   load    x[t0 .. t0+31][128] fp32, each lane 2 float4 in the GEMM2 output layout (time t = 16n + lane&15,
 //           channels 16m + 4(lane>>4) .. +3) -- they stay in registers as the identity skip; the next block's
 //           x is prefetched under this one
@@ -750,7 +750,8 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
 //   out     y = ELU(x + (acc + b1)) -> planes staged over slab rows 2..33                     barrier
 //           -> 1-KB row stores (256-B rows, 4 per wave instruction)                           barrier
 // Slab rows are 288 B (72 dwords = 8 mod 64) and h rows 160 B, 16-B chunks XOR-swizzled by row (r1h_swz): the
-// 16x16x32 fragment reads (row lane&15, 16-B chunk lane>>4) are conflict-free, the row writes 2-way.  LDS: 128 KB weights + 19.1 KB slab + 10 KB h + biases = 157.9 KB.
+// 16x16x32 fragment reads (row lane&15, 16-B chunk lane>>4) are conflict-free, the row writes 2-way.  LDS per
+// workgroup: 32 KB W1 + 19.1 KB slab + 10 KB h + biases (+ the compiler's own): 69 KB.
 // ------------------------------------------------------------------------------------------------
 namespace r1h {
 constexpr int C = 128, H = 64, BM = 32, NW = 8;
