@@ -136,7 +136,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     static_assert(MF == 32 || MF == 16, "MFMA shape");
     static_assert(TM >= 1 && TN >= 1 && KSUB >= 1, "tile");
     static_assert(NS * BM % RPP == 0 && NS * BN % RPP == 0, "whole pieces");
-    static_assert(STAGES >= 2 * KG && STAGES <= 8, "stages");
+    static_assert(STAGES >= 2 * KG && STAGES <= 16, "stages");
     static_assert(PMAX * (STAGES - 2 * KG) <= 63, "vmcnt range");
     static_assert(EPI != EPI_ROPE || (MF == 32 ? TN % 2 == 0 : TN % 4 == 0), "rope pairs (d, d+32) in one lane");
     static_assert(!F16 || NS == 2, "fp16 planes: 2 planes, 3 products");

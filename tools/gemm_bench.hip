@@ -196,6 +196,14 @@ int main(int argc, char** argv) {
         {"B1 16x32 1w+2ld s8", launch_pl<16, 32, 1, 1, 2, 8, 2, 32, 16, 0, true>, 32, 12},
         {"B1 16x32 1w+4ld s6 KG2", launch_pl<16, 32, 1, 1, 2, 6, 4, 32, 16, FL_KG2, true>, 32, 12},
         {"B1 64x64 4w+4ld s8", launch_pl<64, 64, 2, 2, 2, 8, 4, 32, 16, 0, true>, 32, 12},
+        // deeper rings (round 4, late): more bytes in flight per CU for the latency-bound small grids
+        {"B1 16x32 1w+4ld s12 KG2", launch_pl<16, 32, 1, 1, 2, 12, 4, 32, 16, FL_KG2, true>, 32, 12},
+        {"B1 16x32 1w+4ld s16 KG4", launch_pl<16, 32, 1, 1, 2, 16, 4, 32, 16, FL_KG4, true>, 32, 12},
+        {"B1 16x32 1w+4ld s16 KG2", launch_pl<16, 32, 1, 1, 2, 16, 4, 32, 16, FL_KG2, true>, 32, 12},
+        {"B1 16x64 1w+4ld s12 KG2", launch_pl<16, 64, 1, 1, 2, 12, 4, 32, 16, FL_KG2, true>, 32, 12},
+        {"B1 16x64 1w+4ld s16 KG4", launch_pl<16, 64, 1, 1, 2, 16, 4, 32, 16, FL_KG4, true>, 32, 12},
+        {"B1 32x32 2w+4ld s12 KG2", launch_pl<32, 32, 2, 1, 2, 12, 4, 32, 16, FL_KG2, true>, 32, 12},
+        {"B1 16x32 1w+4ld s6 KG2 (fc2)", launch_pl<16, 32, 1, 1, 2, 6, 4, 32, 16, FL_KG2, true>, 32, 12},
         // interleaved-plane timing probe (FL_DIAG_ILV: 8 rows x 128 B pieces; results garbage)
         {"pair PERSIST 8w+4ld s2 ILV", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_ILV, true>, 64, 12, true},
         {"pair PERSIST DIAG nomma ILV", launch_pl<256, 128, 4, 2, 2, 2, 4, 32, 16, FL_PAIR | FL_PERSIST | FL_DIAG_NOMMA | FL_DIAG_ILV, true>, 64, 12, true},

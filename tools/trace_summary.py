@@ -24,3 +24,13 @@ for r in seg:
     agg[n][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
 for k, v in agg.items():
     print(f"{v[0]:3d} {v[1]:8.1f}  {k}")
+# gaps between consecutive dispatches of the step (idle GPU between one kernel's end and the next one's start)
+gaps = []
+for p, q in zip(seg, seg[1:]):
+    g = (int(q["Start_Timestamp"]) - int(p["End_Timestamp"])) / 1e3
+    gaps.append((g, p["Kernel_Name"].replace("void ", "")[:40], q["Kernel_Name"].replace("void ", "")[:40]))
+gs = sorted(g for g, _, _ in gaps)
+if gs:
+    print(f"gaps: {len(gs)}  sum {sum(gs):.1f} us  median {gs[len(gs) // 2]:.2f}  max {gs[-1]:.2f}")
+    for g, a_, b_ in sorted(gaps, reverse=True)[:8]:
+        print(f"  {g:6.2f} us  {a_} -> {b_}")
