@@ -53,6 +53,22 @@ def test_lib_exports_every_header_symbol():
     assert set(syms) == set(_lib.EXPORTED_SYMBOLS)
 
 
+def test_header_documents_every_engine_option():
+    """Every mimi_set_option key of the engine's table (engine.cpp kEngineOptions) is documented in the C header,
+    and the header names no key the engine would reject."""
+    src = open(os.path.join(ROOT, "tokenize-audio_amd", "csrc", "engine.cpp")).read()
+    table = src[src.index("kEngineOptions[] = {"):]
+    table = table[:table.index("};")]
+    keys = re.findall(r'\{"([a-z0-9_]+)", &mimi_engine::', table)
+    assert len(keys) >= 10, keys
+    hdr = open(os.path.join(ROOT, "include", "mimi_hip.h")).read()
+    doc = hdr[hdr.index("mimi_set_option") - 4000:hdr.index("int mimi_set_option(")]
+    for k in keys:
+        assert f'"{k}"' in doc, k
+    for k in re.findall(r'"([a-z0-9_]+)"', doc[doc.index("key"):]):
+        assert k in keys, k
+
+
 def test_lib_length_math_matches_python():
     from mimi_hip import _lib
     lib = _lib.load()
