@@ -292,7 +292,17 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         if (tiles(a, 32, 64) >= 256) return run_planes<32, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
         return run_planes<16, 64, 1, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
     }
-    if (prec == PREC_F16X3 && tiles(a, 128, 128) < kSmallGrid) {
+#ifndef MIMI_SMALL_ROLES
+#define MIMI_SMALL_ROLES 1
+#endif
+    // below one 128x128 workgroup per CU the small-grid tiles (the same MFMA sequence per output) run instead: the
+    // quantizer's GEMMs (downsample, input_proj: M = B x 125 rows, N = 512) leave half the CUs idle up to B = 63 on
+    // 128x128 tiles (0.079 + 0.025 -> 0.056 + 0.018 ms per B = 32 step, profiles/r4ak_ab_quantizer_tiles.txt)
+    const bool qsmall = tiles(a, 128, 128) < 256 &&
+                        (((MIMI_SMALL_ROLES & 1) && (role == ROLE_DOWNSAMPLE || role == ROLE_INPROJ)) ||
+                         ((MIMI_SMALL_ROLES & 2) && role == ROLE_OPROJ) || ((MIMI_SMALL_ROLES & 4) && role == ROLE_FC2) ||
+                         ((MIMI_SMALL_ROLES & 8) && role == ROLE_FINAL));
+    if (prec == PREC_F16X3 && (tiles(a, 128, 128) < kSmallGrid || qsmall)) {
         // <EPI, OUTP, TAG, 64-row BN, 32-row BM x BN / waves, 16-row BN / waves>; 16 x 16 wave tiles are too small for
         // the staged epilogue (64 lanes x 8 columns), and RoPE needs 64 columns per wave
         switch (role) {
