@@ -162,6 +162,9 @@ int mimi_get_precision(const mimi_engine* e);
 int mimi_calibrate(mimi_engine* e);
 /* MIMI_PRECISION_F16X3: encodes that took the overflow fallback so far (diagnostic). */
 int64_t mimi_f16_reruns(const mimi_engine* e);
+/* Encodes (and mimi_rvq_encode calls) re-run on the per-level RVQ kernels because a sweep of the persistent RVQ
+ * chain gave up waiting for a peer workgroup (its codes are never returned; diagnostic). */
+int64_t mimi_rvq_chain_reruns(const mimi_engine* e);
 /* hipGraph replay of MIMI_PRECISION_F16X3 encodes (default on): the second encode of a (batch, length, K) shape
  * captures the whole pass into a graph, later ones replay it (same kernels and arguments: identical codes).
  * Never used while profiling or taps are on.  enable = 0 drops the captured graphs.  Replays so far: */
@@ -172,15 +175,13 @@ int64_t mimi_graph_replays(const mimi_engine* e);
  * chip; default).  key "ln_fused": on small grids (batch 1-4) 0 = LayerNorm launches before q/k/v and fc1, 1 = fc1
  * computes the LayerNorm of its own rows (default), 2-4 = fc1 and q/k/v do (q/k/v tile variants).  key "qkv_attn":
  * q/k/v projection + RoPE + attention as one kernel for items of <= 256 frames, 0 = off, 1 = when the batch has
- * >= 256 (item, head) pairs (default), 2 = whenever the items fit; "qkv_attn_xcd" 0/1 its workgroup placement;
- * "qkv_attn_ln" 0/1 (that kernel forms the input LayerNorm itself, default 0).  "oproj_ln" 0/1 (o_proj + residual +
- * post-attention LayerNorm as one kernel on large grids, default 0).
+ * >= 256 (item, head) pairs (default), 2 = whenever the items fit; "qkv_attn_xcd" 0/1 its workgroup placement.
  * RVQ: "rvq_form" 0-6 (level-kernel form, 0 = default), "rvq_chain" 0/1 (one persistent launch for all levels on
- * small grids, default 1), "rvq_xcd" 0/1.  "sc1_out" 0-7 (sc1 output stores: bit 0 q/k/v, 1 fc1 (default 2),
- * 2 o_proj + fc2), "ln_rpw" 0/1/2/4/8 (LayerNorm rows per wave), "gemm_rows" 0-7 (row-slab GEMM for fc1 / fc2 /
- * o_proj, default 0), "res_rows" 0/1 (stage-2 residual block as one kernel, default 0), "fc1_cg" 0/1/2/4 (fc1's
- * tile order in XCD column groups, default 1 = none), "res1_form" 0/1 (stage-1 block as one 8-wave or two 4-wave
- * workgroups per CU, default 1).  Unknown keys and values:
+ * small grids, default 1; taken only where its give-up flag is read back: mimi_encode_wait re-runs an encode whose
+ * chain gave up), "rvq_chain_fault" 0/1/2 (tests only: 1 = zero spin budget, 2 = every sweep gives up), "rvq_xcd"
+ * 0/1.  "sc1_out" 0-7 (sc1 output stores: bit 0 q/k/v, 1 fc1 (default 2), 2 o_proj + fc2), "ln_rpw" 0/1/2/4/8
+ * (LayerNorm rows per wave), "fc1_cg" 0/1/2/4 (fc1's tile order in XCD column groups, default 1 = none), "res1_form"
+ * 0/1 (stage-1 block as one 8-wave or two 4-wave workgroups per CU, default 1).  Unknown keys and values:
  * MIMI_ERR_INVALID_ARGUMENT.  A change drops the captured graphs. */
 int mimi_set_option(mimi_engine* e, const char* key, int64_t value);
 /* MIMI_PRECISION_F16X3 diagnostics: per plane tensor (64-char names), its fixed activation scale and the max|x|

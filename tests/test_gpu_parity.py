@@ -15,6 +15,7 @@ import pytest
 import torch
 
 from audit import first_flip_margins, margin_audit, perturbation_near_tie
+from conftest import assert_codes_in_range
 from mimi_hip import synthetic
 from mimi_hip.config import encoded_length
 
@@ -95,14 +96,14 @@ def test_quantizer_forms_bit_exact(engine, golden, form):
 
 def test_kernel_options_identical_codes(engine):
     """Kernel-variant options change no bit: sc1 output stores on the transformer GEMMs (sc1_out, large-batch tiles),
-    the row-slab GEMMs (gemm_rows), the fused q/k/v + attention (qkv_attn; B = 16 is below its automatic threshold,
+    the fused q/k/v + attention (qkv_attn; B = 16 is below its automatic threshold,
     2 forces it), fc1's XCD column groups (fc1_cg), the stage-1 block's
     workgroup form (res1_form) and every RVQ form, on a B = 16 x 10 s batch at K = 32."""
     x = torch.from_numpy(synthetic.clip_batch(16, 240000, seed=88))[:, None].cuda()
     base = engine.encode(x, num_quantizers=32).audio_codes.cpu()
-    defaults = {"sc1_out": 2, "rvq_form": 0, "rvq_chain": 1, "rvq_xcd": 1, "gemm_rows": 0, "qkv_attn": 1, "res_rows": 0, "oproj_ln": 0,
+    defaults = {"sc1_out": 2, "rvq_form": 0, "rvq_chain": 1, "rvq_xcd": 1, "qkv_attn": 1,
                 "fc1_cg": 1, "res1_form": 1}
-    cases = [("res1_form", 0), ("fc1_cg", 2), ("fc1_cg", 4), ("sc1_out", 0), ("sc1_out", 7), ("rvq_chain", 0), ("rvq_xcd", 0), ("gemm_rows", 7), ("qkv_attn", 0), ("res_rows", 1), ("oproj_ln", 1),
+    cases = [("res1_form", 0), ("fc1_cg", 2), ("fc1_cg", 4), ("sc1_out", 0), ("sc1_out", 7), ("rvq_chain", 0), ("rvq_xcd", 0), ("qkv_attn", 0),
              ("qkv_attn", 2)] + [("rvq_form", f) for f in range(1, 7)]
     for key, val in cases:
         engine.set_option(key, val)
@@ -111,6 +112,49 @@ def test_kernel_options_identical_codes(engine):
         finally:
             engine.set_option(key, defaults[key])
         assert torch.equal(got, base), (key, val, int((got != base).sum()))
+
+
+@pytest.mark.parametrize("fault", [2, 1])
+def test_quantizer_chain_give_up_reruns(engine, golden, fault):
+    """The persistent RVQ chain never returns codes from a sweep that gave up waiting for a peer workgroup.  Fault 2
+    makes every sweep give up at once: every encode that took the chain must be re-run on the per-level kernels
+    (rvq_chain_reruns counts them) and return exactly the per-level codes -- through the eager pass, the hipGraph
+    replay (a shape's 3rd encode), the async ticket, a ragged batch and mimi_rvq_encode.  Fault 1 (a zero spin budget)
+    gives up or not depending on timing: the codes must be the same either way."""
+    arrays, _ = golden
+    x = torch.from_numpy(synthetic.speech_like(200000, 93, 0))[None].cuda()
+    lens = [48000, 30001, 1921]
+    xr = torch.from_numpy(np.stack([synthetic.speech_like(48000, 94, i) for i in range(3)])).cuda()
+    emb = torch.from_numpy(arrays["emb_speech10s"])[None].cuda()
+    engine.set_option("rvq_chain", 0)
+    try:
+        ref = engine.encode_int32(x, 32).cpu()
+        ref_r = engine.encode_ragged(xr, lens, 32).cpu()
+        ref_q = engine.quantize(emb, 32).cpu()
+        engine.set_option("rvq_chain", 1)
+        engine.set_option("rvq_chain_fault", fault)
+        r0 = engine.rvq_chain_reruns
+        for _ in range(3):  # eager, capture + replay, replay
+            got = engine.encode_int32(x, 32).cpu()
+            assert torch.equal(got, ref), int((got != ref).sum())
+            assert_codes_in_range(got)
+        got = engine.encode_async(x, 32).wait().cpu()
+        assert torch.equal(got, ref)
+        got_r = engine.encode_ragged(xr, lens, 32).cpu()
+        for i, n in enumerate(lens):
+            t = encoded_length(n)
+            assert torch.equal(got_r[i, :, :t], ref_r[i, :, :t]), i
+        assert torch.equal(engine.quantize(emb, 32).cpu(), ref_q)
+        assert np.array_equal(ref_q[0].numpy(), arrays["embcodes_speech10s"])
+        if fault == 2:
+            assert engine.rvq_chain_reruns - r0 == 6, engine.rvq_chain_reruns - r0
+    finally:
+        engine.set_option("rvq_chain_fault", 0)
+        engine.set_option("rvq_chain", 1)
+    # the chain itself, undisturbed again: no give-up on an idle GPU
+    r0 = engine.rvq_chain_reruns
+    assert torch.equal(engine.encode_int32(x, 32).cpu(), ref)
+    assert engine.rvq_chain_reruns == r0
 
 
 @pytest.mark.parametrize("chain", [0, 1])

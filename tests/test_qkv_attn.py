@@ -6,8 +6,7 @@ and its causal sliding-window attention (MimiAttention.forward) without the fp32
 fp32 q/k/v value is formed with the q/k/v GEMM's instruction sequence and the attention with
 attention_t256_h16_kernel's, so the q/k/v taps ("qkv0".."qkv7", written only when taps are on), the attention output
 planes ("att0".."att7"), the transformer output and all 32 codebooks must be equal BITWISE across the "qkv_attn"
-option (0: two kernels; 1: fused for large batches; 2: fused whenever the items fit), "qkv_attn_xcd" and
-"qkv_attn_ln" (the fused kernel forms the input LayerNorm itself, from the residual stream; opt-in, slower) -- on the
+option (0: two kernels; 1: fused for large batches; 2: fused whenever the items fit) and "qkv_attn_xcd" -- on the
 uniform B = 32 x 10 s headline batch, on small forced batches with partial 32-query tiles and a 1-frame item, on
 ragged batches, and through graph replays.  An item alone (batch 1: never fused) equals the same item inside a fused
 batch (test_full_size_batch_properties covers B = 1 vs B = 32; here a ragged case).
@@ -34,10 +33,9 @@ def engine(state_dict):
     m.set_option("qkv_attn_xcd", 1)
 
 
-def run(engine, variant, x, K=32, taps=True, xcd=1, ln=0):
+def run(engine, variant, x, K=32, taps=True, xcd=1):
     engine.set_option("qkv_attn", variant)
     engine.set_option("qkv_attn_xcd", xcd)
-    engine.set_option("qkv_attn_ln", ln)
     engine.set_taps(taps)
     try:
         codes = engine.encode_int32(x, K).cpu().numpy()
@@ -46,7 +44,6 @@ def run(engine, variant, x, K=32, taps=True, xcd=1, ln=0):
         engine.set_taps(False)
         engine.set_option("qkv_attn", 1)
         engine.set_option("qkv_attn_xcd", 1)
-        engine.set_option("qkv_attn_ln", 0)
 
 
 def same(a, b, what):
@@ -62,7 +59,6 @@ def test_fused_headline_batch_bitwise(engine):
     ref = run(engine, 0, x)
     same(ref, run(engine, 1, x), "auto")
     same(ref, run(engine, 1, x, xcd=0), "xcd 0")
-    same(ref, run(engine, 1, x, ln=1), "LayerNorm in the kernel")
     assert ref[0].shape == (32, 32, 125)
 
 
@@ -73,7 +69,6 @@ def test_fused_forced_small_batches_bitwise(engine, B, L):
     ref = run(engine, 0, x)
     got = run(engine, 2, x)
     same(ref, got, (B, L))
-    same(ref, run(engine, 2, x, ln=1), (B, L, "LayerNorm in the kernel"))
     assert got[0].shape == (B, 32, encoded_length(L))
 
 

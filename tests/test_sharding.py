@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
+from conftest import assert_codes_in_range
 from mimi_hip import sharding
 
 
@@ -140,4 +141,5 @@ def test_sharded_real_engines_match_single(tmp_path):
     model.close()
     with np.load(out, allow_pickle=False) as z:
         for i in range(len(audio)):
+            assert_codes_in_range(z[f"c{i}"])
             assert np.array_equal(z[f"c{i}"], exp[i]), i

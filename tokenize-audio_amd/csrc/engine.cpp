@@ -288,6 +288,8 @@ struct mimi_engine {
         std::vector<int64_t> lens;
         int* rg_pinned = nullptr;     // pinned image of its RaggedTable (read by the encode's async upload)
         size_t rg_cap = 0;
+        bool chain = false;           // the encode ran the persistent RVQ chain: chain_word holds its give-up flag
+        unsigned* chain_word = nullptr;  // pinned, copied from the chain's flag behind the encode
     };
     static constexpr int kMaxPending = 16;
     Pending pend[kMaxPending];
@@ -311,6 +313,7 @@ struct mimi_engine {
         hipGraph_t g = nullptr;
         hipGraphExec_t x = nullptr;
         uint64_t used = 0;
+        unsigned* chain_flag = nullptr;  // the captured RVQ chain's give-up flag (null: no chain in the graph)
     };
     static constexpr int kMaxGraphs = 8;
     std::vector<Graph> graphs;
@@ -333,25 +336,17 @@ struct mimi_engine {
     int ln_rpw = 1;  // LayerNorm rows per wave (mimi_set_option "ln_rpw": 1 (A/B r4h: 0.186 vs 0.200 ms per B = 32 step for 2), 2, 4, 8; the same bits)
     int rvq_xcd = 1;  // large grids: a frame tile's RVQ slices on one XCD (mimi_set_option "rvq_xcd"; same bits)
     int rvq_chain = 1;  // small grids: the persistent all-levels RVQ (mimi_set_option "rvq_chain"; RvqArgs::chain)
+    // The chain is taken only where its give-up flag is read back (chain_ok: the main encode path, whose ticket carries
+    // the flag to mimi_encode_wait, and mimi_rvq_encode, which checks it itself); every fallback and internal pass runs
+    // the per-level kernels.  chain_flag: the flag word of the chain launched by the last run_rvq (null: none)
+    bool chain_ok = false;
+    unsigned* chain_flag = nullptr;
+    int rvq_chain_fault = 0;    // tests only (mimi_set_option "rvq_chain_fault"; RvqArgs::chain_fault)
+    int64_t chain_reruns = 0;   // encodes re-run without the chain after a sweep gave up (diagnostic)
     // q/k/v + attention as one kernel (qkv_attn.hip) for items of <= 256 frames: 0 off, 1 when the batch has at least
     // 256 (item, head) pairs (one workgroup per CU), 2 whenever the items fit (mimi_set_option "qkv_attn"; same bits)
     int qkv_attn = 1;
     int qkv_attn_xcd = 1;  // its workgroups: an item's heads on one XCD (mimi_set_option "qkv_attn_xcd"; same bits)
-    // ... forming the input LayerNorm itself from the residual stream (mimi_set_option "qkv_attn_ln"; same bits).  Off:
-    // the per-step LayerNorm + split beside 48 accumulators spills (128 VGPRs at 16 waves): 0.47 -> 0.82 ms against
-    // the 0.09 ms of LayerNorm launches it saves (profiles/r4t_ab_qkv_attn_ln.txt)
-    int qkv_attn_ln = 0;
-    // o_proj + residual + the post-attention LayerNorm as one kernel (oproj_ln.hip) when the rows give >= 128 slabs
-    // of 32 (mimi_set_option "oproj_ln"; same bits).  Off: every 32-row slab streams all of W_o (1 MB of planes) through
-    // a 2-stage ring at ~20 GB/s per CU, 0.405 ms against 0.20 + 0.093 for the two kernels (profiles/r4v_ab_oproj_ln.txt)
-    int oproj_ln = 0;
-    // row-slab GEMM (gemm_rows.h) for the large-batch transformer linears: bit 0 fc1, bit 1 fc2, bit 2 o_proj
-    // (mimi_set_option "gemm_rows"; same bits)
-    int gemm_rows = 0;  // (A/B r4p, B = 32: fc1 0.587 -> 0.645-0.651 ms, fc2 0.50 -> 0.536-0.54, o_proj 0.204 -> 0.198-0.203: off)
-    // stage-2 residual block as one kernel (resblock_rows.hip) on large grids: 0 off, 1 on (mimi_set_option
-    // "res_rows"; same bits).  Off: 0.535-0.568 ms against 0.47 for the two planes GEMMs, the down conv before it
-    // 0.72 -> 0.67 (profiles/r4q_ab_res_rows.txt)
-    int res_rows = 0;
     // transformer GEMMs with sc1 output stores (gemm_planes.h FL_SC1OUT; mimi_set_option "sc1_out"): bit 0 q/k/v,
     // bit 1 fc1, bit 2 o_proj and fc2 (large batches; the same bits either way)
     int sc1_out = 2;  // (A/B, round 4: fc1 0.594 -> 0.576 ms per B = 32 step; q/k/v, o_proj and fc2 slower with it)
@@ -1255,9 +1250,13 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     r.frames_per_item = frames_per_item;
     r.form = e->rvq_form;
     r.chain = e->rvq_chain;
+    r.chain_fault = e->rvq_chain_fault;
     r.xcd_group_ok = e->rvq_xcd;
     const char* kname = "?";
-    LAUNCH_TRY(launch_rvq(r, s, &kname), "rvq");
+    unsigned* cflag = nullptr;
+    e->chain_flag = nullptr;
+    LAUNCH_TRY(launch_rvq(r, s, &kname, e->chain_ok ? &cflag : nullptr), "rvq");
+    e->chain_flag = cflag;
     rec.mark("rvq", 2.0 * frames * valid_share * r.D * r.ncodes * K,
              (double)frames * (2 * r.D) * 4 + (double)frames * K * 4, kname);
     return MIMI_OK;
@@ -1355,12 +1354,6 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         snprintf(b, sizeof b, fmt, i);
         return std::string(b);
     };
-    // stage si's residual block as the one-kernel form (resblock_rows.hip): f16x3 planes, C = 256, >= 256 tiles of 128
-    // frames (smaller batches keep the two planes GEMMs: the same bits)
-    auto res_rows_on = [&](int si, int Cs) {
-        return h16 && ns && e->res_rows && si == 2 && Cs == 256 && c.compress == 2 && c.residual_kernel_size == 3 &&
-               (long long)B * ((p.T[si] + 127) / 128) >= 256;
-    };
     for (int si = 0; si < c.num_ratios; ++si) {
         const int64_t T = p.T[si];
         const bool unf = ns && si > 0 && si >= mimi_engine::kUnfuseFrom;
@@ -1455,35 +1448,6 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             snprintf(nm, sizeof nm, "res_s%d", si);
             const double by = BT * 4 * (si == 0 ? 1 + C : 2 * C) + (3.0 * C * H + H * C) * 4;
             rec.mark(nm, fl, by, kname);
-        } else if (res_rows_on(si, C)) {
-            // one kernel: k3 from the fp32 x (ELU(x) planes built in registers), h in LDS, k1 + skip + ELU -> y planes
-            const int Hh = C / c.compress;
-            hact = new_act(nmf("h%d", si));
-            yact = new_act(nmf("y%d", si));
-            ResRowsArgs rr{};
-            rr.x = w.x;
-            rr.T = (int)T;
-            rr.batch = B;
-            rr.tlen = rg ? dT[si] : nullptr;
-            rr.w3 = e->res3[si].wh;
-            rr.us3 = 1.0f / (xeact.scale * e->res3[si].wscale);
-            rr.b3 = e->res3[si].b;
-            rr.xscale = xeact.scale;
-            rr.xamax = xeact.amax;
-            rr.hscale = hact.scale;
-            rr.hamax = hact.amax;
-            rr.w1 = e->res1[si].wh;
-            rr.us1 = 1.0f / (hact.scale * e->res1[si].wscale);
-            rr.b1 = e->res1[si].b;
-            rr.yp = w.y;
-            rr.y_pstride = (long long)B * T * C;
-            rr.yscale = yact.scale;
-            rr.yamax = yact.amax;
-            LAUNCH_TRY(launch_resblock_rows(C, rr, s, &kname), "resblock rows");
-            const double BT = rows_of(si, (double)B * T);
-            snprintf(nm, sizeof nm, "res_s%d", si);
-            rec.mark(nm, 2.0 * BT * (3.0 * C * Hh + (double)Hh * C), BT * C * 4 * 2 + (3.0 * C * Hh + (double)Hh * C) * 4,
-                     kname);
         } else {
             // two plane GEMMs: h = ELU(b3 + W3 (*) ELU(x)) from the ELU(x) planes the down conv wrote, then
             // y = ELU(x + b1 + W1 . h) with the fp32 x as the skip
@@ -1527,8 +1491,6 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
                 ad.C = nullptr;
                 xact = new_act("x_last");
                 out_act(ad, xact);
-            } else if (next_unf && res_rows_on(si + 1, 2 * C)) {  // fp32 x only: the block kernel splits ELU(x) itself
-                xeact = new_act(nmf("xe%d", si + 1));
             } else if (next_unf) {  // fp32 x (the skip) + ELU(x) planes (the next k3 conv's input)
                 ad.Cp = w.xe;
                 ad.c_pstride = (long long)B * p.T[si + 1] * 2 * C;
@@ -1624,8 +1586,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         // q/k/v + attention in one kernel (qkv_attn.hip): large batches of items <= 256 frames, fp16 planes
         const bool fuse_qa = h16 && ns && e->qkv_attn && Dh == 64 && (rg ? rg->maxT25 <= 256 : T <= 256) &&
                              (e->qkv_attn == 2 || (long long)B * H >= 256);
-        const bool fuse_ln = fuse_qa && e->qkv_attn_ln;  // the fused kernel forms the LayerNorm itself
-        if (!fuse_ln && (fuse_qa || !ln_into(aq, ROLE_QKV, x.ln1_w, x.ln1_b, t1a))) {
+        if (fuse_qa || !ln_into(aq, ROLE_QKV, x.ln1_w, x.ln1_b, t1a)) {
             LAUNCH_TRY(launch_layernorm(w.t0, x.ln1_w, x.ln1_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1a.scale,
                                         t1a.amax, nullptr, 0, e->ln_rpw),
                        "ln1");
@@ -1654,17 +1615,9 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             qa.toff = rg ? dToff : nullptr;
             qa.qkv = e->taps ? w.qkv : nullptr;  // (the q/k/v tap, as the GEMM would have stored it)
             qa.xcd = e->qkv_attn_xcd;
-            if (fuse_ln) {
-                qa.ln_x = w.t0;
-                qa.ln_g = x.ln1_w;
-                qa.ln_b = x.ln1_b;
-                qa.ln_eps = c.norm_eps;
-                qa.ln_scale = t1a.scale;
-                qa.ln_amax = t1a.amax;
-            }
             LAUNCH_TRY(launch_qkv_attention(qa, B, s), "qkv_attention");
             rec.mark("qkv_attention", gemm_flops(aq) + att_flops, (double)rows * Hd * 4 * 2 + 3.0 * H * Dh * Hd * 4,
-                     fuse_ln ? "mimi::qkv_attention_h16_kernel<512, true>" : "mimi::qkv_attention_h16_kernel<512, false>");
+                     "mimi::qkv_attention_h16_kernel<512>");
             if ((rc = save_tap(e, nmf("qkv%d", l).c_str(), w.qkv, tapB, tapT, 3 * H * Dh, s))) return rc;
         } else {
             aq.sc1 = (e->sc1_out & 1) != 0;
@@ -1690,35 +1643,9 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         if (ns) planes_in(ao, w.att, nact);
         use_h(ao, x.wo_h, x.wo_hs, atta);
         ao.sc1 = (e->sc1_out & 4) != 0;
-        ao.rows_form = (e->gemm_rows & 4) != 0;
         const Act t1b = new_act(nmf("xf%d.ln2", l));
-        // o_proj + residual + post-attention LayerNorm in one kernel (oproj_ln.hip) on large batches
-        const bool fuse_oln = h16 && ns && e->oproj_ln && Hd == 512 && H * Dh == 512 && (rows + 31) / 32 >= 128;
-        if (fuse_oln) {
-            OprojLnArgs ol{};
-            ol.Ap = ao.Ap;
-            ol.a_pstride = ao.a_pstride;
-            ol.Wp = ao.Wsplit;
-            ol.M = (int)rows;
-            ol.N = Hd;
-            ol.K = H * Dh;
-            ol.unscale = ao.unscale;
-            ol.scale = x.ls1;
-            ol.R = w.t0;
-            ol.C = w.t0;
-            ol.ln_g = x.ln2_w;
-            ol.ln_b = x.ln2_b;
-            ol.ln_eps = c.norm_eps;
-            ol.ln_scale = t1b.scale;
-            ol.ln_out = w.t1;
-            ol.ln_pstride = nact;
-            ol.ln_amax = t1b.amax;
-            LAUNCH_TRY(launch_oproj_ln(ol, s, &kname), "o_proj + LayerNorm");
-            rec.mark("o_proj_ln", gemm_flops(ao), gemm_bytes(ao, true) + (double)rows * Hd * 4, kname);
-        } else {
-            LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
-            rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
-        }
+        LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
+        rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
         if ((rc = save_tap(e, nmf("oproj%d", l).c_str(), w.t0, tapB, tapT, Hd, s))) return rc;
         GemmArgs a1 = linear_args(w.t1, rows, Hd, x.w1, c.intermediate_size, w.ff);
         a1.Wsplit = x.w1_s;
@@ -1732,14 +1659,13 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             ffa = new_act(nmf("xf%d.ff", l));
             out_act(a1, ffa);
         }
-        if (!fuse_oln && !ln_into(a1, ROLE_FC1, x.ln2_w, x.ln2_b, t1b)) {
+        if (!ln_into(a1, ROLE_FC1, x.ln2_w, x.ln2_b, t1b)) {
             LAUNCH_TRY(launch_layernorm(w.t0, x.ln2_w, x.ln2_b, w.t1, rows, Hd, c.norm_eps, s, w.t1, nact, ns, t1b.scale,
                                         t1b.amax, nullptr, 0, e->ln_rpw),
                        "ln2");
             rec.mark("layernorm", 0, 2.0 * rows * Hd * 4, ln_kname(e->ln_rpw));
         }
         a1.sc1 = (e->sc1_out & 2) != 0;
-        a1.rows_form = (e->gemm_rows & 1) != 0;
         a1.ncg = e->fc1_cg;
         LAUNCH_TRY(launch_gemm(ROLE_FC1, a1, s, &kname, prec), "fc1");
         rec.mark("fc1", gemm_flops(a1), gemm_bytes(a1, false), kname);
@@ -1758,7 +1684,6 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             out_act(a2, dsin);
         }
         a2.sc1 = (e->sc1_out & 4) != 0;
-        a2.rows_form = (e->gemm_rows & 2) != 0;
         LAUNCH_TRY(launch_gemm(ROLE_FC2, a2, s, &kname, prec), "fc2");
         rec.mark("fc2", gemm_flops(a2), gemm_bytes(a2, true), kname);
         snprintf(nm, sizeof nm, "xfmr%d", l);
@@ -2076,6 +2001,7 @@ static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int
     ng.rope_gen = e->rope_gen;
     ng.g = g;
     ng.x = x;
+    ng.chain_flag = e->chain_flag;
     e->graphs.push_back(ng);
     return &e->graphs.back();
 }
@@ -2083,8 +2009,9 @@ static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int
 // Runs the f16x3 pass of (B, L, K) as a graph replay on s when it can (*replayed = true); otherwise leaves
 // everything to the eager path.
 static int graph_encode(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s,
-                        bool* replayed) {
+                        bool* replayed, unsigned** chain_flag) {
     *replayed = false;
+    *chain_flag = nullptr;
     if (!e->graphs_enabled || e->profiling || e->taps || e->calibrating) return MIMI_OK;
     // sizes first: nothing may be allocated inside a capture, and a reallocation retires the graphs
     const StagePlan p = plan_lengths(e->cfg, L);
@@ -2117,6 +2044,7 @@ static int graph_encode(mimi_engine* e, const float* audio, int B, int64_t L, in
     HIP_TRY(hipGraphLaunch(gr->x, s));
     ++e->graph_replays;
     *replayed = true;
+    *chain_flag = gr->chain_flag;
     return MIMI_OK;
 }
 
@@ -2134,6 +2062,8 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
         return set_err(MIMI_ERR_STATE, "%d encodes in flight: call mimi_encode_wait first", mimi_engine::kMaxPending);
     if (!P->done) HIP_TRY(hipEventCreateWithFlags(&P->done, hipEventDisableTiming));
     if (!P->amax) HIP_TRY(hipHostMalloc(&P->amax, kMaxActSlots * sizeof(unsigned), hipHostMallocDefault));
+    if (!P->chain_word) HIP_TRY(hipHostMalloc(&P->chain_word, 16, hipHostMallocDefault));
+    P->chain = false;
     const int prec = e->precision;
     const bool h16 = prec == PREC_F16X3 && act_planes(e, plan_lengths(e->cfg, L), prec) == 2;
     int rc;
@@ -2185,7 +2115,13 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
     }
     if (h16) {
         bool replayed = false;
-        if (!lengths && (rc = graph_encode(e, audio, B, L, K, codes, s, &replayed))) return rc;
+        unsigned* cflag = nullptr;
+        struct ChainScope {  // the chain is allowed inside this pass only (its flag is read back below)
+            mimi_engine* e;
+            explicit ChainScope(mimi_engine* x) : e(x) { e->chain_ok = true; }
+            ~ChainScope() { e->chain_ok = false; }
+        } chain_scope(e);
+        if (!lengths && (rc = graph_encode(e, audio, B, L, K, codes, s, &replayed, &cflag))) return rc;
         n = (int)e->slot_of.size();
         if (!replayed) {
             HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));  // the maxima buffers are part of the workspace
@@ -2198,8 +2134,13 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
                 return set_err(MIMI_ERR_STATE, "f16x3: an activation has no calibrated scale");
             }
             LAUNCH_TRY(launch_amax_reduce(e->amax_dev, n, e->amax_red, s), "amax_reduce");
+            cflag = e->chain_flag;
         }
         HIP_TRY(hipMemcpyAsync(P->amax, e->amax_red, n * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        if (cflag) {  // (before ws_free: the next encode's memset node zeroes the flag)
+            HIP_TRY(hipMemcpyAsync(P->chain_word, cflag, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+            P->chain = true;
+        }
         HIP_TRY(hipEventRecord(e->ws_free, s));
     } else if ((rc = encode_pass(e, audio, B, L, K, codes, s, prec))) {
         return rc;
@@ -2243,6 +2184,7 @@ static int encode_wait(mimi_engine* e, int64_t ticket) {
     for (auto& x : e->pend)
         if (x.id == ticket) P = &x;
     bool ovf = false;
+    const bool chain_gave_up = q.chain && se == hipSuccess && P->chain_word[0] != 0u;
     if (q.h16 && se == hipSuccess) {
         e->last_amax.assign(q.nslots, 0.0f);
         for (int i = 0; i < q.nslots; ++i) {
@@ -2257,6 +2199,16 @@ static int encode_wait(mimi_engine* e, int64_t ticket) {
     if (se != hipSuccess)
         return set_err(se == hipErrorOutOfMemory ? MIMI_ERR_OUT_OF_MEMORY : MIMI_ERR_HIP, "hipEventSynchronize: %s",
                        hipGetErrorString(se));
+    if (chain_gave_up) {  // the persistent RVQ gave up (its codes are not kept): the whole encode again, without it
+        ++e->chain_reruns;
+        HIP_TRY(hipSetDevice(e->device));
+        if (q.ragged) return ragged_item_by_item(e, q.audio, q.B, q.L, q.lens.data(), q.K, q.codes, q.s, PREC_F16X3);
+        bool ovf2 = false;
+        int rc = f16_pass(e, q.audio, q.B, q.L, q.K, q.codes, q.s, &ovf2);
+        if (rc) return rc;
+        if (!ovf2) return MIMI_OK;
+        return overflow_fallback(e, q.audio, q.B, q.L, q.K, q.codes, q.s);
+    }
     if (!ovf) return MIMI_OK;
     HIP_TRY(hipSetDevice(e->device));
     if (q.ragged) {  // each item alone at its own length (the ragged result's definition), bf16x6 if it overflows
@@ -2374,7 +2326,20 @@ extern "C" int mimi_rvq_encode(mimi_engine* e, const float* emb, int64_t frames,
     const char* kname = "?";
     LAUNCH_TRY(launch_gemm(ROLE_INPROJ, ap, s, &kname), "input_proj");
     rec.mark("input_proj", 2.0 * frames * Hd * 2 * Dq, 0, kname);
-    if ((rc = run_rvq(e, proj, frames, K, codes, 0, reinterpret_cast<char*>(e->ws) + projb, s, rec))) return rc;
+    e->chain_ok = true;  // (checked right here: a give-up re-runs the levels on the per-level kernels)
+    rc = run_rvq(e, proj, frames, K, codes, 0, reinterpret_cast<char*>(e->ws) + projb, s, rec);
+    e->chain_ok = false;
+    if (rc) return rc;
+    if (e->chain_flag) {
+        unsigned flag = 0;
+        HIP_TRY(hipMemcpyAsync(&flag, e->chain_flag, sizeof flag, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        e->chain_flag = nullptr;
+        if (flag) {
+            ++e->chain_reruns;
+            if ((rc = run_rvq(e, proj, frames, K, codes, 0, reinterpret_cast<char*>(e->ws) + projb, s, rec))) return rc;
+        }
+    }
     HIP_TRY(hipEventRecord(e->ws_free, s));
     return MIMI_OK;
 }
@@ -2399,6 +2364,7 @@ extern "C" void mimi_destroy(mimi_engine* e) {
         if (q.done) (void)hipEventDestroy(q.done);
         if (q.amax) (void)hipHostFree(q.amax);
         if (q.rg_pinned) (void)hipHostFree(q.rg_pinned);
+        if (q.chain_word) (void)hipHostFree(q.chain_word);
     }
     drop_graphs(e);
     if (e->io_dev) (void)hipFree(e->io_dev);
@@ -2446,14 +2412,11 @@ static const EngineOption kEngineOptions[] = {
     {"ln_rpw", &mimi_engine::ln_rpw, 0x117u, "0, 1, 2, 4 or 8"},
     {"rvq_xcd", &mimi_engine::rvq_xcd, 0x3u, "0 or 1"},
     {"rvq_chain", &mimi_engine::rvq_chain, 0x3u, "0 or 1"},
+    {"rvq_chain_fault", &mimi_engine::rvq_chain_fault, 0x7u, "0, 1 or 2"},
     {"sc1_out", &mimi_engine::sc1_out, 0xffu, "0..7"},
     {"ln_fused", &mimi_engine::ln_fused, 0x1fu, "0 .. 4"},
     {"qkv_attn", &mimi_engine::qkv_attn, 0x7u, "0, 1 or 2"},
     {"qkv_attn_xcd", &mimi_engine::qkv_attn_xcd, 0x3u, "0 or 1"},
-    {"qkv_attn_ln", &mimi_engine::qkv_attn_ln, 0x3u, "0 or 1"},
-    {"oproj_ln", &mimi_engine::oproj_ln, 0x3u, "0 or 1"},
-    {"gemm_rows", &mimi_engine::gemm_rows, 0xffu, "0..7"},
-    {"res_rows", &mimi_engine::res_rows, 0x3u, "0 or 1"},
     {"fc1_cg", &mimi_engine::fc1_cg, 0x17u, "0, 1, 2 or 4"},
     {"res1_form", &mimi_engine::res1_form, 0x3u, "0 or 1"},
 };
@@ -2509,6 +2472,8 @@ extern "C" int mimi_calibrate(mimi_engine* e) {
 }
 
 extern "C" int64_t mimi_f16_reruns(const mimi_engine* e) { return e ? e->f16_reruns : -1; }
+
+extern "C" int64_t mimi_rvq_chain_reruns(const mimi_engine* e) { return e ? e->chain_reruns : -1; }
 
 extern "C" int mimi_set_profiling(mimi_engine* e, int enable) {
     if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");

@@ -20,7 +20,6 @@
 
 
 #include "gemm_planes.h"
-#include "gemm_rows.h"
 
 #ifndef MIMI_QKV_V
 #define MIMI_QKV_V 1
@@ -93,7 +92,9 @@ static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
     if (nwg > 0x7fffffffLL) return hipErrorInvalidValue;
     if (F16 && ((OUTP & 7) ? a.out_scale <= 0.0f : false)) return hipErrorInvalidValue;
     if constexpr ((FL & FL_SC1OUT) != 0) {  // 32-bit byte offsets from an item's output base (gemm_planes.h)
-        const long long rows = (FL & FL_RAGGED) ? (long long)a.M : (long long)a.M;
+        // an item's output rows are at most M (a ragged item's m_rows <= M; a batched item's base is c_base_of(b)
+        // and its rows M), so M rows of ldc bound every sc1 store's offset from that base
+        const long long rows = a.M;
         if ((rows * a.ldc + a.N) * 4 > 0x7fffffffLL || ((OUTP & 7) && (a.c_pstride + rows * a.ldc) * 2 > 0x7fffffffLL))
             return run_planes<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL & ~FL_SC1OUT, F16>(a, s);
     }
@@ -253,29 +254,6 @@ bool gemm_ln_prologue_ok(int role, const GemmArgs& a, int precision) {
            a.a_off == 0 && !a.a_rows && !a.m_rows && !a.a_boff && tiles(a, 128, 128) < kSmallGrid;
 }
 
-// Row-slab kernel (gemm_rows.h) for a flat [M][K] x [N][K] GEMM on fp16 planes: NW waves x 16 rows, BN columns
-template <int K, int BN, int NW, int S, int EPI, int OUTP, int PA = 2>
-static hipError_t run_rows(const GemmArgs& a, hipStream_t s) {
-    static char name[128];
-    if (!name[0])
-        snprintf(name, sizeof(name), "mimi::gemm_rows_kernel<%d, %d, %d, %d, %d, %d, %d>", K, BN, NW, S, EPI, OUTP, PA);
-    g_last_kernel = name;
-    if (a.K != K || a.N % BN || a.ldc != a.N || !a.Ap || !a.Wsplit || ((OUTP & 7) && (!a.Cp || !(a.out_scale > 0.0f))) ||
-        (!(OUTP & 7) && !a.C) || (EPI == EPI_SCALE_RES && (!a.R || !a.scale)))
-        return hipErrorInvalidValue;
-    if ((long long)a.M * K * 2 + 16LL * NW * K * 2 > 0x7fffffffLL || 2LL * a.N * K * 2 > 0x7fffffffLL)
-        return hipErrorInvalidValue;  // 32-bit buffer offsets
-    const long long nwg = (long long)((a.M + 16 * NW - 1) / (16 * NW)) * (a.N / BN);
-    hipLaunchKernelGGL((gemm_rows_kernel<K, BN, NW, S, EPI, OUTP, PA>), dim3((unsigned)nwg), dim3(NW * 64), 0, s, a);
-    return hipGetLastError();
-}
-
-// the row-slab forms: flat GEMMs only (one item or packed rows), no ragged / conv addressing
-static bool rows_ok(const GemmArgs& a) {
-    return a.rows_form && a.batch == 1 && a.a_off == 0 && a.a_rs == a.K && a.a_cin == a.K && !a.a_rows && !a.m_rows &&
-           !a.a_boff && !a.c_boff && !a.ln_x && a.c_pstride % 8 == 0;
-}
-
 static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
     const int prec = g_prec;
     if (prec != PREC_BF16X6 && prec != PREC_BF16X3 && prec != PREC_F16X3) return hipErrorInvalidValue;
@@ -358,14 +336,12 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
             }
             return run_planes_small<EPI_ROPE, 5>(a, s, prec);  // (256x256: -11 % alone, 0 in the engine)
         case ROLE_OPROJ:
-            if (prec == PREC_F16X3 && rows_ok(a) && a.K == 512) return run_rows<512, 128, 8, 6, EPI_SCALE_RES, 0>(a, s);
             return run_planes_small_ld<EPI_SCALE_RES, 6>(a, s, prec);
         case ROLE_FC1:  // planes out: fc2; fp16: 128x128 on a 2-stage ring (two workgroups per CU): -4 % vs
                         // 256x256 x 2 stages, which beat 256x128 x 3 by 8-11 % (profiles/r1j_gemm_bench_256.log,
                         // r1l_ab_small_kernels.txt)
             // (256x128 persistent tiles with FL_PF: -8 % in tools/gemm_bench.hip, +5 % in the engine with the GELU
             // planes epilogue -- profiles/r2c_gemm_bench_pf.log, r2c_ab_fc1.log)
-            if (prec == PREC_F16X3 && rows_ok(a) && a.K == 512 && !a.C) return run_rows<512, 128, 16, 6, EPI_GELU, 2>(a, s);
             if (prec == PREC_F16X3) {
 #if MIMI_FC1_V == 1
                 return run_planes<128, 128, 4, 2, 2, 3, EPI_GELU, 2, 7, 4, 32, 16, FL_PERSIST | FL_PF, true>(a, s);
@@ -376,10 +352,6 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
             }
             return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);
         case ROLE_FC2:
-            if (prec == PREC_F16X3 && rows_ok(a) && a.K == 2048) {
-                if (a.Cp) return run_rows<2048, 128, 8, 6, EPI_SCALE_RES, 2>(a, s);
-                return run_rows<2048, 128, 8, 6, EPI_SCALE_RES, 0>(a, s);
-            }
             return run_planes_small_ld<EPI_SCALE_RES, 8>(a, s, prec);
         case ROLE_DOWN_XE: return run_planes_big<EPI_BIAS, 3 | 8, 2 | 8, 11>(a, s, prec);
         case ROLE_RES3P:  // fp16: 256x128 on a 3-stage ring fed by 4 loader waves: -8 / -13 % vs 128x128 x 2

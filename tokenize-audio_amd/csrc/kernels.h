@@ -230,8 +230,6 @@ struct GemmArgs {
     // (engine option sc1_out; the same bits either way)
     int sc1;
     int ln_tile;  // host-side hint: the q/k/v LayerNorm-prologue tile on small grids (0 16x64, 1 32x64, 2 16x128)
-    int rows_form;  // host-side hint: 1 = the row-slab kernel (gemm_rows.h) where the role has one (fc1 / fc2 / o_proj,
-                    // large grids, f16x3; engine option gemm_rows; the same bits either way)
     int ncg;  // planes kernels: XCD column groups of the tile order (0 / 1 none; must divide the N tiles, else none;
               // engine option fc1_cg; which workgroup computes a tile only, the same bits either way)
 };
@@ -381,62 +379,8 @@ struct QkvAttnArgs {
     const int* toff;
     float* qkv;                // optional: the fp32 q/k/v rows as the GEMM would store them (taps)
     int xcd;                   // 1: an item's heads on one XCD (workgroup order; speed only)
-    // optional: A = LayerNorm(ln_x) formed in-kernel with layernorm_kernel's arithmetic (its planes at ln_scale, max
-    // |out| to ln_amax) instead of read from Ap -- the input LayerNorm launch and its planes' HBM round trip go away
-    const float* ln_x;         // residual stream [rows][K] fp32
-    const float* ln_g;
-    const float* ln_b;
-    float ln_eps;
-    float ln_scale;
-    unsigned* ln_amax;
 };
 hipError_t launch_qkv_attention(const QkvAttnArgs& a, int items, hipStream_t s);
-
-// Stage-2 residual block (C = 256, H = 128) in one kernel on fp16 planes (resblock_rows.hip): the k3 conv's A
-// fragments built in registers from the fp32 x (ELU + the ELU(x) planes' split), h in LDS, the k1 conv + skip + ELU
-// -> y planes.  Bitwise the unfused path's y (down conv ELU(x) planes -> k3 planes GEMM -> k1 planes GEMM).
-struct ResRowsArgs {
-    const float* x;        // [batch][T][C] fp32 (the down conv's output: block input and skip)
-    int T, batch;
-    const int* tlen;       // ragged: valid frames per item (null: T)
-    const void* w3;        // k3 weight planes [2][H][3 C] (tap-major K), 1 / (ELU(x) scale x weight scale) in us3
-    float us3;
-    const float* b3;
-    float xscale;          // the ELU(x) planes' scale and max slot (the act slot the down conv would have filled)
-    unsigned* xamax;
-    float hscale;          // h planes (LDS only): scale and max slot
-    unsigned* hamax;
-    const void* w1;        // k1 weight planes [2][C][H]
-    float us1;
-    const float* b1;
-    void* yp;              // y planes [batch][T][C], plane stride y_pstride, scale yscale, max slot yamax
-    long long y_pstride;
-    float yscale;
-    unsigned* yamax;
-};
-hipError_t launch_resblock_rows(int C, const ResRowsArgs& a, hipStream_t s, const char** kname);
-
-// o_proj + layer scale + residual and the post-attention LayerNorm in one kernel (oproj_ln.hip): workgroups of 32
-// rows x all 512 columns; C (= R, in place) bitwise the o_proj planes GEMM's, the LayerNorm planes the LayerNorm
-// kernel's.
-struct OprojLnArgs {
-    const void* Ap;        // attention output planes [M][K] (plane 1 at + a_pstride)
-    long long a_pstride;
-    const void* Wp;        // o_proj weight planes [2][N][K]
-    int M, N, K;
-    float unscale;         // 1 / (activation scale x weight scale)
-    const float* scale;    // layer scale [N]
-    const float* R;        // residual stream [M][N] (read) ...
-    float* C;              // ... and the updated stream (may equal R)
-    const float* ln_g;
-    const float* ln_b;
-    float ln_eps;
-    float ln_scale;        // LayerNorm planes: out * ln_scale as 2 fp16 planes at ln_out (plane stride ln_pstride)
-    void* ln_out;
-    long long ln_pstride;
-    unsigned* ln_amax;
-};
-hipError_t launch_oproj_ln(const OprojLnArgs& a, hipStream_t s, const char** kname);
 
 // planes -> fp32 (x0 + x1 [+ x2], or (h0 + h1) / hscale for fp16 planes); used only to materialise per-stage
 // taps of plane-format activations.
@@ -474,9 +418,14 @@ struct RvqArgs {
                             // rvq_chain; same codes)
     int xcd_group_ok;       // large grids: the slices of a frame tile on one XCD (engine option rvq_xcd; speed only)
     int xcd_group;          // (set by launch_rvq)
+    int chain_fault;        // fault injection for the chain's give-up path (engine option rvq_chain_fault, tests only):
+                            // 0 off, 1 a zero spin budget, 2 every sweep gives up at once
 };
 size_t rvq_work_bytes(long long frames);
-hipError_t launch_rvq(const RvqArgs& a, hipStream_t s, const char** kname = nullptr);  // kname: the level kernel's symbol
+// kname: the level kernel's symbol.  chain_flag (may be null): set to the device word the persistent chain raises when a
+// sweep gave up (the launch's codes are then invalid and the caller re-runs without the chain), or to null when this
+// launch did not take the chain
+hipError_t launch_rvq(const RvqArgs& a, hipStream_t s, const char** kname = nullptr, unsigned** chain_flag = nullptr);
 
 // polyphase resampler (resample.hip): clips packed at in_off / out_off (device int64 arrays), one launch
 hipError_t launch_resample_poly(const float* x, const long long* in_off, const long long* in_len, int nclips,

@@ -1642,11 +1642,15 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
 // launch), sweeps the granules of the frame tile's other 7 slices, merges the 8 slices in slice order with
 // rvq_merge's rule, stores the codes (slice 0) and subtracts the winning code rows.  The next level's codebook
 // fragments are loaded before the sweep, so they fly under it.  Same codes as the per-level launches.
-// Every workgroup of a launch must be resident at once: the host keeps the grid at <= 128 workgroups (2 fit a CU), and
-// every spin is bounded -- a sweep that times out (only possible if other persistent kernels hold the CUs) stores
-// code -1 for its frames, an impossible code.
+// Every workgroup of a launch must be resident at once: the host takes this kernel only when the occupancy query admits
+// the whole grid (<= 128 workgroups, 2 per CU), and every spin is bounded.  A sweep that gives up (other work -- another
+// process's kernels -- kept a peer off the CUs for the whole budget) never merges what it has: the workgroup raises the
+// launch's flag word (the 16 bytes in front of the granules, zeroed by the same memset node) and leaves, every other
+// workgroup leaves at its next sweep once it sees the flag, and the host, which reads the flag back behind the encode,
+// re-runs the encode without the chain (engine.cpp encode_wait).  So a give-up costs time, never codes.
 constexpr int RVQC_MAX_WG = 128;
 constexpr int RVQC_SPIN = 1 << 20;
+constexpr int RVQC_HDR = 2;  // u64 words in front of the granules: [0] the give-up flag (u32), [1] padding
 
 __device__ __forceinline__ unsigned long long rvqc_granule(unsigned epoch, unsigned long long best) {
     // best = (distance bits << 32) | code (code 0xffffffff: none): tag 16 bits | code 16 bits | distance 32 bits
@@ -1671,7 +1675,7 @@ __device__ __forceinline__ unsigned long long rvqc_granule(unsigned epoch, unsig
 #define RVQC_TPRINT()
 #endif
 template <int D, int EX>
-__global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsigned long long* __restrict__ gran) {
+__global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsigned long long* __restrict__ gbase) {
     constexpr int NWV = 8, NT = 512, FT = 32, CW = 32, SLC = NWV * CW, NSL = 2048 / SLC;
     constexpr int LDH = D / 2 + 4, RLD = D + 8, KS = D / 16;
     static_assert(NSL == 8, "8 slices of 256 codes");
@@ -1698,6 +1702,10 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
     const int slice = blockIdx.y;
     const int code0 = slice * SLC + wave * CW;
     const unsigned ftiles = gridDim.x;
+    typedef __attribute__((address_space(1))) unsigned gu32;
+    gu32* const flag = (gu32*)gbase;  // the launch's give-up flag
+    unsigned long long* const gran = gbase + RVQC_HDR;
+    const unsigned spin_limit = p.chain_fault == 1 ? 0u : (unsigned)RVQC_SPIN;
     // granules [parity 2][chain 2][frame tile][slice 8][32 frames]
     auto gslot = [&](int par, int sl) {
         return gran + ((((long long)par * 2 + chain) * ftiles + blockIdx.x) * NSL + sl) * FT;
@@ -1804,10 +1812,12 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
             __hip_atomic_store((gu64*)(gslot(L & 1, slice) + tid), rvqc_granule(epoch, best[tid]), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         if (L + 1 < Le) load_cb(L + 1);  // the next level's codebook: in flight under the sweep
-        // sweep the frame tile's 8 slices (wave 0, 4 granules per lane) until every tag is this level's
+        // sweep the frame tile's 8 slices (wave 0, 4 granules per lane) until every tag is this level's; give up when
+        // the budget runs out or another workgroup already gave up (the flag, polled every 64th pass)
         if (wave == 0) {
             unsigned long long v[4];
-            for (unsigned spins = 0;; ++spins) {
+            bool fail = p.chain_fault == 2;
+            for (unsigned spins = 0; !fail; ++spins) {
                 bool ok = true;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -1817,20 +1827,30 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
                     ok = ok && (unsigned)(v[q] >> 48) == epoch;
                 }
                 if (__all(ok)) break;
-                if (spins >= RVQC_SPIN) {
-                    if (lane == 0) tmo = 1;
+                if (spins >= spin_limit ||
+                    ((spins & 63) == 63 &&
+                     __any(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u))) {
+                    fail = true;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
+            if (fail) {
+                if (lane == 0) {
+                    __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    tmo = 1;
+                }
+            } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int j = lane + 64 * q;
-                gd[j >> 5][j & 31] = __uint_as_float((unsigned)(v[q] & 0xffffffffu));
-                gi[j >> 5][j & 31] = (int)(short)(unsigned short)((v[q] >> 32) & 0xffffu);
+                for (int q = 0; q < 4; ++q) {
+                    const int j = lane + 64 * q;
+                    gd[j >> 5][j & 31] = __uint_as_float((unsigned)(v[q] & 0xffffffffu));
+                    gi[j >> 5][j & 31] = (int)(short)(unsigned short)((v[q] >> 32) & 0xffffu);
+                }
             }
         }
         __syncthreads();
+        if (tmo) return;  // (workgroup-uniform: LDS, behind the barrier) nothing of this launch is kept
         RVQC_T(5);
         if (tid < FT) {  // rvq_merge's rule over the slices in order
             float d = gd[0][tid];
@@ -1842,7 +1862,7 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
                     ix = gi[q][tid];
                 }
             ix = (ix < 0 || ix >= p.ncodes) ? 0 : ix;
-            codes_l[tid][L] = tmo ? -1 : ix;
+            codes_l[tid][L] = ix;
             prev[tid] = ix;
         }
         __syncthreads();
@@ -1874,9 +1894,27 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
     }
 }
 
-hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
+// whether the chain's whole grid is resident at once by the occupancy query (this process's view: other processes'
+// kernels can still hold CUs for a while, which the bounded sweeps and the give-up flag cover)
+static bool rvq_chain_fits(unsigned grid) {
+    static int cap = -1;
+    if (cap < 0) {
+        int dev = 0, ncu = 0, nb = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rvq_chain_h16_kernel<256, 16>, 512, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            nb = ncu = 0;
+        }
+        cap = nb * ncu;
+    }
+    return grid <= (unsigned)cap;
+}
+
+hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname, unsigned** chain_flag) {
     const char* kn_dummy = nullptr;
     if (!kname) kname = &kn_dummy;
+    if (chain_flag) *chain_flag = nullptr;
     if (args.D != 256 || args.ncodes != 2048 || !args.work) return hipErrorInvalidValue;
     RvqArgs a = args;
     a.sem_split = (a.nsem == 1 && a.levels > 1 && a.cb_h16 && a.cb_unscale && a.cb_emax) ? 1 : 0;
@@ -1899,18 +1937,21 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname) {
         const int form = a.form == 0 ? 5 : a.form;
         // small grids: every level in one persistent launch (rvq_chain_h16_kernel), unless the form asks otherwise
         const int nchain = (a.levels > a.nsem ? 1 : 0) + (a.nsem > 0 ? 1 : 0);
-        if (small && a.chain && form != 1 && ftiles32 * 8 * 2 <= (unsigned)RVQC_MAX_WG && a.nsem <= 1) {
-            const size_t gbytes = (size_t)2 * 2 * ftiles32 * 8 * 32 * 8;
+        // (only for a caller that reads the give-up flag back: chain_flag non-null)
+        if (small && a.chain && chain_flag && form != 1 && ftiles32 * 8 * 2 <= (unsigned)RVQC_MAX_WG && a.nsem <= 1 &&
+            rvq_chain_fits(ftiles32 * 8 * 2)) {
+            const size_t gbytes = (size_t)RVQC_HDR * 8 + (size_t)2 * 2 * ftiles32 * 8 * 32 * 8;
             const size_t pd_off = (size_t)2 * ((a.frames + RVQ_FT - 1) / RVQ_FT * RVQ_FT) * a.D * 4;
             if (gbytes > rvq_work_bytes(a.frames) - pd_off) return hipErrorInvalidValue;
-            unsigned long long* gran = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.work) + pd_off);
-            const hipError_t me = hipMemsetAsync(gran, 0, gbytes, s);
+            unsigned long long* gbase = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.work) + pd_off);
+            const hipError_t me = hipMemsetAsync(gbase, 0, gbytes, s);  // flag + granules: every launch (and replay)
             if (me != hipSuccess) return me;
             static char knc[96];
             snprintf(knc, sizeof knc, "mimi::rvq_chain_h16_kernel<256, 16>");
             *kname = knc;
             (void)nchain;
-            hipLaunchKernelGGL((rvq_chain_h16_kernel<256, 16>), dim3(ftiles32, 8, 2), dim3(512), 0, s, a, gran);
+            hipLaunchKernelGGL((rvq_chain_h16_kernel<256, 16>), dim3(ftiles32, 8, 2), dim3(512), 0, s, a, gbase);
+            *chain_flag = reinterpret_cast<unsigned*>(gbase);
             return hipGetLastError();
         }
         const bool p1 = form >= 2;

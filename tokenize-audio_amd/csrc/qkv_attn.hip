@@ -18,7 +18,7 @@
 //      head's power-of-two scales, per-task Q planes, the chunk loops, the two-half merge and the planes store.
 // Every value is computed as on the unfused path, so an item's codes do not depend on which path its batch took
 // (the engine runs this kernel only for large batches; batch 1 keeps the small-grid GEMM + attention).
-#include "gemm_rows.h"
+#include "ring_wait.h"
 #include "attn_h16.h"
 
 #ifndef QA_DIAG
@@ -32,7 +32,7 @@
 
 namespace mimi {
 
-template <int K, bool LN>
+template <int K>
 __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, int items) {
 #if defined(__HIP_DEVICE_COMPILE__)
     constexpr int D = 64, TM = 256, LDO = D + 1, NWV = 16;
@@ -51,7 +51,6 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
     __shared__ __attribute__((aligned(16))) _Float16 lds[2 * KPL + 2 * VPL + 512];  // (+ the dummy DMA piece's 1 KiB)
     __shared__ float red[2][NWV];
     __shared__ float mlx[8][2][32];
-    __shared__ __attribute__((aligned(16))) float lng[LN ? K : 4], lnb[LN ? K : 4];  // (LN) gamma, beta
 
     const int H = p.H;
     int h, b;
@@ -109,111 +108,32 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
                                                      woff[q] + kt * BK * 2, 0, 0, 0);
         }
     };
-    // LN: the A operand is LayerNorm(x) of the residual stream (p.ln_x, fp32 [rows][K]) formed here with
-    // layernorm_kernel's arithmetic (kernels.h ln_row_coeffs / ln_affine, the same fp16 split at the same scale), so
-    // the fragments are bitwise the planes the LayerNorm launch would have stored; a slot then holds this lane's 8 raw
-    // fp32 x values (the same 32 bytes per lane and step as the two planes)
-    const __amdgpu_buffer_rsrc_t xrs = make_rsrc(LN ? (const void*)p.ln_x : nullptr, LN ? p.a_rows * K * 4 : 0);
-    const int xoff = (int)(((row0 + wave * 16 + (lane & 15)) * K + hsel * 8) * 4);
     auto loadA = [&](int kt, bf16x8 (&a)[2]) {
-        if constexpr (LN) {
-            int o = xoff + kt * BK * 4;
-            asm volatile("" : "+v"(o));  // (the load stays in its step)
-            a[0] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, o, 0, 0));
-            a[1] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, o + 16, 0, 0));
-        } else {
-            a[0] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ars0, aoff + kt * BK * 2, 0, 0));
-            a[1] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ars1, aoff + kt * BK * 2, 0, 0));
-        }
+        a[0] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ars0, aoff + kt * BK * 2, 0, 0));
+        a[1] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ars1, aoff + kt * BK * 2, 0, 0));
     };
 
     f32x4 acc[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // A fragments of K steps kt .. kt + PA (slot kt % (PA + 1)); with the in-kernel LayerNorm one step ahead (its
-    // conversion temporaries need the registers of the third slot: two steps ahead spilled)
-    constexpr int PA = LN ? 1 : 2;
+    // A fragments of K steps kt .. kt + PA (slot kt % (PA + 1))
+    constexpr int PA = 2;
     bf16x8 a[PA + 1][2];
     // W(0) .. W(S - KG - 1) and A(0) .. A(PA - 1) ahead; per K step kt: A(kt + PA); per group of KG steps the W refills
     // (below).  The compiler keeps the DMA issues in order against the waits but places the A register loads freely
-    // (and inserts their waits itself), so the ring waits count DMA pieces only (gemm_rows.h rows_dma_after)
+    // (and inserts their waits itself), so the ring waits count DMA pieces only (ring_wait.h rows_dma_after)
 #pragma unroll
     for (int k = 0; k < S - KG; ++k)
         if (k < KT) issueB(k);
 #pragma unroll
     for (int k = 0; k < PA; ++k)
         if (k < KT) loadA(k, a[k]);
-    // LN: gamma / beta into LDS, and each row's (rstd, -mean rstd) with layernorm_kernel's lane layout (one wave per
-    // row, lane l holding columns 256 q + 4 l + e), the row's pair then moved to the lanes that hold its fragments
-    float lsc = 0.0f, lbi = 0.0f, lnmx = 0.0f;
-    const bool lrow = wave * 16 + (lane & 15) < T;  // (this lane's fragment row is one of the item's frames)
-    if constexpr (LN) {
-        for (int i = tid; i < K; i += 1024) {
-            lng[i] = p.ln_g[i];
-            lnb[i] = p.ln_b[i];
-        }
-        static_assert(K == 512, "LayerNorm width");
-#pragma unroll
-        for (int r0 = 0; r0 < 16; r0 += 4) {
-            float v[4][8];
-            // (an opaque base per group of 4 rows: otherwise all 16 rows' loads are issued at once and spill)
-            int rbase = (int)((row0 + wave * 16 + r0) * K * 4);
-            asm volatile("" : "+v"(rbase));
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int roff = rbase + i * K * 4;
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const f32x4 t = __builtin_bit_cast(
-                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, roff + (q * 256 + lane * 4) * 4, 0, 0));
-                    v[i][q * 4 + 0] = t.x; v[i][q * 4 + 1] = t.y; v[i][q * 4 + 2] = t.z; v[i][q * 4 + 3] = t.w;
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float sc, bi;
-                ln_row_coeffs<K>(v[i], p.ln_eps, sc, bi);
-                if ((lane & 15) == r0 + i) {
-                    lsc = sc;
-                    lbi = bi;
-                }
-            }
-        }
-        __syncthreads();  // gamma / beta visible
-    }
-    // the MFMA operand planes of K step kt from slot `a` (LN: LayerNorm + fp16 split of the raw x in place)
-    auto operand = [&](int kt, bf16x8 (&a)[2]) __attribute__((always_inline)) {
-        if constexpr (LN) {
-            const f32x4 x0 = __builtin_bit_cast(f32x4, a[0]), x1 = __builtin_bit_cast(f32x4, a[1]);
-            int c0 = kt * BK + hsel * 8;
-            asm volatile("" : "+v"(c0));  // (keeps the gamma / beta reads in their step: hoisted, they spill)
-            typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-            h8 hi, lo;
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {  // (4 columns at a time: fewer live temporaries)
-                const f32x4 g = *reinterpret_cast<const f32x4*>(lng + c0 + 4 * half);
-                const f32x4 bb = *reinterpret_cast<const f32x4*>(lnb + c0 + 4 * half);
-                const f32x4 xv = half ? x1 : x0;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float o = ln_affine(xv[e], lsc, lbi, g[e], bb[e]);
-                    if (lrow) lnmx = fmaxf(lnmx, fabsf(o));
-                    const float t = o * p.ln_scale;
-                    hi[4 * half + e] = (_Float16)t;
-                    lo[4 * half + e] = (_Float16)(t - (float)hi[4 * half + e]);
-                }
-            }
-            a[0] = __builtin_bit_cast(bf16x8, hi);
-            a[1] = __builtin_bit_cast(bf16x8, lo);
-        }
-    };
     // one K step with the A fragments in `a`; refills go to `an` (the step PA ahead).  The W ring is retired KG
     // stages per barrier: before group kt0's barrier every wave waits for its pieces of W(kt0 .. kt0 + KG - 1) (the
     // DMA pieces certainly behind them: W(kt0 + KG .. kt0 + S - KG - 1), 2 per wave each), after it refills the KG
     // slots the previous group freed
     auto step = [&](int kt, bf16x8 (&a)[2], bf16x8 (&an)[2]) __attribute__((always_inline)) {
         if (!(QA_DIAG & 2) && kt + PA < KT) loadA(kt + PA, an);
-        operand(kt, a);
         const __bf16* Bs = reinterpret_cast<const __bf16*>(lds + (kt % S) * BSTG);
 #pragma unroll
         for (int j = 0; j < 12; ++j) {
@@ -226,9 +146,6 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
                 acc[j] = mfma16<true>(a[0], b1, acc[j]);
                 acc[j] = mfma16<true>(a[0], b0, acc[j]);
             }
-            // (LN: at most 4 tiles' fragments in flight -- with all 12 hoisted beside the LayerNorm temporaries the
-            // accumulators spilled)
-            if (LN && (j & 3) == 3) asm volatile("" ::: "memory");
         }
     };
     auto dma_after_group = [&](int kt0) {
@@ -253,7 +170,6 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
         }
     }
     __syncthreads();  // every wave is done with the ring
-    if (LN && h == 0) amax_commit(p.ln_amax, lnmx);  // (the item's 8 head workgroups form the same LayerNorm)
 
     // ---- 2. epilogue: unscale + RoPE (the GEMM's EPI_ROPE), q -> LDS, the head's max |k|, |v| -----------------
     float* Qs = reinterpret_cast<float*>(lds);  // [256][QLD]
@@ -446,7 +362,7 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
 }
 
 hipError_t launch_qkv_attention(const QkvAttnArgs& a, int items, hipStream_t s) {
-    if (items <= 0 || a.H <= 0 || a.K != 512 || (!a.Ap && !a.ln_x) || !a.Wp || !a.rope_cos || !a.rope_sin || !a.outp ||
+    if (items <= 0 || a.H <= 0 || a.K != 512 || !a.Ap || !a.Wp || !a.rope_cos || !a.rope_sin || !a.outp ||
         !(a.oscale > 0.0f) || !(a.unscale > 0.0f) || a.a_rows <= 0 || (!a.tlen && (a.Ts < 1 || a.Ts > 256)) ||
         (!a.tlen != !a.toff))
         return hipErrorInvalidValue;
@@ -454,13 +370,7 @@ hipError_t launch_qkv_attention(const QkvAttnArgs& a, int items, hipStream_t s) 
     if (a.a_rows * a.K * 2 + 256LL * a.K * 2 > 0x7fffffffLL || 2LL * 3 * a.H * 64 * a.K * 2 > 0x7fffffffLL)
         return hipErrorInvalidValue;
     const long long nwg = a.xcd ? (long long)(items + 7) / 8 * 8 * a.H : (long long)items * a.H;
-    if (a.ln_x) {
-        if (!a.ln_g || !a.ln_b || !(a.ln_scale > 0.0f) || a.a_rows * a.K * 4 + 256LL * a.K * 4 > 0x7fffffffLL)
-            return hipErrorInvalidValue;
-        hipLaunchKernelGGL((qkv_attention_h16_kernel<512, true>), dim3((unsigned)nwg), dim3(1024), 0, s, a, items);
-    } else {
-        hipLaunchKernelGGL((qkv_attention_h16_kernel<512, false>), dim3((unsigned)nwg), dim3(1024), 0, s, a, items);
-    }
+    hipLaunchKernelGGL((qkv_attention_h16_kernel<512>), dim3((unsigned)nwg), dim3(1024), 0, s, a, items);
     return hipGetLastError();
 }
 

@@ -331,6 +331,11 @@ class MimiHipModel:
         """Encodes that took the f16x3 overflow fallback (per-item re-encode, bf16x6 where an item overflows)."""
         return int(self._lib.mimi_f16_reruns(self._h))
 
+    @property
+    def rvq_chain_reruns(self) -> int:
+        """Encodes re-run on the per-level RVQ kernels because the persistent RVQ chain gave up (never returned)."""
+        return int(self._lib.mimi_rvq_chain_reruns(self._h))
+
     def set_graphs(self, enable: bool = True):
         """hipGraph replay of repeated f16x3 encode shapes (default on; identical codes, fewer launches)."""
         _lib.check(self._lib.mimi_set_graphs(self._h, int(enable)))
