@@ -101,9 +101,9 @@ def test_kernel_options_identical_codes(engine):
     workgroup form (res1_form) and every RVQ form, on a B = 16 x 10 s batch at K = 32."""
     x = torch.from_numpy(synthetic.clip_batch(16, 240000, seed=88))[:, None].cuda()
     base = engine.encode(x, num_quantizers=32).audio_codes.cpu()
-    defaults = {"sc1_out": 2, "rvq_form": 0, "rvq_chain": 1, "rvq_xcd": 1, "qkv_attn": 1,
+    defaults = {"sc1_out": 2, "rvq_form": 0, "rvq_chain": 1, "rvq_xcd": 1, "qkv_attn": 1, "res1_stream": 1,
                 "fc1_cg": 1, "res1_form": 1}
-    cases = [("res1_form", 0), ("fc1_cg", 2), ("fc1_cg", 4), ("sc1_out", 0), ("sc1_out", 7), ("rvq_chain", 0), ("rvq_xcd", 0), ("qkv_attn", 0),
+    cases = [("res1_form", 0), ("fc1_cg", 2), ("fc1_cg", 4), ("sc1_out", 0), ("sc1_out", 7), ("rvq_chain", 0), ("rvq_xcd", 0), ("qkv_attn", 0), ("res1_stream", 0),
              ("qkv_attn", 2)] + [("rvq_form", f) for f in range(1, 7)]
     for key, val in cases:
         engine.set_option(key, val)

@@ -358,6 +358,9 @@ struct mimi_engine {
     // 8-wave workgroup per CU, 1 two 4-wave workgroups per CU (each wave both 16-step tiles of its M tile; their block
     // chains interleave on the SIMDs: 0.59 -> 0.555 ms per B = 32 step, profiles/r4aa_ab_res1_form.txt)
     int res1_form = 1;
+    // stage 2's k1 conv + skip + ELU as the streaming kernel (res1_stream.hip) instead of the planes GEMM
+    // (mimi_set_option "res1_stream"; same bits): res1_s2 0.229-0.231 -> 0.218-0.221 ms per B = 32 step
+    int res1_stream = 1;
     struct Tap {
         float* d = nullptr;
         size_t cap = 0;
@@ -1472,7 +1475,10 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             if (rg) a1.a_rows = a1.m_rows = dT[si];
             yact = new_act(nmf("y%d", si));
             out_act(a1, yact);
-            LAUNCH_TRY(launch_gemm(ROLE_RES1P, a1, s, &kname, prec), "res1");
+            if (h16 && e->res1_stream && res1_stream_ok(a1))
+                LAUNCH_TRY(launch_res1_stream(a1, s, &kname), "res1 stream");
+            else
+                LAUNCH_TRY(launch_gemm(ROLE_RES1P, a1, s, &kname, prec), "res1");
             snprintf(nm, sizeof nm, "res1_s%d", si);
             rec.mark(nm, gemm_flops(a1) * rows_of(si, (double)B * T) / ((double)B * T), gemm_bytes(a1, true), kname);
         }
@@ -2419,6 +2425,7 @@ static const EngineOption kEngineOptions[] = {
     {"qkv_attn_xcd", &mimi_engine::qkv_attn_xcd, 0x3u, "0 or 1"},
     {"fc1_cg", &mimi_engine::fc1_cg, 0x17u, "0, 1, 2 or 4"},
     {"res1_form", &mimi_engine::res1_form, 0x3u, "0 or 1"},
+    {"res1_stream", &mimi_engine::res1_stream, 0x3u, "0 or 1"},
 };
 
 extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {

@@ -359,10 +359,15 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
                 return run_planes<256, 128, 4, 2, 2, 3, EPI_BIAS_ELU, 2, 12, 4, 32, 16, 0, true>(a, s);
             return run_planes_big<EPI_BIAS_ELU, 3, 2, 12>(a, s, prec);
         case ROLE_RES1P:  // K = C/2 = 128 / 256: short K, output-heavy
-            if (prec == PREC_F16X3)  // fp16: 128x128 x 8 waves on a 2-stage ring (64 KiB, two workgroups per CU):
-                                     // -18 % vs 128x64 x 4 waves (profiles/r2c_ab_dispatch.log); + 4 loader
-                                     // waves: -4..-5 % (profiles/r2e_ab_loaders_res1.log)
+            if (prec == PREC_F16X3) {  // fp16: 128x128 x 8 waves on a 2-stage ring (64 KiB, two workgroups per CU):
+                                       // -18 % vs 128x64 x 4 waves (profiles/r2c_ab_dispatch.log); + 4 loader
+                                       // waves: -4..-5 % (profiles/r2e_ab_loaders_res1.log)
+                // (round 5 A/B at B = 32 x 10 s, res1_s2 / res1_s3 ms per step, profiles/r5a_ab_res1p.txt: this tile
+                // 0.229 / 0.108; persistent + next-tile prefetch 0.263 / 0.119; 256x128 0.258 / 0.110; 128x256
+                // 0.253 / 0.111; sc1 stores 0.227 / 0.106; 3 stages 0.300 / 0.127; 64x128 0.270 / 0.129; persistent
+                // 0.264 / 0.122.  Stage 2 runs res1_stream.hip)
                 return run_planes<128, 128, 4, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13, 4, 32, 16, 0, true>(a, s);
+            }
             if (prec == PREC_BF16X6) return run_planes<128, 64, 2, 2, 3, 2, EPI_BIAS_RES_ELU, 3, 13>(a, s);
             return run_planes<128, 64, 2, 2, 2, 2, EPI_BIAS_RES_ELU, 2, 13>(a, s);
         default: return hipErrorInvalidValue;

@@ -233,6 +233,11 @@ struct GemmArgs {
     int ncg;  // planes kernels: XCD column groups of the tile order (0 / 1 none; must divide the N tiles, else none;
               // engine option fc1_cg; which workgroup computes a tile only, the same bits either way)
 };
+// Stage-2 k = 1 residual conv + skip + ELU -> y planes as a streaming kernel (res1_stream.hip): W1 register-resident
+// per wave, 16-step time tiles with the next tile's h and skip in flight; bitwise the ROLE_RES1P planes GEMM.
+// res1_stream_ok: the shapes / layouts it takes (else launch_res1_stream returns hipErrorInvalidValue).
+bool res1_stream_ok(const GemmArgs& a);
+hipError_t launch_res1_stream(const GemmArgs& a, hipStream_t s, const char** kname);
 // true when launch_gemm(role, a, precision) runs a tile with the LayerNorm prologue (a.ln_* then feed A)
 bool gemm_ln_prologue_ok(int role, const GemmArgs& a, int precision);
 
