@@ -27,6 +27,8 @@ namespace mimi {
 
 // DEPTH: register tiles in the ring (DEPTH - 1 tiles of loads in flight under a tile's compute); CPW: output
 // channels per wave (CT = CPW / 16 channel tiles; a lane owns CPW / 4 consecutive channels of one step)
+constexpr int R1S_MAXB = 256;  // ragged batches: items the in-kernel tile table holds (more: the planes GEMM runs)
+
 template <int K, int DEPTH, int CPW>
 __global__ __launch_bounds__(2 * K / CPW * 64) void res1_stream_kernel(GemmArgs p, int ntiles) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -60,13 +62,44 @@ __global__ __launch_bounds__(2 * K / CPW * 64) void res1_stream_kernel(GemmArgs 
     const __amdgpu_buffer_rsrc_t h0 = make_rsrc(p.Ap, rows * K * 2);
     const __amdgpu_buffer_rsrc_t h1 = make_rsrc(reinterpret_cast<const _Float16*>(p.Ap) + p.a_pstride, rows * K * 2);
     const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.R, rows * N * 4);
+    // ragged batches: only the items' valid 16-step tiles (item b's ceil(m_rows[b] / 16) tiles from tst[b]), so the
+    // padding rows cost nothing (a walk over all batch x M rows read and skipped them: YODAS2-style batches +28 %)
+    __shared__ int tst[R1S_MAXB + 1];
+    if (p.m_rows) {
+        if (tid == 0) {
+            int acc = 0;
+            for (int b = 0; b < p.batch; ++b) {
+                tst[b] = acc;
+                acc += (p.m_rows[b] + 15) >> 4;
+            }
+            tst[p.batch] = acc;
+        }
+        __syncthreads();
+        ntiles = tst[p.batch];
+    }
+    // a tile's first row and (ragged) its item's valid steps from there
+    auto tile_at = [&](int tile, int& lim) -> long long {
+        if (!p.m_rows) {
+            lim = 16;
+            return (long long)tile * 16;
+        }
+        int lo = 0, hi = p.batch - 1;  // the last item whose first tile is <= tile
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (tst[mid] <= tile) lo = mid; else hi = mid - 1;
+        }
+        const int tt = tile - tst[lo];
+        lim = p.m_rows[lo] - 16 * tt;
+        return (long long)lo * p.M + 16 * tt;
+    };
 
     struct Tile {
         h8 b[KS][2];  // h fragments (B operand): step l16 of the tile, k chunk 8 q of each K step
         f32x4 r[CT];  // skip x: channels cl .. cl + LC - 1 of step l16
     };
     auto load = [&](int tile, Tile& t) {
-        const long long row = (long long)tile * 16 + l16;  // (past the rows: the buffer range check loads 0)
+        int lim;
+        const long long row = tile_at(tile, lim) + l16;  // (past the rows: the buffer range check loads 0)
         const int ho = (int)((row * K + 8 * q) * 2);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -92,12 +125,10 @@ __global__ __launch_bounds__(2 * K / CPW * 64) void res1_stream_kernel(GemmArgs 
                 acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ct][ks][1], t.b[ks][0], acc[ct], 0, 0, 0);
                 acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ct][ks][0], t.b[ks][0], acc[ct], 0, 0, 0);
             }
-        const long long row = (long long)tile * 16 + l16;
-        bool ok = row < rows;
-        if (ok && p.m_rows) {  // ragged: the item's valid steps only (its rows past them are never stored)
-            const long long b = row / p.M;
-            ok = row - b * p.M < p.m_rows[b];
-        }
+        int lim;
+        const long long row = tile_at(tile, lim) + l16;
+        const bool ok = row < rows && l16 < lim;  // (ragged: the item's valid steps only -- its rows past them are
+                                                  // never stored)
         if (ok) {
 #pragma unroll
             for (int g = 0; g < LC / 8; ++g) {
@@ -141,6 +172,7 @@ bool res1_stream_ok(const GemmArgs& a) {
     return a.K == 128 && a.N == 256 && a.Ap && a.Wsplit && a.R && a.Cp && !a.C && a.bias && a.out_amax &&
            a.a_rs == a.K && a.a_cin == a.K && a.a_off == 0 && a.ldc == a.N && a.a_bstride == (long long)a.M * a.K &&
            a.c_bstride == (long long)a.M * a.N && !a.a_boff && !a.c_boff && (!a.m_rows == !a.a_rows) &&
+           (!a.m_rows || a.batch <= R1S_MAXB) &&
            (long long)a.M * a.batch * a.N * 4 < 0x7fffffffLL && a.out_scale > 0.0f && a.unscale > 0.0f;
 }
 
