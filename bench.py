@@ -51,6 +51,7 @@ for _p in (os.path.join(ROOT, "tokenize-audio_amd"), ROOT):
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 MFMA/vector peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec
+HBM_ACHIEVABLE_GBS = 6300.0  # MI355X_MICROARCH.md §HBM: 8 TB/s spec, ~6.3 TB/s achievable
 BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak
 F16X3_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 3  # fp32-accurate products as 3 fp16 products
 DTYPE_LABEL = {
@@ -264,6 +265,21 @@ def north_star_groups(prof, steps, pmc, pmc_note=None):
             by = sum(b * prof[s]["launches"] / steps for (b, _, _), s in zip(looked, stages))
             d.update({"hbm_bytes_per_step": round(by), "hbm_GBps": round(by / (ms / 1e3) / 1e9, 1),
                       "frac_hbm_peak": round(by / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)})
+        if g == "conv_stack":
+            # the north star's HBM-bound layers (k = 1 residual convs of stages 2-3, and the fused stage-1 block that
+            # holds stage 1's), each on its own: PMC bytes per launch / its event time, against the 8 TB/s spec and
+            # the ~6.3 TB/s MI355X_MICROARCH.md reports achievable
+            per = {}
+            for s, (b, _, _) in zip(stages, looked):
+                if base(s) not in ("res1_s2", "res1_s3", "res_s1") or b is None:
+                    continue
+                t = prof[s]["ms"] / 1e3 / prof[s]["launches"]
+                per[base(s)] = {"kernel": prof[s]["kernel"], "hbm_bytes_per_launch": round(b),
+                                "ms_per_launch": round(1e3 * t, 4), "hbm_GBps": round(b / t / 1e9, 1),
+                                "frac_hbm_peak": round(b / t / 1e9 / HBM_PEAK_GBS, 4),
+                                "frac_hbm_achievable": round(b / t / 1e9 / HBM_ACHIEVABLE_GBS, 4)}
+            if per:
+                d["hbm_bound_layers"] = per
         out[g] = d
     return out
 
