@@ -16,3 +16,10 @@ for i in 1 2; do
     done
   done
 done
+for i in 1 2; do
+  for v in new geludiag; do
+    if [ $v = geludiag ]; then export MIMI_HIP_LIB=$PWD/ab/libmimi_hip_geludiag.so; else unset MIMI_HIP_LIB; fi
+    timeout -k 10 200 python -u bench.py --steps 20 --cpu-baseline-seconds 0 --no-f32-mode --pmc-pass --json-out $O/b32_${v}_$i.json > $O/b32_${v}_$i.log 2>&1 || { tail -5 $O/b32_${v}_$i.log; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/b32_${v}_$i.json')); s=d['stages_ms_per_step']; print('b32 $v', d['value'], d['ms_per_step'], 'fc1', s.get('fc1'), 'fc2', s.get('fc2'))"
+  done
+done
