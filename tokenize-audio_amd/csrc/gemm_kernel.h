@@ -11,7 +11,11 @@ __device__ __forceinline__ float elu1(float x) { return elu_fast(x); }
 
 // torch CPU GELU(approximate='none'): (x * 0.5) * (1 + erf(x * M_SQRT1_2))
 __device__ __forceinline__ float gelu_erf(float x) {
+#ifdef MIMI_GELU_DIAG  // timing diagnostic builds only (results wrong): the epilogue without erf
+    return (x * 0.5f) * (1.0f + x * 0.70710678118654752440f);
+#else
     return (x * 0.5f) * (1.0f + erff(x * 0.70710678118654752440f));
+#endif
 }
 
 // RoPE rotate-half of the pair (x1 = dim d, x2 = dim d + 32), d < 32 (TF/modeling_mimi.py:384-404): the q/k/v
