@@ -51,11 +51,13 @@ for d in sorted(glob.glob(os.path.join(root, "p*"))):
             acc[1] += dur[did]
             acc[2] += c.get("SQ_VALU_MFMA_BUSY_CYCLES", float("nan"))
             acc[3] += 1
+MIN_CLOCK_MS = 0.3  # shorter dispatches: the GRBM-based clock (and the mfma% built on it) is not meaningful
 mean = lambda v: sum(v) / len(v) if v else float("nan")  # noqa: E731
 print(__doc__.strip().splitlines()[0])
-print("clock = sum GRBM_GUI_ACTIVE / 8 / sum duration over the same dispatches of one pass (reads high below ~0.3 ms "
-      "per dispatch, MI355X_MICROARCH.md 'DVFS'); mfma% = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) "
-      "of the pass that collected it")
+print("clock = sum GRBM_GUI_ACTIVE / 8 / sum duration over the same dispatches of one pass; mfma% = "
+      "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) of the pass that collected it.  Both are printed "
+      f"only for kernels whose mean dispatch is >= {MIN_CLOCK_MS} ms: below that GRBM_GUI_ACTIVE over the dispatch "
+      "duration reads above the chip's 2.4 GHz (MI355X_MICROARCH.md 'DVFS'), so neither number is evidence there ('-')")
 print(f"{'kernel':78s} {'wait':>5s} {'stall':>5s} {'activ':>5s} {'ldsst':>5s} {'GHz':>5s} {'mfma%':>5s} {'ldsconf':>9s} "
       f"{'ms':>7s}")
 for k, c in sorted(per.items(), key=lambda kv: -mean(kv[1].get("SQ_WAVE_CYCLES", [0]))):
@@ -70,6 +72,10 @@ for k, c in sorted(per.items(), key=lambda kv: -mean(kv[1].get("SQ_WAVE_CYCLES",
     mparts = [p for p in parts if p[2] == p[2]]
     mf = (sum(p[2] for p in mparts) / (1024 * sum(p[0] for p in mparts) / 8)
           if mparts and sum(p[0] for p in mparts) > 0 else float("nan"))
+    ms = 1e3 * t / n if n else float("nan")
+    ok = ms >= MIN_CLOCK_MS
+    ghz = f"{clk:5.2f}" if ok else f"{'-':>5s}"
+    mfp = f"{100 * mf:5.1f}" if ok else f"{'-':>5s}"
     print(f"{k[:78]:78s} {mean(c['SQ_WAIT_ANY'])/wc:5.2f} {mean(c['SQ_WAIT_INST_ANY'])/wc:5.2f} "
-          f"{mean(c['SQ_ACTIVE_INST_ANY'])/wc:5.2f} {mean(c['SQ_WAIT_INST_LDS'])/wc:5.3f} {clk:5.2f} {100*mf:5.1f} "
-          f"{mean(c['SQ_LDS_BANK_CONFLICT']):9.3g} {1e3 * t / n if n else float('nan'):7.3f}")
+          f"{mean(c['SQ_ACTIVE_INST_ANY'])/wc:5.2f} {mean(c['SQ_WAIT_INST_LDS'])/wc:5.3f} {ghz} {mfp} "
+          f"{mean(c['SQ_LDS_BANK_CONFLICT']):9.3g} {ms:7.3f}")
