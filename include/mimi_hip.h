@@ -111,6 +111,16 @@ int mimi_encode_async(mimi_engine* e, const float* dev_audio, int32_t batch, int
 int mimi_encode_wait(mimi_engine* e, int64_t ticket);
 
 /*
+ * mimi_encode from and to HOST memory in one call: host_audio f32 [batch][length] (any host memory), host_codes
+ * int32 [batch][num_quantizers][mimi_encoded_length(length)].  The engine copies the audio to its own device buffer,
+ * encodes and copies the codes back on `stream`, synchronising the host once -- the per-utterance caller's path
+ * (MimiEncoder.encode_audio_chunk once per utterance: librispeech-mimi/process_librispeech_dev-test.py:136-141,
+ * mls-en-mimi-pretrain/process_shard.py:302-307) without a framework tensor per step.  Same codes as mimi_encode.
+ */
+int mimi_encode_host(mimi_engine* e, const float* host_audio, int32_t batch, int64_t length, int32_t num_quantizers,
+                     int32_t* host_codes, void* stream);
+
+/*
  * Ragged batch: item b's samples are dev_audio[b][0 .. lengths[b]) (rows max_length apart; samples past lengths[b]
  * are never read), lengths a HOST int64 array, 1 <= lengths[b] <= max_length.  Each item is encoded exactly as
  * mimi_encode(dev_audio[b], 1, lengths[b], ...) would encode it alone -- its codes, frames [0,
@@ -181,7 +191,8 @@ int64_t mimi_graph_replays(const mimi_engine* e);
  * chain gave up), "rvq_chain_fault" 0/1/2 (tests only: 1 = zero spin budget, 2 = every sweep gives up), "rvq_xcd"
  * 0/1.  "sc1_out" 0-7 (sc1 output stores: bit 0 q/k/v, 1 fc1 (default 2), 2 o_proj + fc2), "ln_rpw" 0/1/2/4/8
  * (LayerNorm rows per wave), "fc1_cg" 0/1/2/4 (fc1's tile order in XCD column groups, default 1 = none), "res1_form"
- * 0/1 (stage-1 block as one 8-wave or two 4-wave workgroups per CU, default 1).  Unknown keys and values:
+ * 0/1 (stage-1 block as one 8-wave or two 4-wave workgroups per CU, default 1), "res1_stream" 0/1 (stage 2's k = 1
+ * residual conv as the streaming kernel with register-resident weights, default 1).  Unknown keys and values:
  * MIMI_ERR_INVALID_ARGUMENT.  A change drops the captured graphs. */
 int mimi_set_option(mimi_engine* e, const char* key, int64_t value);
 /* MIMI_PRECISION_F16X3 diagnostics: per plane tensor (64-char names), its fixed activation scale and the max|x|

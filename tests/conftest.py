@@ -75,6 +75,7 @@ def _codes_range_guard():
 
     wrap(M, "encode", lambda self, out: assert_codes_in_range(out[0]))
     wrap(M, "encode_int32", lambda self, out: assert_codes_in_range(out))
+    wrap(M, "encode_host", lambda self, out: assert_codes_in_range(out))
     wrap(M, "quantize", lambda self, out: assert_codes_in_range(out))
     # tickets of full (non-ragged) encodes: a ragged output's frames past an item's own are unspecified
     orig_async = M.encode_async

@@ -293,6 +293,16 @@ struct mimi_engine {
     };
     static constexpr int kMaxPending = 16;
     Pending pend[kMaxPending];
+    // mimi_encode_host's buffers: one set per concurrent caller, claimed under mu, grown on demand
+    struct HostIo {
+        bool busy = false;
+        float* d_audio = nullptr;
+        size_t audio_cap = 0;        // bytes
+        int32_t* d_codes = nullptr;
+        int32_t* h_codes = nullptr;  // pinned
+        size_t codes_cap = 0;        // bytes (both code buffers)
+    };
+    HostIo hostio[kMaxPending];
     int64_t next_ticket = 1;
     size_t item_codes_cap = 0;
     int f16_reruns = 0;             // encodes that took the overflow fallback (diagnostic)
@@ -2308,6 +2318,92 @@ extern "C" int mimi_encode(mimi_engine* e, const float* audio, int32_t batch, in
     return encode_wait(e, ticket);
 }
 
+// Host audio in, host codes out (the per-utterance callers' path: MimiEncoder.encode_audio_chunk once per utterance,
+// `librispeech-mimi/process_librispeech_dev-test.py:136-141`, `mls-en-mimi-pretrain/process_shard.py:302-307`).  The
+// same encode as mimi_encode on a device copy of the audio, with no framework tensors around it: the H2D copy, the
+// encode and the codes' D2H into pinned memory are enqueued on `stream` in one call and the host synchronises once
+// (twice when the encode had to be re-run: a chain give-up or an f16x3 overflow re-encodes on the stream inside
+// mimi_encode_wait, after which the codes are copied again).
+static int host_io_grow(mimi_engine::HostIo* io, size_t ab, size_t cb) {
+    if (io->audio_cap < ab) {
+        if (io->d_audio) HIP_TRY(hipFree(io->d_audio));  // (hipFree waits for the device)
+        io->d_audio = nullptr;
+        io->audio_cap = 0;
+        const size_t cap = std::max(ab, (size_t)1 << 22);
+        HIP_TRY(hipMalloc(&io->d_audio, cap));
+        io->audio_cap = cap;
+    }
+    if (io->codes_cap < cb) {
+        if (io->d_codes) HIP_TRY(hipFree(io->d_codes));
+        if (io->h_codes) HIP_TRY(hipHostFree(io->h_codes));
+        io->d_codes = nullptr;
+        io->h_codes = nullptr;
+        io->codes_cap = 0;
+        const size_t cap = std::max(cb, (size_t)1 << 16);
+        HIP_TRY(hipMalloc(&io->d_codes, cap));
+        HIP_TRY(hipHostMalloc(&io->h_codes, cap, hipHostMallocDefault));
+        io->codes_cap = cap;
+    }
+    return MIMI_OK;
+}
+
+extern "C" int mimi_encode_host(mimi_engine* e, const float* host_audio, int32_t batch, int64_t length, int32_t K,
+                                int32_t* host_codes, void* stream) {
+    int rc = check_encode_args(e, host_audio, batch, length, &K, host_codes);
+    if (rc) return rc;
+    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const size_t ab = (size_t)batch * (size_t)length * sizeof(float);
+    const size_t cb = (size_t)batch * K * (size_t)mimi_encoded_length_cfg(&e->cfg, length) * sizeof(int32_t);
+    mimi_engine::HostIo* io = nullptr;
+    int64_t ticket = 0, reruns = 0;
+    {
+        std::lock_guard<std::mutex> lk(e->mu);
+        HIP_TRY(hipSetDevice(e->device));
+        (void)hipGetLastError();
+        for (auto& h : e->hostio)
+            if (!h.busy) {
+                io = &h;
+                break;
+            }
+        if (!io)
+            return set_err(MIMI_ERR_STATE, "%d host encodes in flight", mimi_engine::kMaxPending);
+        if ((rc = host_io_grow(io, ab, cb))) return rc;
+        const hipError_t ce = hipMemcpyAsync(io->d_audio, host_audio, ab, hipMemcpyHostToDevice, s);
+        if (ce != hipSuccess) rc = set_err(MIMI_ERR_HIP, "mimi_encode_host: H2D copy: %s", hipGetErrorString(ce));
+        if (!rc) rc = encode_async_locked(e, io->d_audio, batch, length, K, io->d_codes, s, &ticket);
+        if (rc) {
+            (void)hipStreamSynchronize(s);  // (the slot stays free: nothing of this call is left in flight)
+            return rc;
+        }
+        io->busy = true;  // (from here on every exit path releases it)
+        reruns = e->chain_reruns + e->f16_reruns;
+        const hipError_t de = hipMemcpyAsync(io->h_codes, io->d_codes, cb, hipMemcpyDeviceToHost, s);
+        if (de != hipSuccess) rc = set_err(MIMI_ERR_HIP, "mimi_encode_host: D2H copy: %s", hipGetErrorString(de));
+    }
+    const int wrc = encode_wait(e, ticket);  // (always: it frees the ticket)
+    if (!rc) rc = wrc;
+    if (!rc) {
+        bool again;
+        {
+            std::lock_guard<std::mutex> lk(e->mu);
+            again = e->chain_reruns + e->f16_reruns != reruns;  // (another thread's re-run only costs a copy)
+        }
+        hipError_t he = hipSuccess;
+        if (again) he = hipMemcpyAsync(io->h_codes, io->d_codes, cb, hipMemcpyDeviceToHost, s);
+        if (he == hipSuccess) he = hipStreamSynchronize(s);
+        if (he != hipSuccess)
+            rc = set_err(he == hipErrorOutOfMemory ? MIMI_ERR_OUT_OF_MEMORY : MIMI_ERR_HIP, "mimi_encode_host: %s",
+                         hipGetErrorString(he));
+        else
+            std::memcpy(host_codes, io->h_codes, cb);
+    } else {
+        (void)hipStreamSynchronize(s);  // the buffers are reused: nothing of this call may still be in flight
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    io->busy = false;
+    return rc;
+}
+
 extern "C" int mimi_rvq_encode(mimi_engine* e, const float* emb, int64_t frames, int32_t K, int32_t* codes,
                                void* stream) {
     if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
@@ -2371,6 +2467,11 @@ extern "C" void mimi_destroy(mimi_engine* e) {
         if (q.amax) (void)hipHostFree(q.amax);
         if (q.rg_pinned) (void)hipHostFree(q.rg_pinned);
         if (q.chain_word) (void)hipHostFree(q.chain_word);
+    }
+    for (auto& h : e->hostio) {
+        if (h.d_audio) (void)hipFree(h.d_audio);
+        if (h.d_codes) (void)hipFree(h.d_codes);
+        if (h.h_codes) (void)hipHostFree(h.h_codes);
     }
     drop_graphs(e);
     if (e->io_dev) (void)hipFree(e->io_dev);

@@ -24,7 +24,7 @@ STATUS_NAMES = {
 # every symbol include/mimi_hip.h declares (tests check the library exports exactly these)
 EXPORTED_SYMBOLS = (
     "mimi_config_default", "mimi_create", "mimi_set_weight", "mimi_load_safetensors", "mimi_finalize",
-    "mimi_encode", "mimi_encode_async", "mimi_encode_wait", "mimi_encode_ragged", "mimi_encode_ragged_async", "mimi_rvq_encode", "mimi_set_precision", "mimi_get_precision", "mimi_calibrate", "mimi_f16_reruns", "mimi_rvq_chain_reruns", "mimi_set_graphs", "mimi_graph_replays", "mimi_set_option", "mimi_act_scales", "mimi_encoded_length",
+    "mimi_encode", "mimi_encode_async", "mimi_encode_wait", "mimi_encode_host", "mimi_encode_ragged", "mimi_encode_ragged_async", "mimi_rvq_encode", "mimi_set_precision", "mimi_get_precision", "mimi_calibrate", "mimi_f16_reruns", "mimi_rvq_chain_reruns", "mimi_set_graphs", "mimi_graph_replays", "mimi_set_option", "mimi_act_scales", "mimi_encoded_length",
     "mimi_encoded_length_cfg",
     "mimi_workspace_bytes", "mimi_destroy", "mimi_last_error", "mimi_set_profiling", "mimi_profile_read",
     "mimi_profile_reset", "mimi_profile_sequence", "mimi_set_taps", "mimi_get_tap", "mimi_resample_poly",
@@ -83,6 +83,7 @@ def _declare(lib):
         "mimi_encode": (c.c_int, [vp, vp, c.c_int32, c.c_int64, c.c_int32, vp, vp]),
         "mimi_encode_async": (c.c_int, [vp, vp, c.c_int32, c.c_int64, c.c_int32, vp, vp, c.POINTER(c.c_int64)]),
         "mimi_encode_wait": (c.c_int, [vp, c.c_int64]),
+        "mimi_encode_host": (c.c_int, [vp, vp, c.c_int32, c.c_int64, c.c_int32, vp, vp]),
         "mimi_encode_ragged": (c.c_int, [vp, vp, vp, c.c_int32, c.c_int64, c.c_int32, vp, vp]),
         "mimi_encode_ragged_async": (c.c_int, [vp, vp, vp, c.c_int32, c.c_int64, c.c_int32, vp, vp,
                                                c.POINTER(c.c_int64)]),

@@ -184,6 +184,9 @@ class MimiEncoder:
     def encode_audio_chunk(self, audio_array: np.ndarray, sample_rate: int = 24000) -> np.ndarray:
         with torch.no_grad():
             (a,) = self._check([audio_array], sample_rate)
+            if a.shape[0] and hasattr(self.model, "encode_host"):
+                # one utterance needs no padding: host samples in, host codes out in one engine call
+                return self.model.encode_host(a[None], self._K)[0].astype(np.int64)
             return self._encode_padded([a])[0].astype(np.int64)
 
     def _batch_plan(self, items: List[np.ndarray], sample_rate: int):

@@ -263,6 +263,20 @@ class MimiHipModel:
                                          ctypes.c_void_p(out.data_ptr()), self._stream()))
         return out
 
+    def encode_host(self, audio: np.ndarray, num_quantizers: int) -> np.ndarray:
+        """Host f32 [B, L] in, host int32 [B, K, T] out, in one C call (``mimi_encode_host``: the engine's own device
+        and pinned buffers, one host synchronisation) on the current stream -- the per-utterance path of
+        ``MimiEncoder.encode_audio_chunk``.  The same codes as ``encode_int32`` on a device copy."""
+        K = self._check_k(num_quantizers)
+        a = np.ascontiguousarray(audio, dtype=np.float32)
+        if a.ndim != 2 or a.shape[0] < 1 or a.shape[1] < 1:
+            raise ValueError(f"audio must be a non-empty [batch, length] array, got {tuple(a.shape)}")
+        B, L = a.shape
+        out = np.empty((B, K, encoded_length(L, self.config)), dtype=np.int32)
+        _lib.check(self._lib.mimi_encode_host(self._h, ctypes.c_void_p(a.ctypes.data), B, L, K,
+                                              ctypes.c_void_p(out.ctypes.data), self._stream()))
+        return out
+
     def encode_async(self, audio: torch.Tensor, num_quantizers: int, out: Optional[torch.Tensor] = None
                      ) -> "EncodeTicket":
         """Enqueue an encode of device f32 [B, L] on the current stream and return without waiting
