@@ -357,6 +357,7 @@ struct mimi_engine {
     // 256 (item, head) pairs (one workgroup per CU), 2 whenever the items fit (mimi_set_option "qkv_attn"; same bits)
     int qkv_attn = 1;
     int qkv_attn_xcd = 1;  // its workgroups: an item's heads on one XCD (mimi_set_option "qkv_attn_xcd"; same bits)
+    int attn_band_split = 1;  // items over 256 frames: the banded attention's decomposition (0 / 1 auto / 2; same bits)
     // transformer GEMMs with sc1 output stores (gemm_planes.h FL_SC1OUT; mimi_set_option "sc1_out"): bit 0 q/k/v,
     // bit 1 fc1, bit 2 o_proj and fc2 (large batches; the same bits either way)
     int sc1_out = 2;  // (A/B, round 4: fc1 0.594 -> 0.576 ms per B = 32 step; q/k/v, o_proj and fc2 slower with it)
@@ -1643,13 +1644,13 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             // fp16-plane attention in f16x3 mode (also for the no-plane long clips: the same arithmetic as their
             // prefixes); true fp32 in f32 mode and the bf16 modes
             const bool ah16 = prec == PREC_F16X3;
+            const char* akn = ah16 ? (T <= 256 ? "mimi::attention_t256_h16_kernel" : "mimi::attention_band_h16_kernel")
+                                   : (T <= 256 ? "mimi::attention_t256_kernel" : "mimi::attention_kernel");
             LAUNCH_TRY(launch_attention(w.qkv, w.att, B, (int)T, H, Dh, c.sliding_window, 1.0f / std::sqrt((float)Dh),
                                         s, w.att, nact, ns, atta.scale, atta.amax, ah16, rg ? dT25 : nullptr,
-                                        rg ? rg->maxT25 : 0, rg ? rg->minT25 : 0, dToff),
+                                        rg ? rg->maxT25 : 0, rg ? rg->minT25 : 0, dToff, &akn, e->attn_band_split),
                        "attention");
-            rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4,
-                     ah16 ? (T <= 256 ? "mimi::attention_t256_h16_kernel" : "mimi::attention_band_h16_kernel")
-                         : (T <= 256 ? "mimi::attention_t256_kernel" : "mimi::attention_kernel"));
+            rec.mark("attention", att_flops, (double)rows * 4 * Hd * 4, akn);
         }
         if ((rc = save_tap_planes(e, nmf("att%d", l).c_str(), w.att, ns, tapB, tapT, H * Dh, s, atta.scale))) return rc;
         GemmArgs ao = linear_args(w.att, rows, H * Dh, x.wo, Hd, w.t0);
@@ -2524,6 +2525,7 @@ static const EngineOption kEngineOptions[] = {
     {"ln_fused", &mimi_engine::ln_fused, 0x1fu, "0 .. 4"},
     {"qkv_attn", &mimi_engine::qkv_attn, 0x7u, "0, 1 or 2"},
     {"qkv_attn_xcd", &mimi_engine::qkv_attn_xcd, 0x3u, "0 or 1"},
+    {"attn_band_split", &mimi_engine::attn_band_split, 0x7u, "0, 1 or 2"},
     {"fc1_cg", &mimi_engine::fc1_cg, 0x17u, "0, 1, 2 or 4"},
     {"res1_form", &mimi_engine::res1_form, 0x3u, "0 or 1"},
     {"res1_stream", &mimi_engine::res1_stream, 0x3u, "0 or 1"},

@@ -340,7 +340,7 @@ hipError_t launch_layernorm(const float* x, const float* g, const float* b, floa
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window,
                             float scale, hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
                             unsigned* oamax, bool h16, const int* tlen = nullptr, int max_tlen = 0, int min_tlen = 0,
-                            const int* toff = nullptr);
+                            const int* toff = nullptr, const char** kname = nullptr, int band_split_mode = 1);
 
 // Replicate-padding fix of the downsample conv (k = 4, s = 2) run as a zero-padded planes GEMM: per item,
 // out[0] += (W_0 + W_1) . x[0] (the 2 left pad rows replicate x[0]) and, when T is odd (one right "extra" pad
@@ -354,9 +354,11 @@ hipError_t launch_ds_edge_fix(const float* x, const float* wfix, float* out, voi
 // ragged batches with packed transformer rows: rpos[toff[b] + t] = t for t < tlen[b]
 hipError_t launch_ragged_rows(const int* tlen, const int* toff, int B, int* rpos, hipStream_t s);
 
-// the banded fp16-plane attention at any T (tools/attn_check.hip compares it with the T <= 256 kernel)
+// the banded fp16-plane attention at any T (tools/attn_check.hip compares it with the T <= 256 kernel); split: its
+// decomposition (0 = 128-query workgroups, 1 = by grid size, 2 = one 32-query tile per workgroup; same values)
 hipError_t launch_attention_band(const float* qkv, int batch, int T, int H, int window, float scale,
-                                 hipStream_t s, void* outp, long long out_pstride, float oscale, unsigned* oamax);
+                                 hipStream_t s, void* outp, long long out_pstride, float oscale, unsigned* oamax,
+                                 int split = 1);
 
 // Fused q/k/v projection + RoPE + attention for items of at most 256 frames (qkv_attn.hip): one workgroup per
 // (item, head) computes the head's 192 q/k/v columns of the item's rows on the fp16 planes (the q/k/v GEMM's

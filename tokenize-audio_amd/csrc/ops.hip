@@ -665,52 +665,155 @@ static int attn_qg(int batch, int H) {
     return pairs >= 256 ? 1 : pairs >= 128 ? 2 : 4;
 }
 
-// T > 256 (clips over 10.24 s) on the fp16 matrix cores: a workgroup = 128 queries of one (batch item, head), 4
-// waves x 32 queries.  The keys of its band [q0 - W + 1, q0 + 127] stream through LDS in 32-key chunks as fp16
-// planes of the K rows and of V^T (chunk c + 1's rows load into registers while chunk c is computed), with the
-// chunk math of attention_t256_h16_kernel (attn_chunk_h16).  Scales are powers of two: per chunk for K (each
-// chunk's S^T is formed from scratch, so it is unscaled by that chunk's 1 / (sK sQ)), per wave for Q; V's scale
-// follows the largest chunk seen so far: when a chunk needs a smaller scale the O^T accumulator is rescaled by the
-// ratio (exact: powers of two, folded into the online-softmax correction) and later smaller-valued chunks put the
-// ratio on P instead (P s <= 2^14).  Every scale depends on this item's own q/k/v only.
-__global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __restrict__ qkv, float* __restrict__ out,
-                                                                 int Ts, int H, int window, float scale,
-                                                                 void* __restrict__ outp, long long pstride, int outns,
-                                                                 float oscale, unsigned* __restrict__ oamax,
-                                                                 const int* __restrict__ tlen,
-                                                                 const int* __restrict__ toff) {
-    constexpr int D = 64, KC = 32, LDO = D + 1;
-    constexpr int KLD = 72, KPL = KC * KLD;  // K planes: [32 keys][72 halves] (conflict-free b128 fragment reads)
-    constexpr int VLD = 40, VPL = D * VLD;   // V^T planes: [64 dims][40 halves]
-    constexpr int CH = 2 * KPL + 2 * VPL;    // halves of one chunk image
-    constexpr int OST = 4 * 32 * LDO * 2;    // halves of the output staging (fp32, 4 waves x 32 x 65)
-    __shared__ __attribute__((aligned(16))) _Float16 lds[CH > OST ? CH : OST];
-    __shared__ float red[2][4];
-    _Float16* Ks = lds;
-    _Float16* Vt = lds + 2 * KPL;
-    const int b = blockIdx.z, h = blockIdx.y;
-    // Ts: the row stride; T: this item's frames (ragged batches: items of <= 256 frames run the T <= 256 kernel)
-    const int T = tlen ? tlen[b] : Ts;
-    const int q0 = blockIdx.x * 128;
-    if (tlen && (T <= 256 || q0 >= T)) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int hf = lane >> 5, col = lane & 31;
-    const long long ld = 3LL * H * D;
-    const long long row0 = toff ? (long long)toff[b] : (long long)b * Ts;  // the item's first row (toff: packed rows)
-    const float* base = qkv + row0 * ld;
-    const int qw = q0 + 32 * wave, qi = qw + col;
-    const int kstart = max(0, q0 - window + 1) & ~31;
-    const int kend = min(T - 1, q0 + 127);        // the workgroup's last key
-    const int kend_w = min(T - 1, qw + 31);       // this wave's
-    // Q planes (as attention_t256_h16_kernel)
+// T > 256 (clips over 10.24 s) on the fp16 matrix cores, in a form whose every output is the same arithmetic however
+// the work is split across workgroups.  The keys of a 32-query tile's band [q0 - W + 1, q0 + 31] are visited as whole
+// 32-key chunks c (keys 32 c .. 32 c + 31), and each chunk's contribution is formed on its own (attn_band_scores,
+// attn_band_pv):
+//   K / V fp16 planes at power-of-two scales from THAT chunk's max |K|, |V| over its keys < T (never zeroed at a
+//   workgroup's band end), S^T = K . Q^T on the planes (Q planes at the tile's own power-of-two scale), the masked
+//   chunk max m_c, p = exp(s - m_c), l_c = sum p, O_c^T = V^T . P^T on the planes, unscaled exactly;
+// and the tile's state folds the chunks in ascending order (attn_band_coef / _apply: m = max(m, m_c), o = o a + o_c b,
+// l = l a + l_c b, a = exp(m_old - m), b = exp(m_c - m)); out = o / l.  Two decompositions of that same arithmetic:
+//   SPLIT = false (large grids): a workgroup = 128 queries x 4 waves sharing each chunk image (one chunk per barrier
+//                 pair, K / V rows of chunk c + 1 in registers while chunk c is computed), every wave folds the
+//                 chunks of its own tile in order;
+//   SPLIT = true  (small grids: a batch-1 utterance has 8 x ceil(T / 128) such workgroups for 256 CUs): a workgroup
+//                 = ONE 32-query tile x 4 waves; in round r wave w forms chunk cs + 4 r + w into its own LDS image,
+//                 waves 1-3 hand their partials to wave 0 through LDS (double-buffered by round), wave 0 folds the
+//                 round's chunks in ascending order -- a tile's chain of up to 10 dependent chunk steps becomes 3.
+// Every value either form produces is the same bit for bit (tests/test_attention_band.py), so the engine picks the
+// form by grid size without an utterance's codes depending on its batch.
+namespace {
+constexpr int BD = 64, BKC = 32, BLDO = BD + 1;
+constexpr int BKLD = 72, BKPL = BKC * BKLD;  // K planes: [32 keys][72 halves] (conflict-free b128 fragment reads)
+constexpr int BVLD = 40, BVPL = BD * BVLD;   // V^T planes: [64 dims][40 halves]
+constexpr int BCH = 2 * BKPL + 2 * BVPL;     // halves of one chunk image
+}  // namespace
+
+// One chunk's scores for the wave's 32 queries (lane: query col, half hf): S^T = K . Q^T on the planes, the mask,
+// the chunk's own max mc and p = exp(s - mc) as fp16 planes at 2^14 (pp0 / pp1: keys 16 ks .. of the chunk in the
+// S^T accumulator's order), lc = sum p.  us = 1 / (sK sQ).
+__device__ __forceinline__ void attn_band_scores(f16x8 (&pp0)[2], f16x8 (&pp1)[2], float& mc, float& lc,
+                                                 const f16x8 (&qf)[4][2], const _Float16* Kc, int c0, int qw, int qi,
+                                                 int T, int window, int hf, int col, float us) {
+    f32x16 st;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+        const int ko = col * BKLD + 16 * ks + 8 * hf;
+        const f16x8 k0 = *reinterpret_cast<const f16x8*>(Kc + ko);
+        const f16x8 k1 = *reinterpret_cast<const f16x8*>(Kc + BKPL + ko);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, qf[ks][0], st, 0, 0, 0);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, qf[ks][1], st, 0, 0, 0);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, qf[ks][0], st, 0, 0, 0);
+    }
+    float cmax = -INFINITY;
+    const bool full = c0 + 31 <= qw && c0 > qw + 31 - window && c0 + 31 < T;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        float v = st[r] * us;
+        if (!full) {
+            const int key = c0 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+            const bool ok = key <= qi && key > qi - window && key < T;
+            v = ok ? v : -INFINITY;
+        }
+        st[r] = v;
+        cmax = fmaxf(cmax, v);
+    }
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
+    mc = cmax;
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float pv = (st[r] == -INFINITY) ? 0.f : __expf(st[r] - cmax);
+        st[r] = pv;
+        psum += pv;
+    }
+    psum += __shfl_xor(psum, 32);
+    lc = psum;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        float pe[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pe[e] = st[8 * ks + e];
+        split8_h(pe, 16384.0f, pp0[ks], pp1[ks]);
+    }
+}
+
+// dims 32 t .. 32 t + 31 of the chunk's O^T = V^T . P^T on the planes (at 2^14 sV)
+__device__ __forceinline__ void attn_band_pv(f32x16& oct, const f16x8 (&pp0)[2], const f16x8 (&pp1)[2],
+                                             const _Float16* Vc, int t, int hf, int col) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oct[r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        const int vo = (32 * t + col) * BVLD + 16 * ks + 8 * hf;
+        const f16x8 v0 = *reinterpret_cast<const f16x8*>(Vc + vo);
+        const f16x8 v1 = *reinterpret_cast<const f16x8*>(Vc + BVPL + vo);
+        oct = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1, pp0[ks], oct, 0, 0, 0);
+        oct = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0, pp1[ks], oct, 0, 0, 0);
+        oct = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0, pp0[ks], oct, 0, 0, 0);
+    }
+}
+
+// The tile state after one more chunk, in ascending chunk order: m = max(m, mc), l = l a + lc b, and the factors
+// the caller applies to o (o = o a + oc bu with bu = b uo; uo = 1 / (2^14 sV) is a power of two, so oc bu rounds as
+// (oc uo) b).  A query with no valid key in the chunk (mc = -inf, oc = 0): a = 1, bu = 0, nothing changes.
+__device__ __forceinline__ void attn_band_coef(float& m, float& l, float mc, float lc, float uo, float& a, float& bu) {
+    if (mc == -INFINITY) {
+        a = 1.0f;
+        bu = 0.0f;
+        return;
+    }
+    const float mn = fmaxf(m, mc);
+    a = (m == -INFINITY) ? 0.f : __expf(m - mn);
+    const float bb = __expf(mc - mn);
+    bu = bb * uo;
+    l = __builtin_fmaf(lc, bb, l * a);
+    m = mn;
+}
+__device__ __forceinline__ void attn_band_apply(f32x16& ot, const f32x16& oct, float a, float bu) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ot[r] = __builtin_fmaf(oct[r], bu, ot[r] * a);
+}
+
+// a chunk's K / V rows as fp16 planes at its own scales: K rows [32][BKLD], V^T [64][BVLD] (keys permuted inside each
+// 16 as the S^T accumulator holds them); rows past T hold zeros (loaded as such)
+__device__ __forceinline__ void attn_band_planes(_Float16* img, int r, int c, const f32x4& kr, const f32x4& vr,
+                                                 float sk, float sv) {
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    f16x4 h0, h1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float t = kr[e] * sk;
+        h0[e] = (_Float16)t;
+        h1[e] = (_Float16)(t - (float)h0[e]);
+    }
+    *reinterpret_cast<f16x4*>(img + r * BKLD + c) = h0;
+    *reinterpret_cast<f16x4*>(img + BKPL + r * BKLD + c) = h1;
+    _Float16* Vt = img + 2 * BKPL;
+    const int pr = vt_key_pos(r);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float t = vr[e] * sv;
+        const _Float16 a0 = (_Float16)t;
+        Vt[(c + e) * BVLD + pr] = a0;
+        Vt[BVPL + (c + e) * BVLD + pr] = (_Float16)(t - (float)a0);
+    }
+}
+
+// Q planes of the wave's 32 queries qw .. qw + 31 (lane: query col, dims 16 ks + 8 hf .. +7), pre-scaled by `scale`,
+// at the wave's own power-of-two scale (returned)
+__device__ __forceinline__ float attn_band_q(const float* base, long long ld, int h, int qi, int T, float scale, int hf,
+                                             f16x8 (&qf)[4][2]) {
     float qv[4][8];
     float mq = 0.0f;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
         f32x4 a = {0.f, 0.f, 0.f, 0.f}, c = {0.f, 0.f, 0.f, 0.f};
         if (qi < T) {
-            const float* qr = base + (long long)qi * ld + h * D + 16 * ks + 8 * hf;
+            const float* qr = base + (long long)qi * ld + h * BD + 16 * ks + 8 * hf;
             a = *reinterpret_cast<const f32x4*>(qr);
             c = *reinterpret_cast<const f32x4*>(qr + 4);
         }
@@ -722,125 +825,261 @@ __global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __
         }
     }
     const float sq = pow2_scale(wave_max(mq));
-    f16x8 qf[4][2];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) split8_h(qv[ks], sq, qf[ks][0], qf[ks][1]);
+    return sq;
+}
 
-    // one chunk's K / V rows in registers: 2 + 2 float4 per thread (zeros past the band's last key)
-    f32x4 kr[2], vr[2];
-    auto fetch = [&](int c0) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int idx = tid + q * 256, r = idx >> 4, c = (idx & 15) * 4, j = c0 + r;
-            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-            kr[q] = z;
-            vr[q] = z;
-            if (j <= kend) {
-                kr[q] = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + H * D + h * D + c);
-                vr[q] = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + 2 * H * D + h * D + c);
-            }
-        }
-    };
-    auto chunk_max = [&]() {
-        float a = 0.0f, v = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                a = fmaxf(a, fabsf(kr[q][e]));
-                v = fmaxf(v, fabsf(vr[q][e]));
-            }
-        a = wave_max(a);
-        v = wave_max(v);
-        if (lane == 0) {
-            red[0][wave] = a;
-            red[1][wave] = v;
-        }
-    };
+template <bool SPLIT>
+__global__ __launch_bounds__(256) void attention_band_h16_kernel(const float* __restrict__ qkv, float* __restrict__ out,
+                                                                 int Ts, int H, int window, float scale,
+                                                                 void* __restrict__ outp, long long pstride, int outns,
+                                                                 float oscale, unsigned* __restrict__ oamax,
+                                                                 const int* __restrict__ tlen,
+                                                                 const int* __restrict__ toff) {
+    // LDS: SPLIT -- 4 wave-private chunk images, then the partials of waves 1-3 ([2 rounds][3][35][64] fp32: 32
+    // O^T values, m, l, the V unscale per lane); else one shared chunk image.  The output staging ([waves][32][BLDO] fp32) reuses
+    // the front once the chunks are done.
+    constexpr int PARTF = 2 * 3 * 35 * 64;                          // floats
+    constexpr int IMGH = SPLIT ? 4 * BCH : BCH;                     // halves
+    constexpr int STGH = (SPLIT ? 1 : 4) * 32 * BLDO * 2;           // halves
+    constexpr int LDSH = (IMGH > STGH ? IMGH : STGH) + (SPLIT ? 2 * PARTF : 0);
+    __shared__ __attribute__((aligned(16))) _Float16 lds[LDSH];
+    __shared__ float red[2][4];
+    const int b = blockIdx.z, h = blockIdx.y;
+    // Ts: the row stride; T: this item's frames (ragged batches: items of <= 256 frames run the T <= 256 kernel)
+    const int T = tlen ? tlen[b] : Ts;
+    const int q0 = blockIdx.x * (SPLIT ? 32 : 128);
+    if (tlen && (T <= 256 || q0 >= T)) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hf = lane >> 5, col = lane & 31;
+    const long long ld = 3LL * H * BD;
+    const long long row0 = toff ? (long long)toff[b] : (long long)b * Ts;  // the item's first row (toff: packed rows)
+    const float* base = qkv + row0 * ld;
+    const int qw = SPLIT ? q0 : q0 + 32 * wave, qi = qw + col;
+    f16x8 qf[4][2];
+    const float sq = attn_band_q(base, ld, h, qi, T, scale, hf, qf);
+    // the tile's chunks cs .. ce (every wave of a SPLIT workgroup has the same tile)
+    const int cs = max(0, qw - window + 1) >> 5, ce = min(T - 1, qw + 31) >> 5;
     f32x16 o[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
     float m = -INFINITY, l = 0.f;
-    float svc = 0.0f;  // the V scale o is held at (0: no chunk yet)
-    fetch(kstart);
-    chunk_max();
-    for (int c0 = kstart; c0 <= kend; c0 += KC) {
-        // the previous chunk's fragment reads are done; red holds this chunk's maxima.  The explicit wait: hipcc
-        // emits no lgkmcnt(0) before this barrier on the loop's back edge, so another SIMD's wave could read red
-        // before this wave's write of it has landed (seen as run-to-run differences on real activations)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __syncthreads();
-        const float sk = pow2_scale(fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3])));
-        const float sv = pow2_scale(fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3])));
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int idx = tid + q * 256, r = idx >> 4, c = (idx & 15) * 4;
-            typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-            f16x4 h0, h1;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float t = kr[q][e] * sk;
-                h0[e] = (_Float16)t;
-                h1[e] = (_Float16)(t - (float)h0[e]);
-            }
-            *reinterpret_cast<f16x4*>(Ks + r * KLD + c) = h0;
-            *reinterpret_cast<f16x4*>(Ks + KPL + r * KLD + c) = h1;
-            const int pr = vt_key_pos(r);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float t = vr[q][e] * sv;
-                const _Float16 a0 = (_Float16)t;
-                Vt[(c + e) * VLD + pr] = a0;
-                Vt[VPL + (c + e) * VLD + pr] = (_Float16)(t - (float)a0);
-            }
-        }
-        __syncthreads();  // the chunk image is complete (and red is read)
-        const bool more = c0 + KC <= kend;
-        if (more) fetch(c0 + KC);
-        if (qw < T && c0 <= kend_w && c0 + KC - 1 > qw - window) {
-            float ofac = 1.0f;
-            if (svc == 0.0f || sv < svc) {
-                ofac = svc == 0.0f ? 1.0f : sv / svc;
-                svc = sv;
-            }
-            attn_chunk_h16<KLD, KPL, VLD, VPL>(o, m, l, qf, Ks, Vt, c0, qw, qi, kend_w, window, hf, col,
-                                               1.0f / (sk * sq), ofac, 16384.0f * (svc / sv));
-        }
-        if (more) chunk_max();
-    }
-    __syncthreads();  // the chunk image is dead: the output staging reuses the LDS
-    float* ow = reinterpret_cast<float*>(lds) + wave * 32 * LDO;
-    const float inv = (l > 0.f) ? 1.0f / (16384.0f * svc) / l : 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
-            ow[col * LDO + d] = o[t][r] * inv;
-        }
     float mx = 0.0f;
-    for (int qq = 0; qq < 32; ++qq) {
-        const int q = qw + qq;
-        if (q < T)
-            store_act(out, outp, pstride, outns, (row0 + q) * (H * D) + h * D + lane,
-                      ow[qq * LDO + lane], oscale, &mx);
+    if constexpr (SPLIT) {
+        f32x16 oc[2];
+        _Float16* img = lds + wave * BCH;
+        float* part = reinterpret_cast<float*>(lds + (IMGH > STGH ? IMGH : STGH));
+        // the wave's chunk of a round: 32 K / V rows, lane -> 16-B column (lane & 15) of rows (lane >> 4) + 4 q; the
+        // next round's rows load into the same registers once this round's planes are written
+        f32x4 kr[8], vr[8];
+        auto fetch = [&](int c) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int j = 32 * c + (lane >> 4) + 4 * q, cc = (lane & 15) * 4;
+                const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                kr[q] = z;
+                vr[q] = z;
+                if (j < T) {
+                    kr[q] = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + H * BD + h * BD + cc);
+                    vr[q] = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + 2 * H * BD + h * BD + cc);
+                }
+            }
+        };
+        if (cs + wave <= ce) fetch(cs + wave);
+        for (int r = 0; cs + 4 * r <= ce; ++r) {
+            const int c = cs + 4 * r + wave;
+            float mc = -INFINITY, lc = 0.f, uo = 0.f;
+            if (c <= ce) {
+                float ak = 0.0f, av = 0.0f;
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        ak = fmaxf(ak, fabsf(kr[q][e]));
+                        av = fmaxf(av, fabsf(vr[q][e]));
+                    }
+                const float sk = pow2_scale(wave_max(ak)), sv = pow2_scale(wave_max(av));
+#pragma unroll
+                for (int q = 0; q < 8; ++q) attn_band_planes(img, (lane >> 4) + 4 * q, (lane & 15) * 4, kr[q], vr[q], sk, sv);
+                if (c + 4 <= ce) fetch(c + 4);
+                // the same wave reads its image back: LDS order within a wave (the compiler keeps the writes first)
+                asm volatile("" ::: "memory");
+                f16x8 pp0[2], pp1[2];
+                attn_band_scores(pp0, pp1, mc, lc, qf, img, 32 * c, qw, qi, T, window, hf, col, 1.0f / (sk * sq));
+                attn_band_pv(oc[0], pp0, pp1, img + 2 * BKPL, 0, hf, col);
+                attn_band_pv(oc[1], pp0, pp1, img + 2 * BKPL, 1, hf, col);
+                uo = 1.0f / (16384.0f * sv);
+                if (wave > 0) {
+                    float* pw = part + ((r & 1) * 3 + wave - 1) * 35 * 64;
+#pragma unroll
+                    for (int t = 0; t < 2; ++t)
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) pw[(16 * t + e) * 64 + lane] = oc[t][e];
+                    pw[32 * 64 + lane] = mc;
+                    pw[33 * 64 + lane] = lc;
+                    pw[34 * 64 + lane] = uo;
+                }
+            }
+            __syncthreads();  // the round's partials are in LDS (and the previous round's slots are read)
+            if (wave == 0) {
+                float a, bu;
+                attn_band_coef(m, l, mc, lc, uo, a, bu);  // (mc = -inf when wave 0 had no chunk: no change)
+                attn_band_apply(o[0], oc[0], a, bu);
+                attn_band_apply(o[1], oc[1], a, bu);
+#pragma unroll 1
+                for (int w = 1; w < 4; ++w) {
+                    if (cs + 4 * r + w > ce) break;
+                    const float* pw = part + ((r & 1) * 3 + w - 1) * 35 * 64;
+#pragma unroll
+                    for (int t = 0; t < 2; ++t)
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) oc[t][e] = pw[(16 * t + e) * 64 + lane];
+                    attn_band_coef(m, l, pw[32 * 64 + lane], pw[33 * 64 + lane], pw[34 * 64 + lane], a, bu);
+                    attn_band_apply(o[0], oc[0], a, bu);
+                    attn_band_apply(o[1], oc[1], a, bu);
+                }
+            }
+        }
+        __syncthreads();  // every image is dead: wave 0 stages the tile's output at the front
+        float* ow = reinterpret_cast<float*>(lds);
+        if (wave == 0) {
+            const float inv = (l > 0.f) ? 1.0f / l : 0.f;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+                    ow[col * BLDO + d] = o[t][r] * inv;
+                }
+        }
+        __syncthreads();
+        for (int qq = 8 * wave; qq < 8 * wave + 8; ++qq) {  // wave w stores queries 8 w .. 8 w + 7
+            const int q = qw + qq;
+            if (q < T)
+                store_act(out, outp, pstride, outns, (row0 + q) * (H * BD) + h * BD + lane, ow[qq * BLDO + lane],
+                          oscale, &mx);
+        }
+    } else {
+        // the workgroup's chunks: the union of its 4 tiles' (rows of chunk c + 1 in registers while c is computed)
+        const int kc0 = max(0, q0 - window + 1) >> 5, kc1 = min(T - 1, q0 + 127) >> 5;
+        f32x4 kr[2], vr[2];
+        auto fetch = [&](int c) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int idx = tid + q * 256, rr = idx >> 4, cc = (idx & 15) * 4, j = 32 * c + rr;
+                const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                kr[q] = z;
+                vr[q] = z;
+                if (j < T) {
+                    kr[q] = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + H * BD + h * BD + cc);
+                    vr[q] = *reinterpret_cast<const f32x4*>(base + (long long)j * ld + 2 * H * BD + h * BD + cc);
+                }
+            }
+        };
+        auto chunk_max = [&]() {
+            float a = 0.0f, v = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    a = fmaxf(a, fabsf(kr[q][e]));
+                    v = fmaxf(v, fabsf(vr[q][e]));
+                }
+            a = wave_max(a);
+            v = wave_max(v);
+            if (lane == 0) {
+                red[0][wave] = a;
+                red[1][wave] = v;
+            }
+        };
+        fetch(kc0);
+        chunk_max();
+        for (int c = kc0; c <= kc1; ++c) {
+            // the previous chunk's fragment reads are done; red holds this chunk's maxima (the explicit wait: no
+            // lgkmcnt(0) is emitted before this barrier on the loop's back edge)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __syncthreads();
+            const float sk = pow2_scale(fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3])));
+            const float sv = pow2_scale(fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3])));
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int idx = tid + q * 256;
+                attn_band_planes(lds, idx >> 4, (idx & 15) * 4, kr[q], vr[q], sk, sv);
+            }
+            __syncthreads();  // the chunk image is complete (and red is read)
+            const bool more = c < kc1;
+            if (more) fetch(c + 1);
+            if (qw < T && c >= cs && c <= ce) {
+                float mc, lc, a, bu;
+                f16x8 pp0[2], pp1[2];
+                attn_band_scores(pp0, pp1, mc, lc, qf, lds, 32 * c, qw, qi, T, window, hf, col, 1.0f / (sk * sq));
+                attn_band_coef(m, l, mc, lc, 1.0f / (16384.0f * sv), a, bu);
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {  // one dim half at a time: 16 accumulator registers, not 32
+                    f32x16 oct;
+                    attn_band_pv(oct, pp0, pp1, lds + 2 * BKPL, t, hf, col);
+                    attn_band_apply(o[t], oct, a, bu);
+                }
+            }
+            if (more) chunk_max();
+        }
+        __syncthreads();  // the chunk image is dead: the output staging reuses the LDS
+        float* ow = reinterpret_cast<float*>(lds) + wave * 32 * BLDO;
+        const float inv = (l > 0.f) ? 1.0f / l : 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int d = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+                ow[col * BLDO + d] = o[t][r] * inv;
+            }
+        // same wave wrote and reads its staging rows: LDS order, no barrier
+        for (int qq = 0; qq < 32; ++qq) {
+            const int q = qw + qq;
+            if (q < T)
+                store_act(out, outp, pstride, outns, (row0 + q) * (H * BD) + h * BD + lane, ow[qq * BLDO + lane],
+                          oscale, &mx);
+        }
     }
     amax_commit(oamax, mx);
 }
 
-hipError_t launch_attention_band(const float* qkv, int batch, int T, int H, int window, float scale,
-                                 hipStream_t s, void* outp, long long out_pstride, float oscale, unsigned* oamax) {
-    hipLaunchKernelGGL(attention_band_h16_kernel, dim3((T + 127) / 128, H, batch), dim3(256), 0, s, qkv, nullptr, T, H,
-                       window, scale, outp, out_pstride, 2, oscale, oamax, nullptr, nullptr);
+// the banded kernel's decomposition: SPLIT when the 128-query form would leave most CUs idle (mode: 0 never, 1 when
+// it has fewer than 128 workgroups, 2 always -- the same values every way)
+static bool band_split(int mode, int batch, int Tmax, int H) {
+    if (mode != 1) return mode == 2;
+    return (long long)((Tmax + 127) / 128) * H * batch < 128;
+}
+static hipError_t launch_band(const float* qkv, float* out, int batch, int T, int Tmax, int H, int window,
+                              float scale, hipStream_t s, void* outp, long long pstride, int outns, float oscale,
+                              unsigned* oamax, const int* tlen, const int* toff, const char** kname, int split) {
+    if (band_split(split, batch, Tmax, H)) {
+        hipLaunchKernelGGL(attention_band_h16_kernel<true>, dim3((Tmax + 31) / 32, H, batch), dim3(256), 0, s, qkv,
+                           out, T, H, window, scale, outp, pstride, outns, oscale, oamax, tlen, toff);
+        if (kname) *kname = "mimi::attention_band_h16_kernel<true>";
+    } else {
+        hipLaunchKernelGGL(attention_band_h16_kernel<false>, dim3((Tmax + 127) / 128, H, batch), dim3(256), 0, s, qkv,
+                           out, T, H, window, scale, outp, pstride, outns, oscale, oamax, tlen, toff);
+        if (kname) *kname = "mimi::attention_band_h16_kernel<false>";
+    }
     return hipGetLastError();
+}
+
+hipError_t launch_attention_band(const float* qkv, int batch, int T, int H, int window, float scale,
+                                 hipStream_t s, void* outp, long long out_pstride, float oscale, unsigned* oamax,
+                                 int split) {
+    return launch_band(qkv, nullptr, batch, T, T, H, window, scale, s, outp, out_pstride, 2, oscale, oamax, nullptr,
+                       nullptr, nullptr, split);
 }
 
 hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int H, int D, int window, float scale,
                             hipStream_t s, void* outp, long long out_pstride, int outns, float oscale,
                             unsigned* oamax, bool h16, const int* tlen, int max_tlen, int min_tlen,
-                            const int* toff) {
+                            const int* toff, const char** kname, int band_split_mode) {
     if (D != 64 || (outns != 0 && !outp) || (outns == 0 && !out) || (oscale > 0.0f && outns != 2)) return hipErrorInvalidValue;
     if (tlen) {  // ragged batch: each item the kernel it would run alone (each exits on the other's items)
         if (!h16 || !(oscale > 0.0f && outns == 2) || max_tlen > T || min_tlen < 1) return hipErrorInvalidValue;
@@ -852,8 +1091,8 @@ hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int 
             if (e != hipSuccess) return e;
         }
         if (max_tlen > 256)
-            hipLaunchKernelGGL(attention_band_h16_kernel, dim3((max_tlen + 127) / 128, H, batch), dim3(256), 0, s, qkv,
-                               out, T, H, window, scale, outp, out_pstride, outns, oscale, oamax, tlen, toff);
+            return launch_band(qkv, out, batch, T, max_tlen, H, window, scale, s, outp, out_pstride, outns, oscale,
+                               oamax, tlen, toff, kname, band_split_mode);
         return hipGetLastError();
     }
     // (the banded kernel at T <= 256 measured slower at B = 1 and B = 32: profiles/r2d_ab_attention_band.log)
@@ -864,11 +1103,9 @@ hipError_t launch_attention(const float* qkv, float* out, int batch, int T, int 
                            outp, out_pstride, oscale, oamax, nullptr, qg, nullptr);
         return hipGetLastError();
     }
-    if (h16) {  // T > 256: fp16-plane output, or fp32 for clips too long for the plane buffers
-        hipLaunchKernelGGL(attention_band_h16_kernel, dim3((T + 127) / 128, H, batch), dim3(256), 0, s, qkv, out, T, H,
-                           window, scale, outp, out_pstride, outns, oscale, oamax, nullptr, nullptr);
-        return hipGetLastError();
-    }
+    if (h16)  // T > 256: fp16-plane output, or fp32 for clips too long for the plane buffers
+        return launch_band(qkv, out, batch, T, T, H, window, scale, s, outp, out_pstride, outns, oscale, oamax,
+                           nullptr, nullptr, kname, band_split_mode);
     if (T <= 256) {
         hipLaunchKernelGGL(attention_t256_kernel, dim3(H, batch), dim3(512), 0, s, qkv, out, T, H, window, scale,
                            outp, out_pstride, outns, oscale, oamax);
