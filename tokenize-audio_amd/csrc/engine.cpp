@@ -21,6 +21,7 @@
 #include <fstream>
 #include <map>
 #include <memory>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <tuple>
@@ -297,10 +298,12 @@ struct mimi_engine {
     struct HostIo {
         bool busy = false;
         float* d_audio = nullptr;
-        size_t audio_cap = 0;        // bytes
+        float* h_audio = nullptr;    // pinned staging of the caller's samples (the H2D then runs under the launches)
+        size_t audio_cap = 0;        // bytes (both audio buffers)
         int32_t* d_codes = nullptr;
         int32_t* h_codes = nullptr;  // pinned
         size_t codes_cap = 0;        // bytes (both code buffers)
+        hipEvent_t done = nullptr;   // the codes' D2H
     };
     HostIo hostio[kMaxPending];
     int64_t next_ticket = 1;
@@ -2179,6 +2182,17 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
     return MIMI_OK;
 }
 
+// The host waits for an encode by polling its event for the first 20 ms, then blocks: a blocking wait sleeps and
+// pays a wake-up of tens of microseconds, which a per-utterance caller (one short encode per call) pays every call.
+static hipError_t wait_event(hipEvent_t ev) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q != hipErrorNotReady) return q;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) return hipEventSynchronize(ev);
+    }
+}
+
 // Waits for ticket's encode and runs its f16x3 overflow check.  The engine lock is NOT held while the host
 // synchronises on the encode's event (other threads keep enqueueing on the engine meanwhile): the slot is claimed
 // under the lock -- so it is neither reused nor waited twice -- and released, with the overflow check and any
@@ -2195,7 +2209,7 @@ static int encode_wait(mimi_engine* e, int64_t ticket) {
         q = *P;
     }
     HIP_TRY(hipSetDevice(e->device));
-    const hipError_t se = hipEventSynchronize(q.done);
+    const hipError_t se = wait_event(q.done);
     std::lock_guard<std::mutex> lk(e->mu);
     mimi_engine::Pending* P = nullptr;
     for (auto& x : e->pend)
@@ -2326,12 +2340,16 @@ extern "C" int mimi_encode(mimi_engine* e, const float* audio, int32_t batch, in
 // (twice when the encode had to be re-run: a chain give-up or an f16x3 overflow re-encodes on the stream inside
 // mimi_encode_wait, after which the codes are copied again).
 static int host_io_grow(mimi_engine::HostIo* io, size_t ab, size_t cb) {
+    if (!io->done) HIP_TRY(hipEventCreateWithFlags(&io->done, hipEventDisableTiming));
     if (io->audio_cap < ab) {
         if (io->d_audio) HIP_TRY(hipFree(io->d_audio));  // (hipFree waits for the device)
+        if (io->h_audio) HIP_TRY(hipHostFree(io->h_audio));
         io->d_audio = nullptr;
+        io->h_audio = nullptr;
         io->audio_cap = 0;
         const size_t cap = std::max(ab, (size_t)1 << 22);
         HIP_TRY(hipMalloc(&io->d_audio, cap));
+        HIP_TRY(hipHostMalloc(&io->h_audio, cap, hipHostMallocDefault));
         io->audio_cap = cap;
     }
     if (io->codes_cap < cb) {
@@ -2369,7 +2387,8 @@ extern "C" int mimi_encode_host(mimi_engine* e, const float* host_audio, int32_t
         if (!io)
             return set_err(MIMI_ERR_STATE, "%d host encodes in flight", mimi_engine::kMaxPending);
         if ((rc = host_io_grow(io, ab, cb))) return rc;
-        const hipError_t ce = hipMemcpyAsync(io->d_audio, host_audio, ab, hipMemcpyHostToDevice, s);
+        std::memcpy(io->h_audio, host_audio, ab);  // (the slot's previous H2D finished before its last call returned)
+        const hipError_t ce = hipMemcpyAsync(io->d_audio, io->h_audio, ab, hipMemcpyHostToDevice, s);
         if (ce != hipSuccess) rc = set_err(MIMI_ERR_HIP, "mimi_encode_host: H2D copy: %s", hipGetErrorString(ce));
         if (!rc) rc = encode_async_locked(e, io->d_audio, batch, length, K, io->d_codes, s, &ticket);
         if (rc) {
@@ -2378,7 +2397,8 @@ extern "C" int mimi_encode_host(mimi_engine* e, const float* host_audio, int32_t
         }
         io->busy = true;  // (from here on every exit path releases it)
         reruns = e->chain_reruns + e->f16_reruns;
-        const hipError_t de = hipMemcpyAsync(io->h_codes, io->d_codes, cb, hipMemcpyDeviceToHost, s);
+        hipError_t de = hipMemcpyAsync(io->h_codes, io->d_codes, cb, hipMemcpyDeviceToHost, s);
+        if (de == hipSuccess) de = hipEventRecord(io->done, s);
         if (de != hipSuccess) rc = set_err(MIMI_ERR_HIP, "mimi_encode_host: D2H copy: %s", hipGetErrorString(de));
     }
     const int wrc = encode_wait(e, ticket);  // (always: it frees the ticket)
@@ -2391,7 +2411,8 @@ extern "C" int mimi_encode_host(mimi_engine* e, const float* host_audio, int32_t
         }
         hipError_t he = hipSuccess;
         if (again) he = hipMemcpyAsync(io->h_codes, io->d_codes, cb, hipMemcpyDeviceToHost, s);
-        if (he == hipSuccess) he = hipStreamSynchronize(s);
+        if (again && he == hipSuccess) he = hipEventRecord(io->done, s);
+        if (he == hipSuccess) he = wait_event(io->done);
         if (he != hipSuccess)
             rc = set_err(he == hipErrorOutOfMemory ? MIMI_ERR_OUT_OF_MEMORY : MIMI_ERR_HIP, "mimi_encode_host: %s",
                          hipGetErrorString(he));
@@ -2470,6 +2491,8 @@ extern "C" void mimi_destroy(mimi_engine* e) {
         if (q.chain_word) (void)hipHostFree(q.chain_word);
     }
     for (auto& h : e->hostio) {
+        if (h.done) (void)hipEventDestroy(h.done);
+        if (h.h_audio) (void)hipHostFree(h.h_audio);
         if (h.d_audio) (void)hipFree(h.d_audio);
         if (h.d_codes) (void)hipFree(h.d_codes);
         if (h.h_codes) (void)hipHostFree(h.h_codes);

@@ -58,7 +58,7 @@ class MimiConfig:
     # TF/configuration_mimi.py:143-145
     @property
     def encodec_frame_rate(self) -> int:
-        return math.ceil(self.sampling_rate / int(np.prod(self.upsampling_ratios)))
+        return math.ceil(self.sampling_rate / math.prod(self.upsampling_ratios))
 
     # TF/configuration_mimi.py:152-175
     @property
@@ -129,6 +129,11 @@ def conv_out_len(length: int, kernel: int, stride: int) -> int:
     division of int64 tensors (-> float32), then ``ceil``; the padded input is ``n_frames*s + k`` long,
     giving ``n_frames + 1`` outputs.
     """
+    if 0 <= length < (1 << 22):
+        # (L - s) / s + 1 = L / s, and below 2^22 samples no float32 rounding moves its ceil (every quotient's
+        # fractional part, a multiple of 1 / s, is further from an integer than half an ulp): ceil(L / s) exactly,
+        # without numpy scalars (~70 us per encoded_length on the per-utterance path)
+        return -(-length // stride)
     pt = kernel - stride
     nf = np.float32(np.float32(length - kernel + pt) / np.float32(stride)) + np.float32(1.0)
     n_frames = int(np.ceil(np.float32(nf))) - 1

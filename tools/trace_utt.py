@@ -72,8 +72,43 @@ def summary(d):
         print(f"  {v / n:8.1f}  {k}")
 
 
+
+
+def host_split(n=24):
+    """Host-side split of one encode_audio_chunk call: the engine call (mimi_encode_host) vs the Python around it."""
+    import torch
+    from mimi_hip import synthetic
+    from mimi_hip.encoder import MimiEncoder
+    from mimi_hip.model import MimiHipModel
+    dev = torch.device("cuda", 0)
+    model = MimiHipModel(synthetic.make_state_dict(seed=0, num_quantizers=32), device=dev)
+    enc = MimiEncoder(device=dev, model=model)
+    lens = synthetic.random_lengths(n, 10.0, 20.0, seed=99)
+    utts = [synthetic.speech_like(n_, 99, i) for i, n_ in enumerate(lens)]
+    for a in utts[:2]:
+        enc.encode_audio_chunk(a, 24000)
+    orig = model.encode_host
+    t_eng = []
+
+    def timed(*a, **k):
+        t0 = time.perf_counter()
+        r = orig(*a, **k)
+        t_eng.append(time.perf_counter() - t0)
+        return r
+    model.encode_host = timed
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a in utts:
+        enc.encode_audio_chunk(a, 24000)
+    dt = (time.perf_counter() - t0) / n
+    print(f"per call {1e6 * dt:.1f} us: engine call {1e6 * sum(t_eng) / n:.1f} us, python around it "
+          f"{1e6 * (dt - sum(t_eng) / n):.1f} us", flush=True)
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run(int(sys.argv[2]) if len(sys.argv) > 2 else 24)
+    elif sys.argv[1] == "host":
+        host_split()
     else:
         summary(sys.argv[2])
