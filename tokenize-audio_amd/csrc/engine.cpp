@@ -21,7 +21,6 @@
 #include <fstream>
 #include <map>
 #include <memory>
-#include <chrono>
 #include <mutex>
 #include <string>
 #include <tuple>
@@ -2182,17 +2181,6 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
     return MIMI_OK;
 }
 
-// The host waits for an encode by polling its event for the first 20 ms, then blocks: a blocking wait sleeps and
-// pays a wake-up of tens of microseconds, which a per-utterance caller (one short encode per call) pays every call.
-static hipError_t wait_event(hipEvent_t ev) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-        const hipError_t q = hipEventQuery(ev);
-        if (q != hipErrorNotReady) return q;
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) return hipEventSynchronize(ev);
-    }
-}
-
 // Waits for ticket's encode and runs its f16x3 overflow check.  The engine lock is NOT held while the host
 // synchronises on the encode's event (other threads keep enqueueing on the engine meanwhile): the slot is claimed
 // under the lock -- so it is neither reused nor waited twice -- and released, with the overflow check and any
@@ -2209,7 +2197,7 @@ static int encode_wait(mimi_engine* e, int64_t ticket) {
         q = *P;
     }
     HIP_TRY(hipSetDevice(e->device));
-    const hipError_t se = wait_event(q.done);
+    const hipError_t se = hipEventSynchronize(q.done);
     std::lock_guard<std::mutex> lk(e->mu);
     mimi_engine::Pending* P = nullptr;
     for (auto& x : e->pend)
@@ -2412,7 +2400,7 @@ extern "C" int mimi_encode_host(mimi_engine* e, const float* host_audio, int32_t
         hipError_t he = hipSuccess;
         if (again) he = hipMemcpyAsync(io->h_codes, io->d_codes, cb, hipMemcpyDeviceToHost, s);
         if (again && he == hipSuccess) he = hipEventRecord(io->done, s);
-        if (he == hipSuccess) he = wait_event(io->done);
+        if (he == hipSuccess) he = hipEventSynchronize(io->done);
         if (he != hipSuccess)
             rc = set_err(he == hipErrorOutOfMemory ? MIMI_ERR_OUT_OF_MEMORY : MIMI_ERR_HIP, "mimi_encode_host: %s",
                          hipGetErrorString(he));
