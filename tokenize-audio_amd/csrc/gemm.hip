@@ -228,6 +228,8 @@ static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
     // fp32-only output (down_s0): the next tile's first stage loads under the epilogue (FL_PF: -2.6 %; with the
     // planes epilogues of down_s1 / s2 it costs +2..3 %, profiles/r2c_ab_pf_pair.log)
     constexpr int PF = OUTP == 0 ? FL_PF : 0;
+    // (4 compute waves of 128 x 64 or 64 x 128 -- a third fewer LDS fragment reads per MFMA -- measured 5-6 % slower:
+    // profiles/r5o_ab_down_4waves.txt)
     if (pair_ok(a)) return run_planes<256, 128, 4, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR | FL_PERSIST | PF, true>(a, s);
     return run_planes<256, 128, 4, 2, 2, 3, EPI, OUTP, TAG, 0, 32, 16, 0, true>(a, s);
 }
