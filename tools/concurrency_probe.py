@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--splits", type=int, nargs="+", default=[1, 2])
+    ap.add_argument("--replicas", action="store_true",
+                    help="every stream encodes the WHOLE batch (S batches in flight) instead of 1/S of it")
     args = ap.parse_args()
     import torch
     from mimi_hip import synthetic
@@ -35,13 +37,14 @@ def main():
     streams = [torch.cuda.Stream(dev) for _ in models]
     ref = None
     for S in args.splits:
-        nb = B // S
+        nb = B if args.replicas else B // S
         outs = [torch.empty((nb, K, encoded_length(L)), dtype=torch.int32, device=dev) for _ in range(S)]
 
         def worker(i, n):
             with torch.cuda.stream(streams[i]):
                 for _ in range(n):
-                    models[i].encode_int32(audio[i * nb:(i + 1) * nb], K, out=outs[i])
+                    x = audio if args.replicas else audio[i * nb:(i + 1) * nb]
+                    models[i].encode_int32(x, K, out=outs[i])
             streams[i].synchronize()
 
         def run(n):
@@ -56,8 +59,8 @@ def main():
         t0 = time.perf_counter()
         run(args.steps)
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / args.steps
-        codes = torch.cat(outs, 0)
+        dt = (time.perf_counter() - t0) / args.steps / (S if args.replicas else 1)
+        codes = outs[-1] if args.replicas else torch.cat(outs, 0)
         if ref is None:
             ref = codes.clone()
         same = bool(torch.equal(codes, ref))
