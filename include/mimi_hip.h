@@ -261,7 +261,8 @@ const char* mimi_last_error(void);
 
 /* ---- instrumentation (bench / tests) ---- */
 
-/* When enabled, mimi_encode records a HIP event pair around every stage on the stream it runs on. */
+/* enable = 1: every encode records HIP events between its stages on the stream it runs on (one per stage);
+ * 2: only around its first stage (two events per encode: the light form a timed region can carry); 0: off. */
 int mimi_set_profiling(mimi_engine* e, int enable);
 /* Per-stage totals accumulated over all profiled encodes since the last reset: names (128 chars
  * each, "stage|kernel symbol"), device ms (event pairs on the launch stream), launch counts, and algorithmic work as

@@ -309,7 +309,7 @@ struct mimi_engine {
     size_t item_codes_cap = 0;
     int f16_reruns = 0;             // encodes that took the overflow fallback (diagnostic)
     std::vector<float> last_amax;   // per-slot max|x| of the last waited f16x3 encode (diagnostic)
-    bool profiling = false;
+    int profiling = 0;  // 1: every stage between events; 2: the first stage of each pass only (two events)
     std::vector<ProfEvent> pending;  // recorded since last read; first event of each encode named ""
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, ProfStat> prof;
@@ -1133,6 +1133,7 @@ static hipEvent_t pool_event(mimi_engine* e) {
 struct Recorder {
     mimi_engine* e;
     hipStream_t s;
+    int marks = 0;
     void begin() {
         if (!e->profiling) return;
         ProfEvent pe{"", pool_event(e), 0, 0};
@@ -1141,6 +1142,7 @@ struct Recorder {
     }
     void mark(const std::string& name, double flops, double bytes, const char* kernel) {
         if (!e->profiling) return;
+        if (e->profiling == 2 && marks++ >= 1) return;  // level 2: the pass's first stage only
         ProfEvent pe{name + "|" + kernel, pool_event(e), flops, bytes};
         (void)hipEventRecord(pe.ev, s);
         e->pending.push_back(pe);
@@ -2598,8 +2600,9 @@ extern "C" int64_t mimi_rvq_chain_reruns(const mimi_engine* e) { return e ? e->c
 
 extern "C" int mimi_set_profiling(mimi_engine* e, int enable) {
     if (!e) return set_err(MIMI_ERR_INVALID_ARGUMENT, "null engine");
+    if (enable < 0 || enable > 2) return set_err(MIMI_ERR_INVALID_ARGUMENT, "profiling level %d (0, 1 or 2)", enable);
     std::lock_guard<std::mutex> lk(e->mu);
-    e->profiling = enable != 0;
+    e->profiling = enable;
     return MIMI_OK;
 }
 

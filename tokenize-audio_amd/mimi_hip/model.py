@@ -379,7 +379,8 @@ class MimiHipModel:
             out[name] = (sc[i], mx[i], head)
         return out
 
-    def set_profiling(self, enable: bool = True):
+    def set_profiling(self, enable=True):
+        """True / 1: events between every stage; 2: around each encode's first stage only; False / 0: off."""
         _lib.check(self._lib.mimi_set_profiling(self._h, int(enable)))
 
     def profile_reset(self):
