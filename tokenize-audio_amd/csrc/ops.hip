@@ -1620,6 +1620,50 @@ __device__ __forceinline__ void rvq_exact(const float (*img)[FT][LDH], const flo
     }
 }
 
+// rvq_exact with every candidate's code row staged in LDS first (the persistent chain, whose workgroup has the LDS):
+// wave w issues the rows of candidates w, w + 8, .. as LDS-DMA (one 1-KB row per wave-instruction, all in flight at
+// once), so the exact chains read LDS instead of waiting out D / 4 / EX global round trips each.  Same chain, same
+// order, same values as rvq_exact (|e|^2 from the slice's ynl copy of cnorm).  nc <= NSTG.
+template <int FT, int D, int LDH, int NT, int NSTG>
+__device__ __forceinline__ void rvq_exact_staged(const float (*img)[FT][LDH], const float* xn, const unsigned* cand,
+                                                 unsigned nc, unsigned long long* best, const float* cbr,
+                                                 const float* ynl, int cbase, long long f0, long long frames, int tid,
+                                                 float* rowbuf) {
+    constexpr int NWV = NT / 64, RS = D + 4;  // (row stride: + 16 B, conflict-free b128 reads of different rows)
+    static_assert(D == 256, "one 16-B piece per lane per row");
+    const int lane = tid & 63, wave = tid >> 6;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // LDS-DMA: no registers held; candidate i's 1-KB row lands at rowbuf + i RS (lane l: floats 4 l .. 4 l + 3)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(cbr), (short)0, 0x7fffffff,
+                                                                         0x00020000);
+    for (unsigned i = wave; i < nc; i += NWV) {  // (wave-uniform)
+        const int c = cbase + (int)(cand[i] & 0xffff);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(rowbuf + i * RS), 16,
+                                                 (c * D + 4 * lane) * 4, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    __syncthreads();
+    for (unsigned i = tid; i < nc; i += NT) {
+        const int row = (int)(cand[i] >> 16), cl = (int)(cand[i] & 0xffff);
+        if (f0 + row >= frames) continue;
+        const float* e = rowbuf + i * RS;
+        float a = 0.0f;
+#pragma unroll 4
+        for (int k4 = 0; k4 < D / 4; ++k4) {
+            const f32x4 ev = *reinterpret_cast<const f32x4*>(e + 4 * k4);
+            a = __builtin_fmaf(img[0][row][2 * k4], ev.x, a);
+            a = __builtin_fmaf(img[1][row][2 * k4], ev.y, a);
+            a = __builtin_fmaf(img[0][row][2 * k4 + 1], ev.z, a);
+            a = __builtin_fmaf(img[1][row][2 * k4 + 1], ev.w, a);
+        }
+        float d2 = a + xn[row];
+        d2 = d2 + ynl[cl];
+        const float d = __builtin_sqrtf(fmaxf(d2, 0.0f));
+        atomicMin(&best[row], ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)(cbase + cl));
+    }
+}
+
 template <int D, int PF = 4, int EX = 16, bool RG = false, int CW = 32, int NWV = 8, int FT = 32, bool P1 = false>
 // (HIP's second launch bound is waves per SIMD: 4 = two 8-wave workgroups per CU, i.e. <= 128 VGPRs)
 __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_level_h16_kernel(RvqArgs p, int L0) {
@@ -1888,6 +1932,7 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
 constexpr int RVQC_MAX_WG = 128;
 constexpr int RVQC_SPIN = 1 << 20;
 constexpr int RVQC_HDR = 2;  // u64 words in front of the granules: [0] the give-up flag (u32), [1] padding
+constexpr int RVQC_NSTG = 64;  // candidates whose code rows the exact re-score stages in LDS (more: global reads)
 
 __device__ __forceinline__ unsigned long long rvqc_granule(unsigned epoch, unsigned long long best) {
     // best = (distance bits << 32) | code (code 0xffffffff: none): tag 16 bits | code 16 bits | distance 32 bits
@@ -1931,6 +1976,7 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
     __shared__ int tmo;
     __shared__ int codes_l[FT][32];  // this tile's codes per level, stored at the end (slice 0)
     __shared__ float ynl[SLC];       // |e|^2 of the slice's codes at this level
+    __shared__ __attribute__((aligned(16))) float rowbuf[RVQC_NSTG * (D + 4)];  // candidates' code rows (exact)
     const int chain = blockIdx.z;
     const int Lb = chain ? 0 : p.nsem, Le = chain ? min(p.nsem, p.levels) : p.levels;
     if (Lb >= Le) return;  // (workgroup-uniform)
@@ -2038,9 +2084,15 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
         }
         __syncthreads();
         RVQC_T(3);
-        // exact re-score (the reference's fp32 chain), rvq_exact as in rvq_level_h16_kernel
-        rvq_exact<FT, D, LDH, NT, SLC, EX>(img, xn, cand, ncand, best, p.cb_rows + (long long)L * p.ncodes * D,
-                                           p.cb_norm + (long long)L * p.ncodes, slice * SLC, f0, p.frames, tid);
+        // exact re-score (the reference's fp32 chain), rvq_exact as in rvq_level_h16_kernel; with the candidates'
+        // code rows staged in LDS when they fit (one global round trip instead of D / 4 / EX)
+        if (ncand <= RVQC_NSTG)
+            rvq_exact_staged<FT, D, LDH, NT, RVQC_NSTG>(img, xn, cand, ncand, best,
+                                                        p.cb_rows + (long long)L * p.ncodes * D, ynl, slice * SLC,
+                                                        f0, p.frames, tid, rowbuf);
+        else
+            rvq_exact<FT, D, LDH, NT, SLC, EX>(img, xn, cand, ncand, best, p.cb_rows + (long long)L * p.ncodes * D,
+                                               p.cb_norm + (long long)L * p.ncodes, slice * SLC, f0, p.frames, tid);
         __syncthreads();
         RVQC_T(4);
         // publish this slice's 32 minima (one 8-byte agent-scope store each: the granule is its own flag)
