@@ -29,7 +29,9 @@ namespace mimi {
 // channels per wave (CT = CPW / 16 channel tiles; a lane owns CPW / 4 consecutive channels of one step)
 constexpr int R1S_MAXB = 256;  // ragged batches: items the in-kernel tile table holds (more: the planes GEMM runs)
 
-template <int K, int DEPTH, int CPW>
+// RG: a ragged batch (p.m_rows) -- its own instantiation, so the uniform kernel's loop carries none of the tile-table
+// lookups (run-time-branched into one kernel they cost the uniform batches 13 %: 0.220 -> 0.249 ms per B = 32 step)
+template <int K, int DEPTH, int CPW, bool RG>
 __global__ __launch_bounds__(2 * K / CPW * 64) void res1_stream_kernel(GemmArgs p, int ntiles) {
 #if defined(__HIP_DEVICE_COMPILE__)
     constexpr int N = 2 * K, KS = K / 32, CT = CPW / 16, LC = CPW / 4;
@@ -65,7 +67,7 @@ __global__ __launch_bounds__(2 * K / CPW * 64) void res1_stream_kernel(GemmArgs 
     // ragged batches: only the items' valid 16-step tiles (item b's ceil(m_rows[b] / 16) tiles from tst[b]), so the
     // padding rows cost nothing (a walk over all batch x M rows read and skipped them: YODAS2-style batches +28 %)
     __shared__ int tst[R1S_MAXB + 1];
-    if (p.m_rows) {
+    if constexpr (RG) {
         if (tid == 0) {
             int acc = 0;
             for (int b = 0; b < p.batch; ++b) {
@@ -79,10 +81,6 @@ __global__ __launch_bounds__(2 * K / CPW * 64) void res1_stream_kernel(GemmArgs 
     }
     // a tile's first row and (ragged) its item's valid steps from there
     auto tile_at = [&](int tile, int& lim) -> long long {
-        if (!p.m_rows) {
-            lim = 16;
-            return (long long)tile * 16;
-        }
         int lo = 0, hi = p.batch - 1;  // the last item whose first tile is <= tile
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
@@ -98,8 +96,13 @@ __global__ __launch_bounds__(2 * K / CPW * 64) void res1_stream_kernel(GemmArgs 
         f32x4 r[CT];  // skip x: channels cl .. cl + LC - 1 of step l16
     };
     auto load = [&](int tile, Tile& t) {
-        int lim;
-        const long long row = tile_at(tile, lim) + l16;  // (past the rows: the buffer range check loads 0)
+        long long row;  // (past the rows: the buffer range check loads 0)
+        if constexpr (RG) {
+            int lim;
+            row = tile_at(tile, lim) + l16;
+        } else {
+            row = (long long)tile * 16 + l16;
+        }
         const int ho = (int)((row * K + 8 * q) * 2);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -125,10 +128,21 @@ __global__ __launch_bounds__(2 * K / CPW * 64) void res1_stream_kernel(GemmArgs 
                 acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ct][ks][1], t.b[ks][0], acc[ct], 0, 0, 0);
                 acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[ct][ks][0], t.b[ks][0], acc[ct], 0, 0, 0);
             }
-        int lim;
-        const long long row = tile_at(tile, lim) + l16;
-        const bool ok = row < rows && l16 < lim;  // (ragged: the item's valid steps only -- its rows past them are
-                                                  // never stored)
+        long long row;
+        bool ok;
+        if constexpr (RG) {
+            int lim;
+            row = tile_at(tile, lim) + l16;
+            ok = row < rows && l16 < lim;  // (the item's valid steps only -- its rows past them are never stored)
+        } else {
+            row = (long long)tile * 16 + l16;
+            ok = row < rows;
+            if (ok && p.m_rows) {  // (never taken: the launch sends ragged batches to RG; kept because this form of the
+                                   // loop is the one hipcc schedules best -- 20 waits against 29-41 without it)
+                const long long b = row / p.M;
+                ok = row - b * p.M < p.m_rows[b];
+            }
+        }
         if (ok) {
 #pragma unroll
             for (int g = 0; g < LC / 8; ++g) {
@@ -180,7 +194,9 @@ template <int DEPTH, int CPW>
 static hipError_t run_res1_stream(const GemmArgs& a, hipStream_t s, const char** kname) {
     constexpr int NT = 256 / CPW * 64;
     static char nm[80];
-    snprintf(nm, sizeof nm, "mimi::res1_stream_kernel<128, %d, %d>(mimi::GemmArgs, int)", DEPTH, CPW);
+    const bool rg = a.m_rows != nullptr;
+    snprintf(nm, sizeof nm, "mimi::res1_stream_kernel<128, %d, %d, %s>(mimi::GemmArgs, int)", DEPTH, CPW,
+             rg ? "true" : "false");
     if (kname) *kname = nm;
     const long long rows = (long long)a.M * a.batch;
     const int ntiles = (int)((rows + 15) / 16);
@@ -189,11 +205,15 @@ static hipError_t run_res1_stream(const GemmArgs& a, hipStream_t s, const char**
         int dev = 0, ncu = 256, occ = 1;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, res1_stream_kernel<128, DEPTH, CPW>, NT, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, res1_stream_kernel<128, DEPTH, CPW, false>, NT, 0);
         slots = ncu * (occ > 0 ? occ : 1);
     }
     const int grid = ntiles < slots ? ntiles : slots;
-    hipLaunchKernelGGL((res1_stream_kernel<128, DEPTH, CPW>), dim3((unsigned)grid), dim3(NT), 0, s, a, ntiles);
+    if (rg)
+        hipLaunchKernelGGL((res1_stream_kernel<128, DEPTH, CPW, true>), dim3((unsigned)grid), dim3(NT), 0, s, a, ntiles);
+    else
+        hipLaunchKernelGGL((res1_stream_kernel<128, DEPTH, CPW, false>), dim3((unsigned)grid), dim3(NT), 0, s, a,
+                           ntiles);
     return hipGetLastError();
 }
 
