@@ -137,3 +137,23 @@ def test_feature_extractor_golden_meta(golden):
 def test_config_defaults():
     c = MimiConfig()
     assert c.frame_size == 1920 and c.frame_rate == 12.5 and c.encodec_frame_rate == 25
+
+
+def test_conv_out_len_integer_form_equals_float32_form():
+    """config.conv_out_len answers ceil(L / s) directly below 2^22 samples; that must be the reference's float32
+    expression ((L - s) / s + 1, ceil) for every stride the encoder uses, including the ranges' edges."""
+    import numpy as np
+
+    from mimi_hip.config import conv_out_len
+
+    def f32_form(length, kernel, stride):
+        pt = kernel - stride
+        nf = np.float32(np.float32(length - kernel + pt) / np.float32(stride)) + np.float32(1.0)
+        return int(np.ceil(np.float32(nf)))
+
+    rng = np.random.default_rng(7)
+    for k, s in [(7, 1), (3, 1), (1, 1), (8, 4), (10, 5), (12, 6), (16, 8), (4, 2)]:
+        ls = list(range(0, 5000)) + [int(v) for v in rng.integers(5000, 1 << 22, 4000)] + \
+            list(range((1 << 22) - 2000, (1 << 22) + 50))
+        for L in ls:
+            assert conv_out_len(L, k, s) == f32_form(L, k, s), (k, s, L)
