@@ -142,8 +142,6 @@ def test_config_defaults():
 def test_conv_out_len_integer_form_equals_float32_form():
     """config.conv_out_len answers ceil(L / s) directly below 2^22 samples; that must be the reference's float32
     expression ((L - s) / s + 1, ceil) for every stride the encoder uses, including the ranges' edges."""
-    import numpy as np
-
     from mimi_hip.config import conv_out_len
 
     def f32_form(length, kernel, stride):
