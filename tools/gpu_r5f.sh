@@ -18,7 +18,7 @@ TAG=$TAG STEPS=10 timeout -k 10 900 bash tools/profile_round.sh > $O/profile_rou
 echo profile ok
 PASSES="SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_WAIT_INST_LDS,GRBM_GUI_ACTIVE;SQ_VALU_MFMA_BUSY_CYCLES,SQ_LDS_BANK_CONFLICT,GRBM_GUI_ACTIVE" TAG=${TAG}_sq timeout -k 10 400 bash tools/pmc_pass.sh > $O/sq.log 2>&1 || { echo sq failed; tail $O/sq.log; exit 1; }
 echo sq ok
-for spec in "b1:--batch 1 --no-f32-mode" "b4:--batch 4 --no-f32-mode" "yodas2:--workload yodas2 --steps 6 --warmup 2" "mls:--workload mls --steps 3 --warmup 1"; do
+for spec in "b1:--batch 1 --no-f32-mode" "b4:--batch 4 --no-f32-mode" "yodas2:--workload yodas2 --steps 12 --warmup 2" "mls:--workload mls --steps 8 --warmup 1"; do
   name=${spec%%:*}; args=${spec#*:}
   timeout -k 10 300 python -u bench.py --cpu-baseline-seconds 0 $args --json-out $O/bench_$name.json > $O/bench_$name.log 2>&1 || { echo "$name failed"; tail -5 $O/bench_$name.log; exit 1; }
   python3 -c "import json; d=json.load(open('$O/bench_$name.json')); print('$name', d['value'], d['ms_per_step'])"
