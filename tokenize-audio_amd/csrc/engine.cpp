@@ -1729,6 +1729,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         ad.a_boff = dToff;
     }
     LAUNCH_TRY(launch_gemm(ROLE_DOWNSAMPLE, ad, s, &kname, prec), "downsample");
+    if ((rc = save_tap(e, "ds_gemm", w.dsout, B, T2, Hd, s))) return rc;  // (before the replicate-pad rows)
     if (ds_planes)
         LAUNCH_TRY(launch_ds_edge_fix(w.t0, e->ds_fix, w.dsout, w.att, ad.c_pstride, dsouta.scale, dsouta.amax, B,
                                       (int)T, (int)T2, Hd, Hd, s, rg ? dT25 : nullptr, rg ? dF : nullptr, dToff),
@@ -2461,7 +2462,11 @@ extern "C" int mimi_rvq_encode(mimi_engine* e, const float* emb, int64_t frames,
 extern "C" void mimi_destroy(mimi_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
-    (void)hipDeviceSynchronize();
+    // this engine's work only (every encode ends with ws_free on its stream; a device-wide sync would wait for
+    // other engines and is refused while one of them captures a graph)
+    if (e->ws_free) (void)hipEventSynchronize(e->ws_free);
+    for (auto& q : e->pend)
+        if (q.id && q.done) (void)hipEventSynchronize(q.done);
     for (void* p : e->allocations) (void)hipFree(p);
     if (e->ws) (void)hipFree(e->ws);
     if (e->rope_cos) (void)hipFree(e->rope_cos);
@@ -2704,8 +2709,11 @@ extern "C" int mimi_get_tap(mimi_engine* e, const char* name, float* dst, int64_
     if (dst) {
         if (cap < n) return set_err(MIMI_ERR_INVALID_ARGUMENT, "tap %s needs %lld floats", name, (long long)n);
         HIP_TRY(hipSetDevice(e->device));
-        HIP_TRY(hipDeviceSynchronize());
-        HIP_TRY(hipMemcpy(dst, tp.d, n * 4, hipMemcpyDeviceToHost));
+        // the taps were copied inside the last encode: wait for it alone (a device-wide sync is refused while any
+        // other engine in the process captures a graph)
+        HIP_TRY(hipEventSynchronize(e->ws_free));
+        if (!e->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&e->cap_stream, hipStreamNonBlocking));
+        HIP_TRY(hipMemcpyWithStream(dst, tp.d, n * 4, hipMemcpyDeviceToHost, e->cap_stream));
     }
     return MIMI_OK;
 }

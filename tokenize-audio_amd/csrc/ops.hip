@@ -1629,9 +1629,9 @@ __device__ __forceinline__ void rvq_exact_staged(const float (*img)[FT][LDH], co
                                                  unsigned nc, unsigned long long* best, const float* cbr,
                                                  const float* ynl, int cbase, long long f0, long long frames, int tid,
                                                  float* rowbuf) {
-    constexpr int NWV = NT / 64, RS = D + 4;  // (row stride: + 16 B, conflict-free b128 reads of different rows)
+    [[maybe_unused]] constexpr int NWV = NT / 64, RS = D + 4;  // (row stride: + 16 B, conflict-free b128 reads)
     static_assert(D == 256, "one 16-B piece per lane per row");
-    const int lane = tid & 63, wave = tid >> 6;
+    [[maybe_unused]] const int lane = tid & 63, wave = tid >> 6;
 #if defined(__HIP_DEVICE_COMPILE__)
     // LDS-DMA: no registers held; candidate i's 1-KB row lands at rowbuf + i RS (lane l: floats 4 l .. 4 l + 3)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(cbr), (short)0, 0x7fffffff,
