@@ -93,7 +93,8 @@ def parse():
                     help="wall budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: this process's CPU affinity, capped by OMP_NUM_THREADS)")
-    ap.add_argument("--concurrency", type=int, default=0, help="(ignored: per-utterance encodes run as ragged batches)")
+    ap.add_argument("--concurrency", type=int, default=1,
+                    help="host-fed workloads: engines MimiEncoder's pipeline alternates between (batches overlap)")
     ap.add_argument("--bpe", action="store_true",
                     help="mls workload: after the timed encodes, train codec-BPE (GPU merge loop) over the emitted "
                          "codes on rank 0, timed separately (configs[4])")
@@ -392,7 +393,7 @@ class Workload:
             self.desc = (f"LibriTTS-R-style batch encode (configs[{1 if B <= 32 else 2}]): batch={B} x "
                          f"{args.seconds:g} s @ 24 kHz resident in HBM, K={K} codebooks, 1 encode per step per GPU")
             return
-        enc = MimiEncoder(device=dev, model=model, num_quantizers=K)
+        enc = MimiEncoder(device=dev, model=model, num_quantizers=K, concurrency=max(1, args.concurrency))
         lo, hi = (1.5, 20.0) if self.kind == "yodas2" else (10.0, 20.0)
         n_steps = args.warmup + args.steps
         # the whole shard's utterance list; this rank takes i % world == rank (sharding.py), in batches of B

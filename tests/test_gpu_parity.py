@@ -351,6 +351,28 @@ def test_encode_audio_chunks_equals_per_utterance_calls(engine, golden):
     assert enc.encode_audio_chunks([], 24000) == []
 
 
+def test_pipeline_engines_alternate_same_codes(engine):
+    """concurrency = 2: the pipelined paths alternate consecutive batches between two engines on two streams (they run
+    on the GPU at the same time); encode_batches and encode_audio_chunks must give exactly the one-engine codes."""
+    from mimi_hip.encoder import MimiEncoder
+    rng = np.random.default_rng(17)
+    lens = [int(x) for x in rng.integers(1, 24000 * 16, size=14)]
+    audio = [synthetic.speech_like(L, 41, i) for i, L in enumerate(lens)]
+    batches = [audio[0:4], audio[4:7], audio[7:11], audio[11:14]]
+    one = MimiEncoder(device="cuda:0", model=engine, concurrency=1, chunk_batch=3)
+    two = MimiEncoder(device="cuda:0", model=engine, concurrency=2, chunk_batch=3)
+    ref_b = list(one.encode_batches(batches, 24000))
+    got_b = list(two.encode_batches(batches, 24000))
+    assert len(two._engines) == 2
+    for rb, gb in zip(ref_b, got_b):
+        assert len(rb) == len(gb) and all(np.array_equal(x, y) for x, y in zip(rb, gb))
+    ref_c = one.encode_audio_chunks(audio, 24000)
+    got_c = two.encode_audio_chunks(audio, 24000)
+    for i, (x, y) in enumerate(zip(ref_c, got_c)):
+        assert np.array_equal(x, y), i
+        assert np.array_equal(x, one.encode_audio_chunk(audio[i], 24000)), i
+
+
 @pytest.mark.parametrize("ragged", [True, False])
 def test_padded_batch_b32_vs_reference_wrapper(engine, state_dict, parity_log, ragged):
     """B = 32 mixed lengths U[1.5, 20] s (17 items > 10.24 s: window-250 attention path; items 3 and 7 at -40 /

@@ -67,14 +67,19 @@ def padded_batch_lengths(lengths: Sequence[int]) -> List[int]:
 class _Pipeline:
     """Double-buffered ragged encodes: pinned host staging -> device on a copy stream -> encode on a compute stream.
     Slot k's buffers are reused by the (k + depth)-th submit, after the result of the k-th was collected (its
-    encode finished reading them)."""
+    encode finished reading them).  With several engines (MimiEncoder concurrency > 1) slot k encodes on engine
+    k % n, each engine on its own compute stream with its own workspace, so consecutive batches run on the GPU
+    at the same time; every engine has the same weights and activation scales, so the codes are the same."""
 
-    def __init__(self, model: MimiHipModel, K: int, depth: int = 2):
-        self.model, self.K, self.depth = model, K, depth
-        self.dev = model.device
+    def __init__(self, models, K: int, depth: int = 2):
+        models = list(models) if isinstance(models, (list, tuple)) else [models]
+        self.models, self.model, self.K = models, models[0], K
+        self.depth = max(depth, len(models))
+        self.dev = self.model.device
         self.copy = torch.cuda.Stream(device=self.dev)
-        self.comp = torch.cuda.Stream(device=self.dev)
-        self.slots = [dict(pin=None, din=None, out=None) for _ in range(depth)]
+        self.comps = [torch.cuda.Stream(device=self.dev) for _ in models]
+        self.comp = self.comps[0]
+        self.slots = [dict(pin=None, din=None, out=None) for _ in range(self.depth)]
         self.n = 0
 
     def _buf(self, slot, key, numel, dtype, pinned):
@@ -87,7 +92,9 @@ class _Pipeline:
 
     def submit(self, arrays: List[np.ndarray], enc_lens: List[int], keep: List[int]):
         B, L = len(arrays), max(enc_lens)
-        slot = self.slots[self.n % self.depth]
+        k = self.n % self.depth
+        slot = self.slots[k]
+        model, comp = self.models[k % len(self.models)], self.comps[k % len(self.models)]
         self.n += 1
         pin = self._buf(slot, "pin", B * L, torch.float32, True)[:B * L].view(B, L)
         pn = pin.numpy()
@@ -103,9 +110,9 @@ class _Pipeline:
             din.copy_(pin, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.copy)
-        self.comp.wait_event(ev)
-        with torch.cuda.stream(self.comp):
-            ticket = self.model.encode_ragged_async(din, enc_lens, self.K, out=out)
+        comp.wait_event(ev)
+        with torch.cuda.stream(comp):
+            ticket = model.encode_ragged_async(din, enc_lens, self.K, out=out)
         return ticket, keep
 
     @staticmethod
@@ -131,7 +138,12 @@ class MimiEncoder:
         # first K levels do not depend on the later ones (split RVQ, TF/modeling_mimi.py:1060-1066), so a
         # caller that only keeps K may set num_quantizers=K for the same result with less work.
         self.num_quantizers = num_quantizers
-        self.concurrency = max(1, int(concurrency))  # (kept for API compatibility; ragged batches replace it)
+        # concurrency: engines the pipelined paths (encode_batches, encode_audio_chunks) alternate between, each with
+        # its own workspace and compute stream, so consecutive batches overlap on the GPU (clones share the weights'
+        # values and the activation scales: the same codes)
+        self.concurrency = max(1, int(concurrency))
+        self._engines = [self.model]
+        self._engines_lock = threading.Lock()
         self.ragged = bool(ragged) and hasattr(self.model, "encode_ragged_async")
         self.chunk_batch = max(1, int(chunk_batch))
         self._local = threading.local()  # per-thread _Pipeline (its buffers are never shared between callers)
@@ -175,10 +187,20 @@ class MimiEncoder:
                 x[i, :a.shape[0]].copy_(torch.from_numpy(a))
         return self.model.encode_async(x, self._K).wait().cpu().numpy()
 
+    def _engine_list(self):
+        n = self.concurrency if hasattr(self.model, "clone") else 1
+        with self._engines_lock:
+            while len(self._engines) < n:
+                m = self.model.clone()
+                if hasattr(m, "calibrate"):
+                    m.calibrate()  # (now, not inside the clone's first encode)
+                self._engines.append(m)
+            return self._engines[:n]
+
     def _pipeline(self) -> _Pipeline:
         pipe = getattr(self._local, "pipe", None)
         if pipe is None or pipe.K != self._K:
-            pipe = self._local.pipe = _Pipeline(self.model, self._K)
+            pipe = self._local.pipe = _Pipeline(self._engine_list(), self._K)
         return pipe
 
     def encode_audio_chunk(self, audio_array: np.ndarray, sample_rate: int = 24000) -> np.ndarray:
