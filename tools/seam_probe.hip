@@ -56,7 +56,13 @@ __global__ __launch_bounds__(256) void persistent_kernel(float* buf, unsigned* b
 // two-level barrier: a workgroup arrives on its XCD's counter (workgroups are dealt to the 8 XCDs round-robin), the
 // XCD's last arrival bumps the global counter, the last of those publishes the generation everyone waits on.
 // bar (uints): [16 (x + 1)] XCD counters x = 0..7 (64 B apart), [192] global count, [224] generation, [1] give-ups
+// RELAXED: the same barrier with relaxed atomics and no fences -- no cache write-back / invalidate per arrival, so
+// not a correct barrier for data; the synchronisation's own floor
+template <bool RELAXED>
 __global__ __launch_bounds__(256) void persistent2_kernel(float* buf, unsigned* bar, int phases) {
+    constexpr int ORD_RMW = RELAXED ? __ATOMIC_RELAXED : __ATOMIC_ACQ_REL;
+    constexpr int ORD_ST = RELAXED ? __ATOMIC_RELAXED : __ATOMIC_RELEASE;
+    constexpr int ORD_LD = RELAXED ? __ATOMIC_RELAXED : __ATOMIC_ACQUIRE;
     float* p = buf + (size_t)blockIdx.x * 256 + threadIdx.x;
     const unsigned per_xcd = gridDim.x / 8, x = blockIdx.x & 7;
     __shared__ int bail;
@@ -68,13 +74,13 @@ __global__ __launch_bounds__(256) void persistent2_kernel(float* buf, unsigned* 
         __syncthreads();
         if (threadIdx.x == 0) {
             const unsigned gen = (unsigned)ph + 1;
-            const unsigned old = __hip_atomic_fetch_add(bar + 16 * (x + 1), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned old = __hip_atomic_fetch_add(bar + 16 * (x + 1), 1u, ORD_RMW, __HIP_MEMORY_SCOPE_AGENT);
             if (old == per_xcd * gen - 1) {
-                const unsigned g = __hip_atomic_fetch_add(bar + 192, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-                if (g == 8 * gen - 1) __hip_atomic_store(bar + 224, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned g = __hip_atomic_fetch_add(bar + 192, 1u, ORD_RMW, __HIP_MEMORY_SCOPE_AGENT);
+                if (g == 8 * gen - 1) __hip_atomic_store(bar + 224, gen, ORD_ST, __HIP_MEMORY_SCOPE_AGENT);
             }
             int spins = 0;
-            while (__hip_atomic_load(bar + 224, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < gen) {
+            while (__hip_atomic_load(bar + 224, ORD_LD, __HIP_MEMORY_SCOPE_AGENT) < gen) {
                 if (++spins > (1 << 18)) {
                     __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     bail = 1;
@@ -137,10 +143,16 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms_b, e0, e1));
         unsigned hb[2];
         CK(hipMemcpy(hb, bar, 8, hipMemcpyDeviceToHost));
-        // (b2) the two-level barrier
+        // (b2) the two-level barrier; (b3) the same, relaxed
+        float ms_b3 = 0.0f, ms_b2 = 0.0f;
+        unsigned hb2[2] = {0, 0};
+        for (int relaxed = 1; relaxed >= 0; --relaxed) {
         CK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
         CK(hipMemsetAsync(bar, 0, 1024, s));
-        hipLaunchKernelGGL(persistent2_kernel, dim3(grid), dim3(256), 0, s, buf, bar, phases);
+        if (relaxed)
+            hipLaunchKernelGGL(persistent2_kernel<true>, dim3(grid), dim3(256), 0, s, buf, bar, phases);
+        else
+            hipLaunchKernelGGL(persistent2_kernel<false>, dim3(grid), dim3(256), 0, s, buf, bar, phases);
         hipGraph_t g3;
         hipGraphExec_t gx3;
         CK(hipStreamEndCapture(s, &g3));
@@ -151,12 +163,12 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 20; ++i) CK(hipGraphLaunch(gx3, s));
         CK(hipEventRecord(e1, s));
         CK(hipEventSynchronize(e1));
-        float ms_b2;
         CK(hipEventElapsedTime(&ms_b2, e0, e1));
-        unsigned hb2[2];
         CK(hipMemcpy(hb2, bar, 8, hipMemcpyDeviceToHost));
         CK(hipGraphExecDestroy(gx3));
         CK(hipGraphDestroy(g3));
+        if (relaxed) ms_b3 = ms_b2;
+        }
         // (c) one launch of one phase: the floor both forms pay once
         CK(hipEventRecord(e0, s));
         for (int i = 0; i < 20; ++i) hipLaunchKernelGGL(phase_kernel, dim3(grid), dim3(256), 0, s, buf, i);
@@ -164,6 +176,8 @@ int main(int argc, char** argv) {
         CK(hipEventSynchronize(e1));
         float ms_c;
         CK(hipEventElapsedTime(&ms_c, e0, e1));
+        printf("grid %4d: relaxed two-level barrier (synchronisation floor) %7.2f us (%.2f us per seam)\n", grid,
+               ms_b3 * 1000 / 20, ms_b3 * 1000 / 20 / (phases - 1));
         printf("grid %4d (%d per CU), %d phases: graph of launches %7.2f us (%.2f us per seam); persistent + grid "
                "barriers %7.2f us (%.2f us per seam; gave up: %u); two-level barrier %7.2f us (%.2f us per seam; "
                "gave up: %u); single launch %.2f us\n",
