@@ -332,7 +332,7 @@ struct mimi_engine {
     std::map<std::tuple<int, int64_t, int>, int> graph_seen;  // eager encodes per shape (capture on the 2nd)
     bool graphs_enabled = true;
     bool capturing = false;
-    void** io_dev = nullptr;  // [audio, codes] of the replay
+    void** io_dev = nullptr;  // [audio, codes, pinned maxima, pinned give-up word] of the replay
     hipStream_t cap_stream = nullptr;
     int ws_gen = 0, rope_gen = 0;
     uint64_t graph_clock = 0;
@@ -1976,7 +1976,7 @@ static void drop_graphs(mimi_engine* e) {
 // caller runs the eager pass (the error is cleared: a graph is an optimisation, never a requirement).
 static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int B, int64_t L, int K,
                                           int32_t* codes) {
-    if (!e->io_dev && hipMalloc(&e->io_dev, 2 * sizeof(void*)) != hipSuccess) {
+    if (!e->io_dev && hipMalloc(&e->io_dev, 4 * sizeof(void*)) != hipSuccess) {
         (void)hipGetLastError();
         e->io_dev = nullptr;
         return nullptr;
@@ -1998,6 +1998,10 @@ static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int
     // from the zeros the previous encode's fold left behind)
     rc = encode_pass(e, audio, B, L, K, codes, cs, PREC_F16X3);
     if (!rc && launch_amax_reduce(e->amax_dev, (int)e->slot_of.size(), e->amax_red, cs) != hipSuccess) rc = MIMI_ERR_HIP;
+    // the ticket's host words from inside the graph (destinations through io_dev, set before each replay)
+    if (!rc && launch_ticket_out(e->amax_red, (int)e->slot_of.size(), nullptr, e->chain_flag, nullptr, cs,
+                                 e->io_dev) != hipSuccess)
+        rc = MIMI_ERR_HIP;
     e->capturing = false;
     hipGraph_t g = nullptr;
     const hipError_t ec = hipStreamEndCapture(cs, &g);
@@ -2031,7 +2035,7 @@ static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int
 // Runs the f16x3 pass of (B, L, K) as a graph replay on s when it can (*replayed = true); otherwise leaves
 // everything to the eager path.
 static int graph_encode(mimi_engine* e, const float* audio, int B, int64_t L, int K, int32_t* codes, hipStream_t s,
-                        bool* replayed, unsigned** chain_flag) {
+                        bool* replayed, unsigned** chain_flag, unsigned* host_amax, unsigned* host_flag) {
     *replayed = false;
     *chain_flag = nullptr;
     if (!e->graphs_enabled || e->profiling || e->taps || e->calibrating) return MIMI_OK;
@@ -2062,7 +2066,7 @@ static int graph_encode(mimi_engine* e, const float* audio, int B, int64_t L, in
     }
     gr->used = ++e->graph_clock;
     HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));
-    LAUNCH_TRY(launch_set_io(e->io_dev, audio, codes, s), "set_io");
+    LAUNCH_TRY(launch_set_io(e->io_dev, audio, codes, s, host_amax, host_flag), "set_io");
     HIP_TRY(hipGraphLaunch(gr->x, s));
     ++e->graph_replays;
     *replayed = true;
@@ -2143,7 +2147,9 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
             explicit ChainScope(mimi_engine* x) : e(x) { e->chain_ok = true; }
             ~ChainScope() { e->chain_ok = false; }
         } chain_scope(e);
-        if (!lengths && (rc = graph_encode(e, audio, B, L, K, codes, s, &replayed, &cflag))) return rc;
+        if (!lengths &&
+            (rc = graph_encode(e, audio, B, L, K, codes, s, &replayed, &cflag, P->amax, P->chain_word)))
+            return rc;
         n = (int)e->slot_of.size();
         if (!replayed) {
             HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));  // the maxima buffers are part of the workspace
@@ -2158,11 +2164,12 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
             LAUNCH_TRY(launch_amax_reduce(e->amax_dev, n, e->amax_red, s), "amax_reduce");
             cflag = e->chain_flag;
         }
-        HIP_TRY(hipMemcpyAsync(P->amax, e->amax_red, n * sizeof(unsigned), hipMemcpyDeviceToHost, s));
-        if (cflag) {  // (before ws_free: the next encode's memset node zeroes the flag)
-            HIP_TRY(hipMemcpyAsync(P->chain_word, cflag, sizeof(unsigned), hipMemcpyDeviceToHost, s));
-            P->chain = true;
-        }
+        // the maxima and (chain) the give-up flag into the ticket's pinned words, before ws_free (the next encode's
+        // memset node zeroes the flag); a replay's graph ends with the same kernel (capture_graph)
+        if (!replayed)
+            LAUNCH_TRY(launch_ticket_out(e->amax_red, n, P->amax, cflag, cflag ? P->chain_word : nullptr, s),
+                       "ticket_out");
+        P->chain = cflag != nullptr;
         HIP_TRY(hipEventRecord(e->ws_free, s));
     } else if ((rc = encode_pass(e, audio, B, L, K, codes, s, prec))) {
         return rc;

@@ -1203,14 +1203,18 @@ hipError_t launch_ragged_rows(const int* tlen, const int* toff, int B, int* rpos
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(64) void set_io_kernel(void** io, const float* audio, int32_t* codes) {
+__global__ __launch_bounds__(64) void set_io_kernel(void** io, const float* audio, int32_t* codes, unsigned* hamax,
+                                                    unsigned* hflag) {
     if (threadIdx.x == 0) {
         io[0] = const_cast<float*>(audio);
         io[1] = codes;
+        io[2] = hamax;
+        io[3] = hflag;
     }
 }
-hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStream_t s) {
-    hipLaunchKernelGGL(set_io_kernel, dim3(1), dim3(64), 0, s, io, audio, codes);
+hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStream_t s, unsigned* hamax,
+                         unsigned* hflag) {
+    hipLaunchKernelGGL(set_io_kernel, dim3(1), dim3(64), 0, s, io, audio, codes, hamax, hflag);
     return hipGetLastError();
 }
 
@@ -1229,6 +1233,27 @@ hipError_t launch_amax_reduce(unsigned* amax, int nslots, unsigned* out, hipStre
     if (nslots <= 0) return hipSuccess;
     static_assert(AMAX_SUB <= 64, "one wave per slot");
     hipLaunchKernelGGL(amax_reduce_kernel, dim3(nslots), dim3(64), 0, s, amax, out);
+    return hipGetLastError();
+}
+
+// An encode ticket's host words written by the device into their pinned slots: the folded maxima and the persistent
+// RVQ chain's give-up flag (one launch in place of two D2H copy launches, ~7 us each at batch 1)
+// (io != null: a graph replay's destinations, io[2] / io[3] as set_io_kernel wrote them before the replay)
+__global__ __launch_bounds__(64) void ticket_out_kernel(const unsigned* __restrict__ amax, int n, unsigned* hamax,
+                                                        const unsigned* __restrict__ flag, unsigned* hflag,
+                                                        void* const* __restrict__ io) {
+    if (io) {
+        hamax = static_cast<unsigned*>(io[2]);
+        hflag = static_cast<unsigned*>(io[3]);
+    }
+    for (int i = threadIdx.x; i < n; i += 64) hamax[i] = amax[i];
+    if (flag && hflag && threadIdx.x == 0) hflag[0] = *flag;
+}
+
+hipError_t launch_ticket_out(const unsigned* amax, int n, unsigned* hamax, const unsigned* flag, unsigned* hflag,
+                             hipStream_t s, void* const* io) {
+    if (n < 0 || (n > 0 && !amax) || (!io && ((n > 0 && !hamax) || (!flag != !hflag)))) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ticket_out_kernel, dim3(1), dim3(64), 0, s, amax, n, hamax, flag, hflag, io);
     return hipGetLastError();
 }
 
