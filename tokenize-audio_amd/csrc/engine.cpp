@@ -1997,10 +1997,9 @@ static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int
     // (no maxima reset node: amax_reduce_kernel leaves every sub-slot at 0 as it reads it, so a replay starts
     // from the zeros the previous encode's fold left behind)
     rc = encode_pass(e, audio, B, L, K, codes, cs, PREC_F16X3);
-    if (!rc && launch_amax_reduce(e->amax_dev, (int)e->slot_of.size(), e->amax_red, cs) != hipSuccess) rc = MIMI_ERR_HIP;
-    // the ticket's host words from inside the graph (destinations through io_dev, set before each replay)
-    if (!rc && launch_ticket_out(e->amax_red, (int)e->slot_of.size(), nullptr, e->chain_flag, nullptr, cs,
-                                 e->io_dev) != hipSuccess)
+    // (+ the ticket's host words from inside the graph: destinations through io_dev, set before each replay)
+    if (!rc && launch_amax_reduce(e->amax_dev, (int)e->slot_of.size(), e->amax_red, cs, nullptr, e->chain_flag, nullptr,
+                                  e->io_dev) != hipSuccess)
         rc = MIMI_ERR_HIP;
     e->capturing = false;
     hipGraph_t g = nullptr;
@@ -2161,14 +2160,12 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
                 e->uncalibrated_slot = false;
                 return set_err(MIMI_ERR_STATE, "f16x3: an activation has no calibrated scale");
             }
-            LAUNCH_TRY(launch_amax_reduce(e->amax_dev, n, e->amax_red, s), "amax_reduce");
             cflag = e->chain_flag;
+            // the maxima and (chain) the give-up flag also into the ticket's pinned words, before ws_free (the next
+            // encode's memset node zeroes the flag); a replay's graph ends with the same kernel (capture_graph)
+            LAUNCH_TRY(launch_amax_reduce(e->amax_dev, n, e->amax_red, s, P->amax, cflag, cflag ? P->chain_word : nullptr),
+                       "amax_reduce");
         }
-        // the maxima and (chain) the give-up flag into the ticket's pinned words, before ws_free (the next encode's
-        // memset node zeroes the flag); a replay's graph ends with the same kernel (capture_graph)
-        if (!replayed)
-            LAUNCH_TRY(launch_ticket_out(e->amax_red, n, P->amax, cflag, cflag ? P->chain_word : nullptr, s),
-                       "ticket_out");
         P->chain = cflag != nullptr;
         HIP_TRY(hipEventRecord(e->ws_free, s));
     } else if ((rc = encode_pass(e, audio, B, L, K, codes, s, prec))) {

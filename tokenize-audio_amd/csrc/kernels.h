@@ -157,11 +157,10 @@ hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStrea
                          unsigned* hflag = nullptr);
 
 // out[i] = max over the AMAX_SUB sub-slots of slot i (one wave per slot); the sub-slots are left at 0
-hipError_t launch_amax_reduce(unsigned* amax, int nslots, unsigned* out, hipStream_t s);
-// an encode ticket's pinned host words: hamax[0 .. n) = amax[0 .. n), and *hflag = *flag when both are given; io:
-// take hamax / hflag from io[2] / io[3] (set_io) at run time -- the form a captured graph holds
-hipError_t launch_ticket_out(const unsigned* amax, int n, unsigned* hamax, const unsigned* flag, unsigned* hflag,
-                             hipStream_t s, void* const* io = nullptr);
+// (+ an encode ticket's pinned host words: hamax[slot] = the folded maximum, *hflag = *flag when both are given; io:
+// take hamax / hflag from io[2] / io[3] (set_io) at run time -- the form a captured graph holds)
+hipError_t launch_amax_reduce(unsigned* amax, int nslots, unsigned* out, hipStream_t s, unsigned* hamax = nullptr,
+                              const unsigned* flag = nullptr, unsigned* hflag = nullptr, void* const* io = nullptr);
 
 // Epilogues of the implicit-GEMM conv / linear kernel.
 enum Epi : int {

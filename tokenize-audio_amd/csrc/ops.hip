@@ -1221,39 +1221,32 @@ hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStrea
 // Each sub-slot is read AND reset to 0 by one device-scope atomic exchange (at the memory side, like the
 // producers' atomicMax): no XCD's L2 can hand this fold a stale line, and the next encode (or graph replay)
 // starts from zeros without a memset.
-__global__ __launch_bounds__(64) void amax_reduce_kernel(unsigned* __restrict__ amax, unsigned* __restrict__ out) {
-    unsigned* a = amax + (long long)blockIdx.x * AMAX_SLOT_WORDS;
-    unsigned v = threadIdx.x < AMAX_SUB ? atomicExch(a + threadIdx.x * AMAX_STRIDE, 0u) : 0u;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
-    if (threadIdx.x == 0) out[blockIdx.x] = v;
-}
-
-hipError_t launch_amax_reduce(unsigned* amax, int nslots, unsigned* out, hipStream_t s) {
-    if (nslots <= 0) return hipSuccess;
-    static_assert(AMAX_SUB <= 64, "one wave per slot");
-    hipLaunchKernelGGL(amax_reduce_kernel, dim3(nslots), dim3(64), 0, s, amax, out);
-    return hipGetLastError();
-}
-
-// An encode ticket's host words written by the device into their pinned slots: the folded maxima and the persistent
-// RVQ chain's give-up flag (one launch in place of two D2H copy launches, ~7 us each at batch 1)
-// (io != null: a graph replay's destinations, io[2] / io[3] as set_io_kernel wrote them before the replay)
-__global__ __launch_bounds__(64) void ticket_out_kernel(const unsigned* __restrict__ amax, int n, unsigned* hamax,
-                                                        const unsigned* __restrict__ flag, unsigned* hflag,
-                                                        void* const* __restrict__ io) {
+// With a ticket (hamax: pinned host words) the folded maxima also go straight to the host, and workgroup 0 copies the
+// persistent RVQ chain's give-up flag beside them -- in place of two D2H copy launches after the encode (~7 us each
+// at batch 1).  io != null: a graph replay's destinations, io[2] / io[3] as set_io_kernel wrote them before it.
+__global__ __launch_bounds__(64) void amax_reduce_kernel(unsigned* __restrict__ amax, unsigned* __restrict__ out,
+                                                         unsigned* hamax, const unsigned* __restrict__ flag,
+                                                         unsigned* hflag, void* const* __restrict__ io) {
     if (io) {
         hamax = static_cast<unsigned*>(io[2]);
         hflag = static_cast<unsigned*>(io[3]);
     }
-    for (int i = threadIdx.x; i < n; i += 64) hamax[i] = amax[i];
-    if (flag && hflag && threadIdx.x == 0) hflag[0] = *flag;
+    unsigned* a = amax + (long long)blockIdx.x * AMAX_SLOT_WORDS;
+    unsigned v = threadIdx.x < AMAX_SUB ? atomicExch(a + threadIdx.x * AMAX_STRIDE, 0u) : 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
+    if (threadIdx.x == 0) {
+        out[blockIdx.x] = v;
+        if (hamax) hamax[blockIdx.x] = v;
+        if (blockIdx.x == 0 && flag && hflag) hflag[0] = *flag;
+    }
 }
 
-hipError_t launch_ticket_out(const unsigned* amax, int n, unsigned* hamax, const unsigned* flag, unsigned* hflag,
-                             hipStream_t s, void* const* io) {
-    if (n < 0 || (n > 0 && !amax) || (!io && ((n > 0 && !hamax) || (!flag != !hflag)))) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(ticket_out_kernel, dim3(1), dim3(64), 0, s, amax, n, hamax, flag, hflag, io);
+hipError_t launch_amax_reduce(unsigned* amax, int nslots, unsigned* out, hipStream_t s, unsigned* hamax,
+                              const unsigned* flag, unsigned* hflag, void* const* io) {
+    if (nslots <= 0) return hipSuccess;
+    static_assert(AMAX_SUB <= 64, "one wave per slot");
+    hipLaunchKernelGGL(amax_reduce_kernel, dim3(nslots), dim3(64), 0, s, amax, out, hamax, flag, hflag, io);
     return hipGetLastError();
 }
 
