@@ -35,7 +35,7 @@ namespace mimi {
 // ------------------------------------------------------------------------------------------------
 template <int BM, int BN, int WM, int WN, int BK, int NBUF, bool NFAST, bool ELU_IN, int PAD, int EPI, int TAG>
 static const char* kernel_symbol() {
-    static char name[160];
+    static thread_local char name[160];
     if (!name[0])
         snprintf(name, sizeof(name), "mimi::gemm_f32_kernel<%d, %d, %d, %d, %d, %d, %s, %s, %d, %d, %d>", BM, BN, WM,
                  WN, BK, NBUF, NFAST ? "true" : "false", ELU_IN ? "true" : "false", PAD, EPI, TAG);
@@ -56,7 +56,7 @@ static hipError_t run(const GemmArgs& a, hipStream_t s) {
 
 template <int BM, int BN, int WM, int WN, int NS, bool ELU_IN, int PAD, int EPI, int TAG>
 static hipError_t run_split(const GemmArgs& a, hipStream_t s) {
-    static char name[160];
+    static thread_local char name[160];
     if (!name[0])
         snprintf(name, sizeof(name), "mimi::gemm_bf16x_kernel<%d, %d, %d, %d, %d, %s, %d, %d, %d>", BM, BN, WM, WN, NS,
                  ELU_IN ? "true" : "false", PAD, EPI, TAG);
@@ -77,7 +77,7 @@ static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
             return run_planes<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL | FL_RAGGED, F16>(a, s);
         }
     }
-    static char name[160];
+    static thread_local char name[160];
     if (!name[0])
         snprintf(name, sizeof(name), "mimi::gemm_planes_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %d, %s>", BM,
                  BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL, F16 ? "true" : "false");
@@ -101,14 +101,13 @@ static hipError_t run_planes(const GemmArgs& a, hipStream_t s) {
     auto kern = gemm_planes_kernel<BM, BN, WM, WN, NS, ST, EPI, OUTP, TAG, LW, BK, MF, FL, F16>;
     long long grid = nwg;
     if (FL & FL_PERSIST) {  // one workgroup per resident slot, a multiple of the 8 XCDs
-        static int slots = 0;
-        if (!slots) {
+        static const int slots = [kern] {  // (once per instantiation; thread-safe initialisation)
             int dev = 0, ncu = 256, occ = 1;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, (WM * WN + LW) * 64, 0);
-            slots = std::max(8, ncu * std::max(1, occ) / 8 * 8);
-        }
+            return std::max(8, ncu * std::max(1, occ) / 8 * 8);
+        }();
         grid = std::min<long long>(nwg, slots);
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3((WM * WN + LW) * 64), 0, s, a);

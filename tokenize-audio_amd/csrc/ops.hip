@@ -2204,8 +2204,7 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
 // whether the chain's whole grid is resident at once by the occupancy query (this process's view: other processes'
 // kernels can still hold CUs for a while, which the bounded sweeps and the give-up flag cover)
 static bool rvq_chain_fits(unsigned grid) {
-    static int cap = -1;
-    if (cap < 0) {
+    static const int cap = [] {  // (once; thread-safe initialisation)
         int dev = 0, ncu = 0, nb = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -2213,8 +2212,8 @@ static bool rvq_chain_fits(unsigned grid) {
             (void)hipGetLastError();
             nb = ncu = 0;
         }
-        cap = nb * ncu;
-    }
+        return nb * ncu;
+    }();
     return grid <= (unsigned)cap;
 }
 
@@ -2253,7 +2252,7 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname, un
             unsigned long long* gbase = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.work) + pd_off);
             const hipError_t me = hipMemsetAsync(gbase, 0, gbytes, s);  // flag + granules: every launch (and replay)
             if (me != hipSuccess) return me;
-            static char knc[96];
+            static thread_local char knc[96];
             snprintf(knc, sizeof knc, "mimi::rvq_chain_h16_kernel<256, 16>");
             *kname = knc;
             (void)nchain;
@@ -2268,7 +2267,7 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname, un
         const unsigned ftiles = (unsigned)((a.frames + ft - 1) / ft);
         constexpr int nwv = 8;
         const unsigned nsl = 2048 / (scfg ? nwv * 32 : 8 * 64);
-        static char kn[112];
+        static thread_local char kn[112];
         snprintf(kn, sizeof kn, "mimi::rvq_level_h16_kernel<256, %d, %d, %s, %d, %d, %d, %s>", pf, scfg ? 32 : 16,
                  a.flen ? "true" : "false", scfg ? 32 : 64, nwv, ft, p1 ? "true" : "false");
         *kname = kn;

@@ -193,21 +193,20 @@ bool res1_stream_ok(const GemmArgs& a) {
 template <int DEPTH, int CPW>
 static hipError_t run_res1_stream(const GemmArgs& a, hipStream_t s, const char** kname) {
     constexpr int NT = 256 / CPW * 64;
-    static char nm[80];
+    static thread_local char nm[80];
     const bool rg = a.m_rows != nullptr;
     snprintf(nm, sizeof nm, "mimi::res1_stream_kernel<128, %d, %d, %s>(mimi::GemmArgs, int)", DEPTH, CPW,
              rg ? "true" : "false");
     if (kname) *kname = nm;
     const long long rows = (long long)a.M * a.batch;
     const int ntiles = (int)((rows + 15) / 16);
-    static int slots = 0;
-    if (!slots) {
+    static const int slots = [] {  // (once per instantiation; thread-safe initialisation)
         int dev = 0, ncu = 256, occ = 1;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, res1_stream_kernel<128, DEPTH, CPW, false>, NT, 0);
-        slots = ncu * (occ > 0 ? occ : 1);
-    }
+        return ncu * (occ > 0 ? occ : 1);
+    }();
     const int grid = ntiles < slots ? ntiles : slots;
     if (rg)
         hipLaunchKernelGGL((res1_stream_kernel<128, DEPTH, CPW, true>), dim3((unsigned)grid), dim3(NT), 0, s, a, ntiles);

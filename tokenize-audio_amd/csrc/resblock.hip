@@ -1007,7 +1007,7 @@ __global__ __launch_bounds__(512 / NN) __attribute__((amdgpu_waves_per_eu(NN))) 
 
 template <int C, int BM, bool WINDOW, bool FIRST, int W1M, int W1N, int W2M, int W2N, int NP>
 static hipError_t run_res(const ResArgs& a, hipStream_t s, const char** kname) {
-    static char name[160];
+    static thread_local char name[160];
     if (!name[0])
         snprintf(name, sizeof(name), "mimi::resblock_kernel<%d, %d, %s, %s, %d, %d, %d, %d, %d>", C, BM,
                  WINDOW ? "true" : "false", FIRST ? "true" : "false", W1M, W1N, W2M, W2N, NP);
