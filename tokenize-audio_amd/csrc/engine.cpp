@@ -326,6 +326,7 @@ struct mimi_engine {
         hipGraphExec_t x = nullptr;
         uint64_t used = 0;
         unsigned* chain_flag = nullptr;  // the captured RVQ chain's give-up flag (null: no chain in the graph)
+        size_t chain_clear = 0;          // bytes from chain_flag zeroed before each replay (set_io_kernel)
     };
     static constexpr int kMaxGraphs = 8;
     std::vector<Graph> graphs;
@@ -333,6 +334,7 @@ struct mimi_engine {
     bool graphs_enabled = true;
     bool capturing = false;
     void** io_dev = nullptr;  // [audio, codes, pinned maxima, pinned give-up word] of the replay
+    size_t cap_chain_clear = 0;  // (capture) the captured chain's flag + granule bytes
     hipStream_t cap_stream = nullptr;
     int ws_gen = 0, rope_gen = 0;
     uint64_t graph_clock = 0;
@@ -1273,8 +1275,10 @@ static int run_rvq(mimi_engine* e, const float* proj, int64_t frames, int K, int
     const char* kname = "?";
     unsigned* cflag = nullptr;
     e->chain_flag = nullptr;
-    LAUNCH_TRY(launch_rvq(r, s, &kname, e->chain_ok ? &cflag : nullptr), "rvq");
+    size_t clear = 0;  // (capturing: the replay's set_io_kernel zeroes the chain's words instead of a memset node)
+    LAUNCH_TRY(launch_rvq(r, s, &kname, e->chain_ok ? &cflag : nullptr, e->capturing ? &clear : nullptr), "rvq");
     e->chain_flag = cflag;
+    if (e->capturing) e->cap_chain_clear = cflag ? clear : 0;
     rec.mark("rvq", 2.0 * frames * valid_share * r.D * r.ncodes * K,
              (double)frames * (2 * r.D) * 4 + (double)frames * K * 4, kname);
     return MIMI_OK;
@@ -1992,6 +1996,7 @@ static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int
         return nullptr;
     }
     e->capturing = true;
+    e->cap_chain_clear = 0;
     e->uncalibrated_slot = false;
     int rc = MIMI_OK;
     // (no maxima reset node: amax_reduce_kernel leaves every sub-slot at 0 as it reads it, so a replay starts
@@ -2027,6 +2032,7 @@ static mimi_engine::Graph* capture_graph(mimi_engine* e, const float* audio, int
     ng.g = g;
     ng.x = x;
     ng.chain_flag = e->chain_flag;
+    ng.chain_clear = e->chain_flag ? e->cap_chain_clear : 0;
     e->graphs.push_back(ng);
     return &e->graphs.back();
 }
@@ -2065,7 +2071,8 @@ static int graph_encode(mimi_engine* e, const float* audio, int B, int64_t L, in
     }
     gr->used = ++e->graph_clock;
     HIP_TRY(hipStreamWaitEvent(s, e->ws_free, 0));
-    LAUNCH_TRY(launch_set_io(e->io_dev, audio, codes, s, host_amax, host_flag), "set_io");
+    LAUNCH_TRY(launch_set_io(e->io_dev, audio, codes, s, host_amax, host_flag, gr->chain_flag, gr->chain_clear),
+               "set_io");
     HIP_TRY(hipGraphLaunch(gr->x, s));
     ++e->graph_replays;
     *replayed = true;

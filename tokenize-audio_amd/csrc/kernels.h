@@ -154,7 +154,7 @@ __device__ __forceinline__ T* io_pointer(T* const* ref, T* direct) {
 }
 // io[0] = audio, io[1] = codes (the pointers of one graph replay)
 hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStream_t s, unsigned* hamax = nullptr,
-                         unsigned* hflag = nullptr);
+                         unsigned* hflag = nullptr, void* zero = nullptr, size_t zero_bytes = 0);
 
 // out[i] = max over the AMAX_SUB sub-slots of slot i (one wave per slot); the sub-slots are left at 0
 // (+ an encode ticket's pinned host words: hamax[slot] = the folded maximum, *hflag = *flag when both are given; io:
@@ -436,7 +436,10 @@ size_t rvq_work_bytes(long long frames);
 // kname: the level kernel's symbol.  chain_flag (may be null): set to the device word the persistent chain raises when a
 // sweep gave up (the launch's codes are then invalid and the caller re-runs without the chain), or to null when this
 // launch did not take the chain
-hipError_t launch_rvq(const RvqArgs& a, hipStream_t s, const char** kname = nullptr, unsigned** chain_flag = nullptr);
+// clear_bytes (with chain_flag): the persistent chain's flag + granules are NOT zeroed here; *clear_bytes = how many
+// bytes from *chain_flag the caller zeroes before every launch (a captured graph's replays: set_io_kernel)
+hipError_t launch_rvq(const RvqArgs& a, hipStream_t s, const char** kname = nullptr, unsigned** chain_flag = nullptr,
+                      size_t* clear_bytes = nullptr);
 
 // polyphase resampler (resample.hip): clips packed at in_off / out_off (device int64 arrays), one launch
 hipError_t launch_resample_poly(const float* x, const long long* in_off, const long long* in_len, int nclips,

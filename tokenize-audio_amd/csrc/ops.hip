@@ -1203,18 +1203,23 @@ hipError_t launch_ragged_rows(const int* tlen, const int* toff, int B, int* rpos
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(64) void set_io_kernel(void** io, const float* audio, int32_t* codes, unsigned* hamax,
-                                                    unsigned* hflag) {
+// (+ zeroes the replay's RVQ chain flag and granules, n16 16-B units from zero: the memset node a graph would hold)
+__global__ __launch_bounds__(256) void set_io_kernel(void** io, const float* audio, int32_t* codes, unsigned* hamax,
+                                                     unsigned* hflag, uint4* zero, long long n16) {
     if (threadIdx.x == 0) {
         io[0] = const_cast<float*>(audio);
         io[1] = codes;
         io[2] = hamax;
         io[3] = hflag;
     }
+    const uint4 z = {0u, 0u, 0u, 0u};
+    for (long long i = threadIdx.x; i < n16; i += 256) zero[i] = z;
 }
 hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStream_t s, unsigned* hamax,
-                         unsigned* hflag) {
-    hipLaunchKernelGGL(set_io_kernel, dim3(1), dim3(64), 0, s, io, audio, codes, hamax, hflag);
+                         unsigned* hflag, void* zero, size_t zero_bytes) {
+    if (zero_bytes % 16 || (zero_bytes && (!zero || reinterpret_cast<uintptr_t>(zero) % 16))) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(set_io_kernel, dim3(1), dim3(256), 0, s, io, audio, codes, hamax, hflag,
+                       static_cast<uint4*>(zero), (long long)(zero_bytes / 16));
     return hipGetLastError();
 }
 
@@ -2217,7 +2222,8 @@ static bool rvq_chain_fits(unsigned grid) {
     return grid <= (unsigned)cap;
 }
 
-hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname, unsigned** chain_flag) {
+hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname, unsigned** chain_flag,
+                      size_t* clear_bytes) {
     const char* kn_dummy = nullptr;
     if (!kname) kname = &kn_dummy;
     if (chain_flag) *chain_flag = nullptr;
@@ -2250,8 +2256,14 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname, un
             const size_t pd_off = (size_t)2 * ((a.frames + RVQ_FT - 1) / RVQ_FT * RVQ_FT) * a.D * 4;
             if (gbytes > rvq_work_bytes(a.frames) - pd_off) return hipErrorInvalidValue;
             unsigned long long* gbase = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.work) + pd_off);
-            const hipError_t me = hipMemsetAsync(gbase, 0, gbytes, s);  // flag + granules: every launch (and replay)
-            if (me != hipSuccess) return me;
+            // flag + granules zeroed before every launch: by a memset here, or (clear_bytes: a captured graph) by the
+            // caller before each replay (set_io_kernel), *clear_bytes bytes from the returned flag's address
+            if (clear_bytes) {
+                *clear_bytes = gbytes;
+            } else {
+                const hipError_t me = hipMemsetAsync(gbase, 0, gbytes, s);
+                if (me != hipSuccess) return me;
+            }
             static thread_local char knc[96];
             snprintf(knc, sizeof knc, "mimi::rvq_chain_h16_kernel<256, 16>");
             *kname = knc;
