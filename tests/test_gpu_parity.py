@@ -550,14 +550,15 @@ def test_long_clip_batch_properties(engine):
 
 def test_graph_replay_identical(engine):
     """hipGraph replays (2nd+ encode of a shape) give the eager codes for new audio / codes buffers, across
-    interleaved shapes and a workspace reallocation (which retires the captured graphs)."""
+    interleaved shapes and a workspace reallocation (which retires the captured graphs) -- without the persistent
+    RVQ chain giving up (its words are zeroed by set_io_kernel before each replay, not inside the graph)."""
     rng = np.random.default_rng(5)
     clips = {L: [torch.from_numpy(synthetic.clip_batch(B, L, seed=int(rng.integers(1 << 30)))).cuda()
                  for _ in range(3)] for B, L in ((1, 240000), (2, 96000))}
     engine.set_graphs(False)
     ref = {L: [engine.encode_int32(a, 8).cpu() for a in v] for L, v in clips.items()}
     engine.set_graphs(True)
-    before = engine.graph_replays
+    before, reruns = engine.graph_replays, engine.rvq_chain_reruns
     for rnd in range(3):
         for L, v in clips.items():
             for a, r in zip(v, ref[L]):
@@ -565,6 +566,7 @@ def test_graph_replay_identical(engine):
         if rnd == 1:  # a bigger workspace: the graphs of the smaller shapes are recaptured
             engine.encode_int32(torch.zeros(4, 480000, device="cuda"), 8)
     assert engine.graph_replays - before >= 8, engine.graph_replays - before
+    assert engine.rvq_chain_reruns == reruns
 
 
 def test_thread_safety(engine):
