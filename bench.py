@@ -613,6 +613,44 @@ def train_bpe_over_codes(args, wl, dist, rank, world, device, encode_s):
     return out
 
 
+def rank_map(dist, backend, world, rank, local, dev, audio_s, elapsed_s):
+    """Every rank's device as the driver sees it, so an N-GPU line can show that it ran on N distinct GPUs:
+    [{rank, local_rank, host, device, pci_bus, name, audio_s, elapsed_s}] in rank order, plus the process group's own
+    world size.  Under nccl (RCCL) two ranks on one PCI device of one host are an error -- a line from ranks sharing a
+    GPU must not pass for an N-GPU measurement; the gloo rehearsal (MIMI_BENCH_DIST_BACKEND=gloo, ranks sharing the
+    box's GPUs) is allowed and labelled `sharing`.  (One GPU per job is the reference's unit of work:
+    yodas2-mimi/submit/job_template.sh:10.)"""
+    import socket
+
+    import torch
+    p = torch.cuda.get_device_properties(dev)
+    bus = "{:04x}:{:02x}:{:02x}".format(getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", -1) & 0xFF,
+                                        getattr(p, "pci_device_id", -1) & 0xFF)
+    mine = {"rank": rank, "local_rank": local, "host": socket.gethostname(), "device": dev.index, "pci_bus": bus,
+            "name": p.name, "audio_s": round(audio_s, 3), "elapsed_s": round(elapsed_s, 6)}
+    if dist is None:
+        ranks = [mine]
+        pg_world = 1
+    else:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        pg_world = dist.get_world_size()
+    return ranks, check_rank_places(ranks, backend if dist is not None else "none", pg_world, world)
+
+
+def check_rank_places(ranks, backend, pg_world, world):
+    """The `dist` object of the line from the gathered rank map; SystemExit when the map contradicts an N-GPU claim
+    (a process group of another size, or two nccl ranks on one device of one host)."""
+    places = {(r["host"], r["pci_bus"]) for r in ranks}
+    sharing = len(places) < len(ranks)
+    if pg_world != world or len(ranks) != world:
+        sys.exit(f"bench.py: the process group has {pg_world} ranks ({len(ranks)} reported), WORLD_SIZE says {world}")
+    if sharing and backend == "nccl":
+        sys.exit("bench.py: ranks share a GPU under nccl: " +
+                 ", ".join(f"rank {r['rank']} -> {r['host']} {r['pci_bus']}" for r in ranks))
+    return {"backend": backend, "world_size": pg_world, "distinct_devices": len(places), "sharing": sharing}
+
+
 def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
@@ -710,6 +748,8 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed, audio_s = float(tmax.item()), float(t[1].item())
+    ranks, dist_info = rank_map(dist, backend, world, rank, local, dev, wl.timed_seconds(args.warmup, args.steps),
+                                t1 - t0)
     prof, lead = {}, {}
     if lead_only:
         model.set_profiling(False)
@@ -746,6 +786,8 @@ def main():
                    "clip_seconds": args.seconds if wl.kind == "batch" else "mixed",
                    "num_quantizers": K, "parallelism": f"utterance round-robin x{world} (no collective)",
                    "gemm_precision": model.precision},
+        "ranks": ranks,
+        "dist": dist_info,
     }
     if model.precision == "f16x3":
         # fixed activation scales on these weights: overflow fallbacks taken, and the tightest tensor's headroom

@@ -5,7 +5,8 @@
  * ``transformers.MimiModel`` (no native FFI of its own); the entry points below are what a binding of that
  * path binds, one for one:
  *
- *   mimi_create / mimi_load_safetensors / mimi_set_weight / mimi_finalize
+ *   mimi_create_from_dir (one call), or mimi_config_from_json + mimi_create / mimi_load_safetensors /
+ *   mimi_set_weight / mimi_finalize
  *       replace ``MimiModel.from_pretrained(model_id).to(device).eval()``
  *       (/root/reference/emilia-mimi/process_shard.py:57-60; TF/modeling_mimi.py:1186-1228)
  *   mimi_encode
@@ -77,6 +78,25 @@ typedef struct mimi_config {
 /* Fill *cfg with the kyutai/mimi defaults. */
 void mimi_config_default(mimi_config* cfg);
 
+/*
+ * Read a checkpoint's HF config.json (path = the file, or a directory holding it) into *cfg: the encode-path
+ * fields of MimiConfig (TF/configuration_mimi.py:86-175; unknown keys ignored, absent keys keep the defaults,
+ * rope_theta at the top level or in rope_parameters, head_dim null -> hidden_size / num_attention_heads, the
+ * downsample kernel from frame_rate).  MIMI_ERR_IO: unreadable file, malformed JSON or a field of the wrong type;
+ * MIMI_ERR_UNSUPPORTED: an architecture outside the kyutai/mimi family (stereo, non-causal convs, GQA, ...).
+ * Host-only: no device is touched.
+ */
+int mimi_config_from_json(const char* path, mimi_config* cfg);
+
+/*
+ * The one-call constructor: weights_dir is a checkpoint directory in the HF layout (config.json, optional, and
+ * *.safetensors -- the first in byte order, as the Python host's sorted glob picks it) or a lone .safetensors file
+ * (default config).  Reads the config, creates the engine on `device`, loads the safetensors file and finalizes:
+ * = mimi_config_from_json + mimi_create + mimi_load_safetensors + mimi_finalize, with the engine released again on
+ * any failure (*out stays NULL; mimi_last_error names the first failure).
+ */
+int mimi_create_from_dir(const char* weights_dir, int device, mimi_engine** out);
+
 /* Create an engine on HIP device `device` (cfg NULL = defaults).  Weights are supplied next. */
 int mimi_create(const mimi_config* cfg, int device, mimi_engine** out);
 
@@ -103,7 +123,8 @@ int mimi_encode(mimi_engine* e, const float* dev_audio, int32_t batch, int64_t l
  * codes) with the encode: mimi_encode_async enqueues the encode on `stream` and returns a ticket without
  * waiting; mimi_encode_wait(ticket) waits for it on the host and, in f16x3, applies the overflow check (and the
  * per-item fallback when a fixed activation scale overflowed) before returning.  dev_codes is valid once the
- * wait returns; dev_audio and dev_codes must stay allocated until then.  At most 16 encodes per engine may be
+ * wait returns; dev_audio and dev_codes must stay allocated, and dev_audio unmodified, until then (the wait may
+ * re-encode from dev_audio: a fixed f16x3 scale overflowed, or the persistent RVQ chain gave up).  At most 16 encodes per engine may be
  * in flight; each ticket is waited exactly once.  mimi_encode = mimi_encode_async + mimi_encode_wait.
  */
 int mimi_encode_async(mimi_engine* e, const float* dev_audio, int32_t batch, int64_t length, int32_t num_quantizers,
@@ -208,13 +229,15 @@ int64_t mimi_encoded_length_cfg(const mimi_config* cfg, int64_t length);
 /*
  * Host-ingest resampler (replaces the resampling inside librosa.load(path, sr=24000):
  * librispeech-mimi/utils.py:84-87, emilia-mimi/process_shard.py:479-482, yodas2-mimi/process_shard.py:389),
- * bit-exact with librosa's res_type='polyphase' = scipy.signal.resample_poly on float32 input.  nclips clips
+ * bit-exact with librosa's res_type='polyphase' = scipy.signal.resample_poly on float32 input, and the engine of
+ * the soxr_hq-spec mode (mimi_hip.ingest: a linear-phase Kaiser FIR designed to libsoxr's published HQ quality
+ * spec, same polyphase arithmetic; parity with libsoxr itself unpinned).  nclips clips
  * packed in dev_in at dev_in_off[i] (dev_in_len[i] samples) -> dev_out at dev_out_off[i] (dev_out_len[i]
  * samples, max_out = their maximum), all int64 arrays on the device.  dev_filter: the up-scaled Kaiser(5.0)
- * low-pass with its zero pre-padding (filter_len taps, <= MIMI_RESAMPLE_MAX_TAPS); pre_remove: leading
+ * low-pass with its zero pre-padding, or any other FIR (filter_len taps, <= MIMI_RESAMPLE_MAX_TAPS); pre_remove: leading
  * outputs of the full upfirdn skipped (resample_poly's n_pre_remove).  No engine handle needed.
  */
-#define MIMI_RESAMPLE_MAX_TAPS 8192
+#define MIMI_RESAMPLE_MAX_TAPS 65536
 int mimi_resample_poly(const float* dev_in, const int64_t* dev_in_off, const int64_t* dev_in_len, int32_t nclips,
                        float* dev_out, const int64_t* dev_out_off, const int64_t* dev_out_len, int64_t max_out,
                        const float* dev_filter, int32_t filter_len, int32_t up, int32_t down, int64_t pre_remove,

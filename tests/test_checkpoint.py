@@ -160,3 +160,169 @@ def test_malformed_checkpoints_fail_with_status(tmp_path):
     st, _ = _status(lib.mimi_load_safetensors, h, str(tmp_path / "does_not_exist.safetensors").encode())
     lib.mimi_destroy(h)
     assert st == 6
+
+
+# ---- the one-call C constructor: mimi_config_from_json + mimi_create_from_dir --------------------------------------
+
+def _c_config_from_json(path):
+    """C: config.json -> (status, struct as a dict, message)."""
+    from mimi_hip import _lib
+    lib = _lib.load()
+    c = _lib.MimiConfigC()
+    st = lib.mimi_config_from_json(str(path).encode(), ctypes.byref(c))
+    msg = lib.mimi_last_error().decode()
+    d = {name: (list(getattr(c, name)) if name == "upsampling_ratios" else getattr(c, name))
+         for name, _ in _lib.MimiConfigC._fields_}
+    return st, d, msg
+
+
+def _py_config_struct(path):
+    """The Python host's reading of the same file (MimiConfig.from_json + validate_supported + config_from_py)."""
+    from mimi_hip import _lib
+    cfg = MimiConfig.from_json(str(path))
+    cfg.validate_supported()
+    c = _lib.config_from_py(cfg)
+    return {name: (list(getattr(c, name)) if name == "upsampling_ratios" else getattr(c, name))
+            for name, _ in _lib.MimiConfigC._fields_}
+
+
+def _variant(tmp_path, name, edit):
+    import json
+    with open(os.path.join(GOLDEN, "mimi_config.json")) as f:
+        raw = json.load(f)
+    edit(raw)
+    p = tmp_path / f"{name}.json"
+    p.write_text(json.dumps(raw, indent=1))
+    return p
+
+
+def test_c_config_from_json_equals_python_host(tmp_path):
+    """CPU, C ABI only: the golden config.json (transformers 5.15.0 MimiConfig()) and variants of it read by
+    mimi_config_from_json give the struct the Python host builds from MimiConfig.from_json, field for field --
+    rope_theta at the top level, head_dim null, a frame_rate override (the downsample kernel follows it), other
+    ratios, and unknown keys; a directory path reads its config.json."""
+    st, got, msg = _c_config_from_json(os.path.join(GOLDEN, "mimi_config.json"))
+    assert st == 0, msg
+    assert got == _py_config_struct(os.path.join(GOLDEN, "mimi_config.json"))
+    assert got["downsample_kernel"] == 4 and got["head_dim"] == 64 and got["rope_theta"] == 10000.0
+    variants = {
+        "top_rope": lambda r: (r.pop("rope_parameters"), r.__setitem__("rope_theta", 5000.0)),
+        "head_dim_null": lambda r: r.__setitem__("head_dim", None),
+        "frame_rate_25": lambda r: r.__setitem__("frame_rate", 25.0),
+        "ratios": lambda r: r.__setitem__("upsampling_ratios", [8, 6, 5, 2]),
+        "ratios_null": lambda r: r.__setitem__("upsampling_ratios", None),
+        "unknown_keys": lambda r: r.update({"foo": {"bar": [1, 2, {"baz": "é\\n"}]}, "num_quantizers": 16}),
+        "eps": lambda r: r.__setitem__("norm_eps", 1e-6),
+    }
+    for name, edit in variants.items():
+        p = _variant(tmp_path, name, edit)
+        st, got, msg = _c_config_from_json(p)
+        assert st == 0, (name, msg)
+        assert got == _py_config_struct(p), name
+    assert _c_config_from_json(tmp_path / "frame_rate_25.json")[1]["downsample_kernel"] == 2
+    d = tmp_path / "ckpt"
+    d.mkdir()
+    (d / "config.json").write_text((tmp_path / "eps.json").read_text())
+    st, got, _ = _c_config_from_json(d)
+    assert st == 0 and abs(got["norm_eps"] - 1e-6) < 1e-12
+
+
+def test_c_config_from_json_rejects_what_python_rejects(tmp_path):
+    """Architectures outside the kyutai/mimi family -> MIMI_ERR_UNSUPPORTED (5) with the Python host's wording
+    (MimiConfig.validate_supported raises ValueError for the same files); malformed JSON, a field of the wrong type
+    or a missing file -> MIMI_ERR_IO (6)."""
+    unsupported = {
+        "stereo": (lambda r: r.__setitem__("audio_channels", 2), "audio_channels must be 1 (mono)"),
+        "gqa": (lambda r: r.__setitem__("num_key_value_heads", 4), "GQA"),
+        "noncausal": (lambda r: r.__setitem__("use_causal_conv", False), "use_causal_conv must be True"),
+        "reflect": (lambda r: r.__setitem__("pad_mode", "reflect"), "pad_mode must be 'constant'"),
+        "two_layers": (lambda r: r.__setitem__("num_residual_layers", 2), "num_residual_layers must be 1"),
+        "silu": (lambda r: r.__setitem__("hidden_act", "silu"), "hidden_act must be 'gelu'"),
+        "bias": (lambda r: r.__setitem__("attention_bias", True), "attention_bias must be False"),
+        "head_dim": (lambda r: r.__setitem__("head_dim", 32), "head_dim * num_attention_heads"),
+    }
+    for name, (edit, words) in unsupported.items():
+        p = _variant(tmp_path, name, edit)
+        st, _, msg = _c_config_from_json(p)
+        assert st == 5 and words in msg, (name, st, msg)
+        with pytest.raises(ValueError, match=words.replace("*", r"\*").replace("(", r"\(").replace(")", r"\)")):
+            _py_config_struct(p)
+    bad = {"truncated": '{"hidden_size": 512', "trailing": "{} x", "not_object": "[1, 2]",
+           "bad_number": '{"hidden_size": 5.1.2}', "string_int": '{"hidden_size": "512"}',
+           "float_int": '{"kernel_size": 7.5}', "bad_escape": '{"a": "\\q"}', "ctrl": '{"a": "x\ty"}',
+           "deep": "[" * 100 + "]" * 100, "empty": ""}
+    for name, text in bad.items():
+        p = tmp_path / f"bad_{name}.json"
+        p.write_text(text)
+        st, _, msg = _c_config_from_json(p)
+        assert st == 6 and msg, (name, st, msg)
+    st, _, msg = _c_config_from_json(tmp_path / "does_not_exist.json")
+    assert st == 6 and "does_not_exist" in msg
+
+
+def test_c_create_from_dir_checks_before_the_device(tmp_path):
+    """CPU: mimi_create_from_dir reads config.json and picks the checkpoint file before it touches a device -- an
+    unsupported config (5), a directory without .safetensors (6) and a missing path (6) fail the same on any host;
+    a well-formed directory gets as far as the device (here: none, so MIMI_ERR_HIP or MIMI_ERR_INVALID_ARGUMENT),
+    and *out stays NULL on every failure."""
+    from mimi_hip import _lib
+    if torch.cuda.is_available():
+        pytest.skip("CPU-only check (the GPU test below creates a real engine)")
+    lib = _lib.load()
+
+    def create(path):
+        h = ctypes.c_void_p(1234)
+        st = lib.mimi_create_from_dir(str(path).encode(), 0, ctypes.byref(h))
+        return st, h.value, lib.mimi_last_error().decode()
+
+    d = tmp_path / "stereo"
+    d.mkdir()
+    (d / "config.json").write_text(_variant(tmp_path, "s", lambda r: r.__setitem__("audio_channels", 2)).read_text())
+    (d / "model.safetensors").write_bytes(b"\0" * 16)
+    st, h, msg = create(d)
+    assert st == 5 and h is None and "audio_channels" in msg
+    e = tmp_path / "empty"
+    e.mkdir()
+    (e / "config.json").write_text(open(os.path.join(GOLDEN, "mimi_config.json")).read())
+    (e / ".hidden.safetensors").write_bytes(b"\0" * 16)  # (glob skips dot files)
+    st, h, msg = create(e)
+    assert st == 6 and h is None and "no .safetensors" in msg
+    st, h, msg = create(tmp_path / "missing")
+    assert st == 6 and h is None
+    sd = synthetic.make_state_dict(seed=0, num_quantizers=2)
+    ok = tmp_path / "ok"
+    write_hf_checkpoint(sd, str(ok))
+    st, h, msg = create(ok)
+    assert st in (1, 2) and h is None, (st, msg)
+
+
+@pytest.mark.gpu
+def test_c_create_from_dir_matches_from_pretrained(tmp_path, state_dict):
+    """GPU, C ABI only: an engine from mimi_create_from_dir on an HF-layout directory (config.json + model.safetensors
+    with decoder tensors beside the encode path) encodes the codes of MimiHipModel.from_pretrained on the same
+    directory, bit for bit (mimi_encode on the caller's device buffers, K = 8 and 32); a lone .safetensors file
+    works too (default config)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from mimi_hip import _lib
+    from mimi_hip.model import MimiHipModel
+    lib = _lib.load()
+    d = tmp_path / "ckpt"
+    st_path = write_hf_checkpoint(state_dict, str(d))
+    ref = MimiHipModel.from_pretrained(str(d), device="cuda:0")
+    x = torch.from_numpy(synthetic.clip_batch(3, 72000, seed=11)).cuda()
+    for path in (d, st_path):
+        h = ctypes.c_void_p()
+        _lib.check(lib.mimi_create_from_dir(str(path).encode(), 0, ctypes.byref(h)))
+        try:
+            for K in (8, 32):
+                T = lib.mimi_encoded_length(72000)
+                out = torch.empty(3, K, T, dtype=torch.int32, device="cuda:0")
+                torch.cuda.synchronize()
+                _lib.check(lib.mimi_encode(h, ctypes.c_void_p(x.data_ptr()), 3, 72000, K,
+                                           ctypes.c_void_p(out.data_ptr()), None))
+                torch.cuda.synchronize()
+                want = ref.encode_int32(x, K)
+                assert torch.equal(out, want.view_as(out)), (str(path), K)
+        finally:
+            lib.mimi_destroy(h)

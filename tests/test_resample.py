@@ -162,3 +162,93 @@ def test_resample_kernel_window_variants_vs_scipy():
             m = int(math.ceil(len(x) * (24000.0 / orig)))
             want = want[:m] if len(want) >= m else np.concatenate([want, np.zeros(m - len(want), np.float32)])
             assert bits_equal(o.cpu().numpy(), want), (orig, len(x))
+
+
+# ---- soxr_hq-spec mode (librosa's default res_type; libsoxr's published HQ spec, parity with libsoxr unpinned) ----
+
+SOXR_PAIRS = [16000, 8000, 48000, 32000, 44100, 22050]
+
+
+def _upfirdn_ref(x, up, down, hp, pre, n_out):
+    """scipy.signal.upfirdn over the padded filter, trimmed as resample_poly trims: the arithmetic the kernel runs."""
+    from scipy.signal import upfirdn
+    y = upfirdn(hp, np.asarray(x, np.float32), up, down)
+    out = np.zeros(n_out, np.float32)
+    seg = y[pre:pre + n_out]
+    out[:len(seg)] = seg
+    return out
+
+
+@pytest.mark.parametrize("rate", SOXR_PAIRS)
+def test_soxr_hq_filter_meets_spec(rate):
+    """The filter of every source rate -> 24 kHz, as the kernel receives it (float32 taps, /up): linear phase
+    (symmetric), passband ripple < 0.01 dB up to 0.913 of the lower Nyquist, >= 120.4 dB (20 bits) rejection from the
+    lower Nyquist to the up-sampled Nyquist."""
+    up, down, hp, pre = ingest.soxr_hq_plan(rate, 24000)
+    h = hp[np.flatnonzero(hp)[0]:].astype(np.float64) / up  # (pre-padding zeros off)
+    assert len(h) % 2 == 1 and np.array_equal(h, h[::-1])
+    fs_up = rate * up
+    nyq = min(rate, 24000) / 2
+    nfft = 1 << 21  # (a bin of fs_up / 2^21: <= 1.7 Hz at the largest up-sampled rate)
+    H = np.fft.rfft(h, nfft)
+    w = np.arange(len(H)) * fs_up / nfft
+    mag = 20 * np.log10(np.abs(H) + 1e-300)
+    spec = ingest.SOXR_HQ_SPEC
+    passband = mag[w <= spec["passband_end"] * nyq]
+    stopband = mag[w >= spec["stopband_begin"] * nyq]
+    assert np.abs(passband).max() < 0.01, np.abs(passband).max()
+    assert stopband.max() <= -spec["precision_bits"] * 20 * math.log10(2), stopband.max()
+
+
+def test_soxr_hq_tones():
+    """Tones through the soxr_hq-spec resampler (the kernel's arithmetic, restated by scipy.signal.upfirdn):
+    a passband tone keeps its amplitude within 0.01 dB and its phase (zero delay: the output is the tone sampled at
+    the new rate to -100 dB), a tone in the stopband of a down-conversion leaves <= -120 dB (20 bits)."""
+    def tone(f, rate, n):
+        return np.sin(2 * np.pi * f * np.arange(n) / rate).astype(np.float32)
+
+    def resample(x, rate):
+        up, down, hp, pre = ingest.soxr_hq_plan(rate, 24000)
+        return _upfirdn_ref(x, up, down, hp, pre, int(math.ceil(len(x) * 24000 / rate)))
+
+    for rate, f in ((16000, 1000.0), (16000, 7290.0), (48000, 10950.0), (44100, 3000.0)):
+        n = rate * 2
+        y = resample(tone(f, rate, n), rate)
+        ideal = np.sin(2 * np.pi * f * np.arange(len(y)) / 24000)
+        mid = slice(len(y) // 4, 3 * len(y) // 4)  # away from the clip edges (implicit zeros outside)
+        gain = np.sqrt(np.mean(y[mid].astype(np.float64) ** 2) / np.mean(ideal[mid] ** 2))
+        assert abs(20 * np.log10(gain)) < 0.01, (rate, f, gain)
+        err = np.sqrt(np.mean((y[mid] - ideal[mid]) ** 2) / np.mean(ideal[mid] ** 2))
+        assert err < 1e-5, (rate, f, err)  # (float32 arithmetic: ~-120 dB; the filter's own error is below)
+    for rate, f in ((48000, 12500.0), (48000, 20000.0), (44100, 13000.0)):
+        n = rate
+        y = resample(tone(f, rate, n), rate)
+        mid = slice(len(y) // 4, 3 * len(y) // 4)
+        leak = np.sqrt(np.mean(y[mid].astype(np.float64) ** 2) / 0.5)
+        assert 20 * np.log10(leak + 1e-30) <= -120.0, (rate, f, leak)
+
+
+def test_soxr_hq_mode_switch_and_errors():
+    assert ingest.RES_TYPES == ("polyphase", "soxr_hq")
+    with pytest.raises(ValueError, match="res_type"):
+        ingest.resample([np.zeros(10, np.float32)], 16000, 24000, device="cuda:0", res_type="kaiser_best")
+    up, down, hp, pre = ingest.soxr_hq_plan(16000, 24000)
+    assert (up, down) == (3, 2) and hp.dtype == np.float32 and pre > 0
+    p_up, p_down, p_hp, _ = ingest.resample_plan(16000, 24000)
+    assert (p_up, p_down) == (up, down) and len(hp) > len(p_hp)  # (the HQ spec's narrow transition band)
+
+
+@pytest.mark.gpu
+def test_soxr_hq_kernel_bit_exact_vs_upfirdn():
+    """GPU: the soxr_hq-spec mode through the kernel equals scipy.signal.upfirdn over the same filter bit for bit,
+    ragged clips in one launch, for an LDS-resident filter (16 / 48 kHz) and the long filters read from global
+    memory (44.1 / 22.05 kHz: ~28-30k taps)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    for rate in (16000, 48000, 44100, 22050):
+        clips = [_clip(rate, n) for n in (1, 37, 1001, 3 * rate + 17)]
+        outs = ingest.resample(clips, rate, 24000, device="cuda:0", res_type="soxr_hq")
+        up, down, hp, pre = ingest.soxr_hq_plan(rate, 24000)
+        for c, o in zip(clips, outs):
+            want = _upfirdn_ref(c, up, down, hp, pre, int(math.ceil(len(c) * 24000 / rate)))
+            assert bits_equal(o.cpu().numpy(), want), (rate, len(c))

@@ -97,3 +97,15 @@ def test_safetensors_reader_under_sanitizers(harness, tmp_path):
         assert st == w[0], (f, st)
         if w[1] is not None:
             assert sm == w[1], f
+
+
+def test_config_json_reader_under_sanitizers(harness, tmp_path):
+    """config.json (csrc/config_json.cpp) and 1500 mutations of it: a status every time, never an invalid access; the
+    golden file reads as MIMI_OK."""
+    golden = os.path.join(ROOT, "tests", "golden", "mimi_config.json")
+    p = tmp_path / "config.json"
+    p.write_bytes(open(golden, "rb").read())
+    q = tmp_path / "nested.json"
+    q.write_text('{"a": [[[{"b": "\\u00e9\\ud83d\\ude00"}]]], "upsampling_ratios": [8, 6, 5, 4], "frame_rate": 12.5}')
+    got = run(harness, [p, q], 1500)
+    assert got[str(p)][0] == 0 and got[str(q)][0] == 0

@@ -5,6 +5,8 @@ uses; the merged result must equal a single-process run over the same per-rank b
 import os
 import socket
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 import numpy as np
 import pytest
 import torch.multiprocessing as mp
@@ -143,3 +145,22 @@ def test_sharded_real_engines_match_single(tmp_path):
         for i in range(len(audio)):
             assert_codes_in_range(z[f"c{i}"])
             assert np.array_equal(z[f"c{i}"], exp[i]), i
+
+
+def test_bench_rank_map_rejects_shared_gpus_under_nccl():
+    """bench.py's N-GPU line carries each rank's device (host, PCI bus): under nccl two ranks on one device abort the
+    run, under the gloo rehearsal they are labelled `sharing`; a process group of another size aborts too."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    r = lambda i, bus: {"rank": i, "host": "h", "pci_bus": bus}  # noqa: E731
+    ok = bench.check_rank_places([r(i, f"0000:{0x10 * (i + 1):02x}:00") for i in range(8)], "nccl", 8, 8)
+    assert ok == {"backend": "nccl", "world_size": 8, "distinct_devices": 8, "sharing": False}
+    shared = [r(0, "0000:75:00"), r(1, "0000:75:00")]
+    assert bench.check_rank_places(shared, "gloo", 2, 2)["sharing"] is True
+    with pytest.raises(SystemExit, match="share a GPU"):
+        bench.check_rank_places(shared, "nccl", 2, 2)
+    with pytest.raises(SystemExit, match="process group"):
+        bench.check_rank_places(shared[:1], "nccl", 1, 2)
+    assert bench.check_rank_places([r(0, "0000:75:00")], "none", 1, 1)["distinct_devices"] == 1

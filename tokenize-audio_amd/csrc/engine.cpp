@@ -75,37 +75,7 @@ int mimi::set_error_message(int code, const char* msg) {
 // ------------------------------------------------------------------------------------------------
 // config / length math
 // ------------------------------------------------------------------------------------------------
-extern "C" void mimi_config_default(mimi_config* c) {
-    std::memset(c, 0, sizeof(*c));
-    c->sampling_rate = 24000;
-    c->audio_channels = 1;
-    c->hidden_size = 512;
-    c->num_filters = 64;
-    c->num_ratios = 4;
-    c->upsampling_ratios[0] = 8;
-    c->upsampling_ratios[1] = 6;
-    c->upsampling_ratios[2] = 5;
-    c->upsampling_ratios[3] = 4;
-    c->kernel_size = 7;
-    c->last_kernel_size = 3;
-    c->residual_kernel_size = 3;
-    c->compress = 2;
-    c->codebook_size = 2048;
-    c->codebook_dim = 256;
-    c->num_quantizers = 32;
-    c->num_semantic_quantizers = 1;
-    c->vq_hidden_dim = 256;
-    c->num_hidden_layers = 8;
-    c->intermediate_size = 2048;
-    c->num_attention_heads = 8;
-    c->head_dim = 64;
-    c->sliding_window = 250;
-    c->downsample_kernel = 4;
-    c->downsample_stride = 2;
-    c->norm_eps = 1e-5f;
-    c->rope_theta = 10000.0f;
-    c->codebook_eps = 1e-5f;
-}
+// mimi_config_default and mimi_config_from_json: config_json.cpp (host-only)
 
 // MimiConv1d output length, reproducing the reference's float32 tensor arithmetic
 // (TF/modeling_mimi.py:269-279): n_frames = ceil(float32(L - s) / float32(s) + 1) - 1; out = n_frames + 1.
@@ -582,6 +552,32 @@ extern "C" int mimi_create(const mimi_config* cfg, int device, mimi_engine** out
     HIP_TRY(hipHostMalloc(&e->amax_host, kMaxActSlots * sizeof(unsigned), hipHostMallocDefault));
     build_expected(e.get());
     *out = e.release();
+    return MIMI_OK;
+}
+
+// The one-call constructor: a checkpoint directory in the HF layout (config.json + *.safetensors,
+// what MimiModel.from_pretrained("kyutai/mimi") reads: emilia-mimi/process_shard.py:57-60) or a lone .safetensors
+// file (default config) -> a finalized engine.  config_json.cpp parses the config and picks the file; on any failure
+// the half-built engine is released and the first error is the one mimi_last_error reports.
+extern "C" int mimi_create_from_dir(const char* weights_dir, int device, mimi_engine** out) {
+    if (!out) return set_err(MIMI_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    if (!weights_dir) return set_err(MIMI_ERR_INVALID_ARGUMENT, "weights_dir is NULL");
+    std::string cfg_path, st_path;
+    int rc = mimi::find_checkpoint(weights_dir, cfg_path, st_path);
+    if (rc) return rc;
+    mimi_config cfg;
+    mimi_config_default(&cfg);
+    if (!cfg_path.empty() && (rc = mimi_config_from_json(cfg_path.c_str(), &cfg))) return rc;
+    mimi_engine* e = nullptr;
+    if ((rc = mimi_create(&cfg, device, &e))) return rc;
+    if ((rc = mimi_load_safetensors(e, st_path.c_str())) || (rc = mimi_finalize(e))) {
+        const std::string msg = g_last_error;
+        mimi_destroy(e);
+        g_last_error = msg;
+        return rc;
+    }
+    *out = e;
     return MIMI_OK;
 }
 
@@ -2095,6 +2091,9 @@ static int encode_async_locked(mimi_engine* e, const float* audio, int B, int64_
     if (!P->done) HIP_TRY(hipEventCreateWithFlags(&P->done, hipEventDisableTiming));
     if (!P->amax) HIP_TRY(hipHostMalloc(&P->amax, kMaxActSlots * sizeof(unsigned), hipHostMallocDefault));
     if (!P->chain_word) HIP_TRY(hipHostMalloc(&P->chain_word, 16, hipHostMallocDefault));
+    // the slot's last ticket was waited, so nothing in flight writes this word: clear it here rather than trust that
+    // a kernel of this encode writes it (amax_reduce skips its launch when there is nothing to reduce)
+    P->chain_word[0] = 0u;
     P->chain = false;
     const int prec = e->precision;
     const bool h16 = prec == PREC_F16X3 && act_planes(e, plan_lengths(e->cfg, L), prec) == 2;
@@ -2377,10 +2376,10 @@ extern "C" int mimi_encode_host(mimi_engine* e, const float* host_audio, int32_t
     const size_t cb = (size_t)batch * K * (size_t)mimi_encoded_length_cfg(&e->cfg, length) * sizeof(int32_t);
     mimi_engine::HostIo* io = nullptr;
     int64_t ticket = 0, reruns = 0;
-    {
+    {  // claim a staging slot and size it under the engine lock (a re-allocation's hipFree must not land inside
+       // another thread's graph capture on this engine) ...
         std::lock_guard<std::mutex> lk(e->mu);
         HIP_TRY(hipSetDevice(e->device));
-        (void)hipGetLastError();
         for (auto& h : e->hostio)
             if (!h.busy) {
                 io = &h;
@@ -2389,15 +2388,28 @@ extern "C" int mimi_encode_host(mimi_engine* e, const float* host_audio, int32_t
         if (!io)
             return set_err(MIMI_ERR_STATE, "%d host encodes in flight", mimi_engine::kMaxPending);
         if ((rc = host_io_grow(io, ab, cb))) return rc;
-        std::memcpy(io->h_audio, host_audio, ab);  // (the slot's previous H2D finished before its last call returned)
+        io->busy = true;  // (from here on every exit path releases it)
+    }
+    // ... then copy the caller's samples into its pinned buffer without the lock: other threads' encodes on this
+    // engine are not held up behind a host memcpy of up to several MB (the slot's previous H2D finished before its
+    // last call returned)
+    if (const hipError_t de = hipSetDevice(e->device); de != hipSuccess) {
+        std::lock_guard<std::mutex> lk(e->mu);
+        io->busy = false;
+        return set_err(MIMI_ERR_HIP, "mimi_encode_host: hipSetDevice: %s", hipGetErrorString(de));
+    }
+    std::memcpy(io->h_audio, host_audio, ab);
+    {
+        std::lock_guard<std::mutex> lk(e->mu);
+        (void)hipGetLastError();
         const hipError_t ce = hipMemcpyAsync(io->d_audio, io->h_audio, ab, hipMemcpyHostToDevice, s);
         if (ce != hipSuccess) rc = set_err(MIMI_ERR_HIP, "mimi_encode_host: H2D copy: %s", hipGetErrorString(ce));
         if (!rc) rc = encode_async_locked(e, io->d_audio, batch, length, K, io->d_codes, s, &ticket);
         if (rc) {
-            (void)hipStreamSynchronize(s);  // (the slot stays free: nothing of this call is left in flight)
+            (void)hipStreamSynchronize(s);  // (the slot is released: nothing of this call is left in flight)
+            io->busy = false;
             return rc;
         }
-        io->busy = true;  // (from here on every exit path releases it)
         reruns = e->chain_reruns + e->f16_reruns;
         hipError_t de = hipMemcpyAsync(io->h_codes, io->d_codes, cb, hipMemcpyDeviceToHost, s);
         if (de == hipSuccess) de = hipEventRecord(io->done, s);

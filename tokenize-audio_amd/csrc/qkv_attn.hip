@@ -121,7 +121,8 @@ __global__ __launch_bounds__(1024) void qkv_attention_h16_kernel(QkvAttnArgs p, 
     bf16x8 a[PA + 1][2];
     // W(0) .. W(S - KG - 1) and A(0) .. A(PA - 1) ahead; per K step kt: A(kt + PA); per group of KG steps the W refills
     // (below).  The compiler keeps the DMA issues in order against the waits but places the A register loads freely
-    // (and inserts their waits itself), so the ring waits count DMA pieces only (ring_wait.h rows_dma_after)
+    // (and inserts their waits itself), so the ring waits count DMA pieces only (dma_after_group below, ring_wait.h
+    // vm_wait)
 #pragma unroll
     for (int k = 0; k < S - KG; ++k)
         if (k < KT) issueB(k);

@@ -41,7 +41,9 @@ __device__ __forceinline__ long long pass_w0(long long m0, long long pre_remove,
 // UPC > 0: the up-sampling factor as a compile-time constant (1: 48/72/96 -> 24 kHz, 3: 8/16 -> 24 kHz), so the
 // unrolled tap loop's LDS addresses are immediate offsets from two bases (2 ds_read + mul + add per tap); 0:
 // any factor, read at run time
-template <int WPT, int UPC>
+// HG: the filter stays in global memory (L2 / L1-cached reads) instead of LDS -- the long linear-phase filters of the
+// soxr_hq-spec mode for 44.1 / 22.05 kHz sources (~28-30k taps, ~350 per output phase) do not fit beside the window
+template <int WPT, int UPC, bool HG = false>
 __global__ __launch_bounds__(RS_BLOCK) void resample_poly_kernel(const float* __restrict__ x,
                                                                  const long long* __restrict__ in_off,
                                                                  const long long* __restrict__ in_len,
@@ -53,10 +55,11 @@ __global__ __launch_bounds__(RS_BLOCK) void resample_poly_kernel(const float* __
     const int up = UPC > 0 ? UPC : up_rt;
     extern __shared__ float lds[];
     const int W = (int)resample_window(lh, up, down);
-    float* hs = lds;           // the filter, lh taps
-    float* xsb = lds + lh;     // input window(s): [2][W] (WPT > 0) or [W]
+    const float* hs = HG ? h : lds;  // the filter, lh taps
+    float* xsb = lds + (HG ? 0 : lh);   // input window(s): [2][W] (WPT > 0) or [W]
     const int tid = threadIdx.x;
-    for (int i = tid; i < lh; i += RS_BLOCK) hs[i] = h[i];
+    if (!HG)
+        for (int i = tid; i < lh; i += RS_BLOCK) lds[i] = h[i];
     const int c = blockIdx.y;
     const long long n_in = in_len[c], n_out = out_len[c];
     const float* __restrict__ xc = x + in_off[c];
@@ -256,17 +259,23 @@ hipError_t launch_resample_poly(const float* x, const long long* in_off, const l
     }
     const long long W = resample_window(lh, up, down);
     const int wpt = W <= RS_BLOCK ? 1 : W <= 2 * RS_BLOCK ? 2 : W <= 4 * RS_BLOCK ? 4 : 0;
-    const long long lds_bytes = (lh + (wpt > 0 ? 2 : 1) * W) * 4;
-    if (lds_bytes > 64 * 1024) return hipErrorInvalidValue;  // default dynamic-LDS limit
+    long long lds_bytes = (lh + (wpt > 0 ? 2 : 1) * W) * 4;
+    const bool hg = lds_bytes > 64 * 1024;  // default dynamic-LDS limit: the filter is read from global memory
+    if (hg) lds_bytes -= (long long)lh * 4;
+    if (lds_bytes > 64 * 1024) return hipErrorInvalidValue;
     // ~4096 workgroups in all (16 per CU), each sweeping many 256-output passes of one clip: a workgroup per
     // pass would spend more time being dispatched and loading the filter than resampling
     long long bx = (max_out + RS_BLOCK - 1) / RS_BLOCK;
     const long long cap = (4096 + nclips - 1) / nclips;
     if (bx > cap) bx = cap;
     const dim3 grid((unsigned)bx, (unsigned)nclips);
-#define RS_LAUNCH(N, U)                                                                                      \
-    hipLaunchKernelGGL((resample_poly_kernel<N, U>), grid, dim3(RS_BLOCK), (size_t)lds_bytes, s, x, in_off, in_len, \
-                       y, out_off, out_len, h, lh, up, down, pre_remove)
+#define RS_LAUNCH(N, U)                                                                                          \
+    if (hg)                                                                                                      \
+        hipLaunchKernelGGL((resample_poly_kernel<N, 0, true>), grid, dim3(RS_BLOCK), (size_t)lds_bytes, s, x,   \
+                           in_off, in_len, y, out_off, out_len, h, lh, up, down, pre_remove);                    \
+    else                                                                                                         \
+        hipLaunchKernelGGL((resample_poly_kernel<N, U>), grid, dim3(RS_BLOCK), (size_t)lds_bytes, s, x, in_off,  \
+                           in_len, y, out_off, out_len, h, lh, up, down, pre_remove)
 #define RS_LAUNCH_W(U)              \
     switch (wpt) {                  \
         case 1: RS_LAUNCH(1, U); break; \

@@ -23,14 +23,14 @@ STATUS_NAMES = {
 
 # every symbol include/mimi_hip.h declares (tests check the library exports exactly these)
 EXPORTED_SYMBOLS = (
-    "mimi_config_default", "mimi_create", "mimi_set_weight", "mimi_load_safetensors", "mimi_finalize",
+    "mimi_config_default", "mimi_config_from_json", "mimi_create_from_dir", "mimi_create", "mimi_set_weight", "mimi_load_safetensors", "mimi_finalize",
     "mimi_encode", "mimi_encode_async", "mimi_encode_wait", "mimi_encode_host", "mimi_encode_ragged", "mimi_encode_ragged_async", "mimi_rvq_encode", "mimi_set_precision", "mimi_get_precision", "mimi_calibrate", "mimi_f16_reruns", "mimi_rvq_chain_reruns", "mimi_set_graphs", "mimi_graph_replays", "mimi_set_option", "mimi_act_scales", "mimi_encoded_length",
     "mimi_encoded_length_cfg",
     "mimi_workspace_bytes", "mimi_destroy", "mimi_last_error", "mimi_set_profiling", "mimi_profile_read",
     "mimi_profile_reset", "mimi_profile_sequence", "mimi_set_taps", "mimi_get_tap", "mimi_resample_poly",
     "mimi_bpe_create", "mimi_bpe_best", "mimi_bpe_merge", "mimi_bpe_destroy", "mimi_flac_info", "mimi_flac_decode",
 )
-RESAMPLE_MAX_TAPS = 8192  # MIMI_RESAMPLE_MAX_TAPS
+RESAMPLE_MAX_TAPS = 65536  # MIMI_RESAMPLE_MAX_TAPS
 
 
 class MimiConfigC(ctypes.Structure):
@@ -76,6 +76,8 @@ def _declare(lib):
     vp = c.c_void_p
     sig = {
         "mimi_config_default": (None, [c.POINTER(MimiConfigC)]),
+        "mimi_config_from_json": (c.c_int, [c.c_char_p, c.POINTER(MimiConfigC)]),
+        "mimi_create_from_dir": (c.c_int, [c.c_char_p, c.c_int, c.POINTER(vp)]),
         "mimi_create": (c.c_int, [c.POINTER(MimiConfigC), c.c_int, c.POINTER(vp)]),
         "mimi_set_weight": (c.c_int, [vp, c.c_char_p, vp, c.c_int64]),
         "mimi_load_safetensors": (c.c_int, [vp, c.c_char_p]),

@@ -13,9 +13,13 @@ Replaces ``librosa.load(path, sr=24000)`` on the shard scripts' load path (``lib
   decoded by the library's spec-written decoder (``mimi_flac_decode``, csrc/flac.cpp), then the same float
   conversion and channel mean.
 
-Parity limits: librosa is not installed, so its DEFAULT mode (``soxr_hq``, libsoxr) is
-unpinned -- a script that wants bit-identical inputs to an existing soxr-resampled shard must keep librosa;
-what is pinned is the polyphase mode, against scipy itself.  FLAC is lossless, so a correct decoder returns
+* ``resample(..., res_type="soxr_hq")``: librosa's DEFAULT mode as libsoxr publishes its HQ spec (20-bit
+  rejection, passband to 0.913 of Nyquist, linear phase): one long Kaiser FIR (``soxr_hq_plan``) on the same kernel.
+
+Parity limits: librosa and libsoxr are not installed, so parity with librosa's default mode is
+unpinned -- the soxr_hq-spec mode meets the published spec (tested on its response and on tones) but is not
+libsoxr's algorithm, so a script that wants bit-identical inputs to an existing soxr-resampled shard must keep
+librosa; what is pinned is the polyphase mode, against scipy itself.  FLAC is lossless, so a correct decoder returns
 exactly the encoded PCM; libFLAC is absent here, so the decoder is checked by round trips through a test-side
 encoder written from the format specification (tests/flac_writer.py), not against libFLAC itself.  mp3 / opus
 (Emilia's tar members) need decoders this image lacks and are out of scope.
@@ -31,7 +35,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["resample_plan", "resample", "resample_packed", "load_wav", "load_flac", "decode_flac", "load"]
+__all__ = ["resample_plan", "soxr_hq_plan", "SOXR_HQ_SPEC", "resample", "resample_packed", "load_wav", "load_flac",
+           "decode_flac", "load"]
 
 
 def resample_plan(orig_sr: int, target_sr: int) -> Tuple[int, int, np.ndarray, int]:
@@ -54,6 +59,50 @@ def resample_plan(orig_sr: int, target_sr: int) -> Tuple[int, int, np.ndarray, i
     return up, down, hp, (half_len + n_pre_pad) // down
 
 
+# libsoxr's published quality spec for its HQ recipe -- the one librosa.resample's default res_type='soxr_hq' asks
+# for (librosa 0.10 core/audio.py; soxr.h soxr_quality_spec field defaults: precision 20 bits, phase_response 50 =
+# linear, passband_end 0.913, stopband_begin 1, both relative to the Nyquist frequency of the lower of the two rates)
+SOXR_HQ_SPEC = {"precision_bits": 20, "passband_end": 0.913, "stopband_begin": 1.0, "phase": "linear"}
+SOXR_HQ_DESIGN_ATTEN_DB = 126.0  # Kaiser design target: >= 20 x 20 log10(2) = 120.4 dB measured on every pair tested
+
+
+def soxr_hq_plan(orig_sr: int, target_sr: int) -> Tuple[int, int, np.ndarray, int]:
+    """(up, down, filter with its zero pre-padding, n_pre_remove) of the ``soxr_hq``-spec mode: ONE linear-phase
+    Kaiser low-pass at the up-sampled rate meeting ``SOXR_HQ_SPEC`` -- passband to 0.913 of the lower Nyquist
+    with < 0.01 dB ripple, stopband from the lower Nyquist at >= 120.4 dB (20 bits) -- run by the same polyphase
+    kernel, zero-delay aligned (the filter's centre on the output grid, as resample_poly aligns its own).
+
+    This restates the spec libsoxr publishes, not its algorithm (a multi-stage DFT-domain design): libsoxr and
+    librosa are absent from this image, so parity with librosa's ``soxr_hq`` output is UNPINNED; what is tested is
+    the spec itself (tests/test_resample.py: the filter's response, tones through it) and the kernel's arithmetic
+    (bit-exact with ``scipy.signal.upfirdn`` over the same filter)."""
+    from scipy.signal import firwin
+    if int(orig_sr) != orig_sr or int(target_sr) != target_sr or orig_sr <= 0 or target_sr <= 0:
+        raise ValueError("resampling requires positive integer sample rates")
+    g = math.gcd(int(orig_sr), int(target_sr))
+    up, down = int(target_sr) // g, int(orig_sr) // g
+    fs_up = float(orig_sr) * up
+    nyq = min(orig_sr, target_sr) / 2.0
+    f_pass, f_stop = SOXR_HQ_SPEC["passband_end"] * nyq, SOXR_HQ_SPEC["stopband_begin"] * nyq
+    a = SOXR_HQ_DESIGN_ATTEN_DB
+    # Kaiser's length and shape formulas (Oppenheim & Schafer 7.6): N - 1 = (A - 7.95) / (2.285 dw), beta(A)
+    n = int(math.ceil((a - 7.95) / (2.285 * 2.0 * math.pi * (f_stop - f_pass) / fs_up))) + 1
+    n += 1 - n % 2  # odd: a type-I filter, integer group delay
+    beta = 0.1102 * (a - 8.7)
+    h = firwin(n, (f_pass + f_stop) / 2.0, window=("kaiser", beta), fs=fs_up).astype(np.float32)
+    h *= up
+    half_len = (n - 1) // 2
+    n_pre_pad = down - half_len % down
+    hp = np.concatenate([np.zeros(n_pre_pad, np.float32), h])
+    if len(hp) > _lib.RESAMPLE_MAX_TAPS:
+        raise ValueError(f"resampling {orig_sr} -> {target_sr} Hz in soxr_hq mode needs a {len(hp)}-tap filter "
+                         f"(the kernel takes at most {_lib.RESAMPLE_MAX_TAPS})")
+    return up, down, hp, (half_len + n_pre_pad) // down
+
+
+RES_TYPES = ("polyphase", "soxr_hq")
+
+
 def _device(device) -> torch.device:
     d = torch.device(device)
     if d.type != "cuda":
@@ -61,21 +110,26 @@ def _device(device) -> torch.device:
     return d
 
 
-_FILTERS = {}  # (orig_sr, target_sr, device) -> (up, down, device filter, taps, n_pre_remove)
+_FILTERS = {}  # (orig_sr, target_sr, device, res_type) -> (up, down, device filter, taps, n_pre_remove)
 
 
-def _plan_on(orig_sr: int, target_sr: int, dev: torch.device):
-    key = (int(orig_sr), int(target_sr), str(dev))
+def _plan_on(orig_sr: int, target_sr: int, dev: torch.device, res_type: str = "polyphase"):
+    if res_type not in RES_TYPES:
+        raise ValueError(f"res_type {res_type!r}: expected one of {RES_TYPES}")
+    key = (int(orig_sr), int(target_sr), str(dev), res_type)
     if key not in _FILTERS:
-        up, down, hp, pre = resample_plan(orig_sr, target_sr)
+        plan = resample_plan if res_type == "polyphase" else soxr_hq_plan
+        up, down, hp, pre = plan(orig_sr, target_sr)
         _FILTERS[key] = (up, down, torch.from_numpy(hp).to(dev), len(hp), pre)
     return _FILTERS[key]
 
 
-def resample_packed(x: torch.Tensor, lengths: Sequence[int], orig_sr: int, target_sr: int = 24000
-                    ) -> Tuple[torch.Tensor, List[int]]:
+def resample_packed(x: torch.Tensor, lengths: Sequence[int], orig_sr: int, target_sr: int = 24000,
+                    res_type: str = "polyphase") -> Tuple[torch.Tensor, List[int]]:
     """The kernel call: ``x`` is a device float32 buffer holding the clips back to back (``lengths``).
-    Returns (packed output, output lengths = ``ceil(len * target_sr / orig_sr)``, librosa's fix_length)."""
+    Returns (packed output, output lengths = ``ceil(len * target_sr / orig_sr)``, librosa's fix_length).
+    ``res_type``: ``"polyphase"`` (bit-exact with scipy's resample_poly) or ``"soxr_hq"`` (the soxr HQ spec,
+    ``soxr_hq_plan``)."""
     dev = _device(x.device)
     if x.dtype != torch.float32 or not x.is_contiguous():
         raise ValueError("x must be a contiguous float32 device tensor")
@@ -86,7 +140,7 @@ def resample_packed(x: torch.Tensor, lengths: Sequence[int], orig_sr: int, targe
     n_fix = [int(math.ceil(n * ratio)) for n in n_in]                  # librosa fix_length target
     if orig_sr == target_sr:
         return x[:sum(n_in)].clone(), n_fix
-    up, down, filt, taps, pre_remove = _plan_on(orig_sr, target_sr, dev)
+    up, down, filt, taps, pre_remove = _plan_on(orig_sr, target_sr, dev, res_type)
     n_poly = [-(-n * up // down) for n in n_in]                         # resample_poly's own length
     n_run = [min(a, b) for a, b in zip(n_fix, n_poly)]                  # longer fix_length: zero tail
     in_off = np.concatenate([[0], np.cumsum(n_in)[:-1]]).astype(np.int64) if n_in else np.zeros(0, np.int64)
@@ -108,17 +162,20 @@ def resample_packed(x: torch.Tensor, lengths: Sequence[int], orig_sr: int, targe
 
 
 def resample(clips: Sequence[Union[np.ndarray, torch.Tensor]], orig_sr: int, target_sr: int = 24000,
-             device: Union[str, torch.device] = "cuda") -> List[torch.Tensor]:
+             device: Union[str, torch.device] = "cuda", res_type: str = "polyphase") -> List[torch.Tensor]:
     """Resample ragged mono clips (numpy or torch, any float dtype -> float32) in one launch.  Returns device
     float32 tensors of ``ceil(len * target_sr / orig_sr)`` samples (librosa's length), views into one
-    packed buffer."""
+    packed buffer.  ``res_type`` as librosa.resample names it: ``"polyphase"`` (pinned: bit-exact with scipy) or
+    ``"soxr_hq"`` (librosa's default; here its published spec, parity with libsoxr unpinned)."""
+    if res_type not in RES_TYPES:
+        raise ValueError(f"res_type {res_type!r}: expected one of {RES_TYPES}")
     dev = _device(device)
     xs = [torch.as_tensor(np.asarray(c, dtype=np.float32) if isinstance(c, np.ndarray) else c)
           .to(device=dev, dtype=torch.float32).reshape(-1) for c in clips]
     if not xs:
         return []
     xin = torch.cat(xs) if len(xs) > 1 else xs[0].contiguous()
-    out, n_fix = resample_packed(xin, [x.numel() for x in xs], orig_sr, target_sr)
+    out, n_fix = resample_packed(xin, [x.numel() for x in xs], orig_sr, target_sr, res_type)
     offs = np.concatenate([[0], np.cumsum(n_fix)[:-1]]).tolist()
     return [out[o:o + n] for o, n in zip(offs, n_fix)]
 
@@ -185,12 +242,13 @@ def _is_flac(path: str) -> bool:
 
 
 def load(path: str, sr: Optional[int] = 24000, device: Union[str, torch.device] = "cuda",
-         as_numpy: bool = True):
-    """``librosa.load(path, sr=sr, res_type='polyphase')`` for WAV and FLAC files: returns (samples, sr).  Samples
-    are a numpy float32 array (``as_numpy``) or the device tensor, ready for ``MimiHipModel.encode``."""
+         as_numpy: bool = True, res_type: str = "polyphase"):
+    """``librosa.load(path, sr=sr, res_type=res_type)`` for WAV and FLAC files: returns (samples, sr).  Samples
+    are a numpy float32 array (``as_numpy``) or the device tensor, ready for ``MimiHipModel.encode``.  The default
+    stays the pinned ``"polyphase"``; ``"soxr_hq"`` (librosa's own default) is the soxr HQ spec, unpinned."""
     y, file_sr = load_flac(path) if _is_flac(path) else load_wav(path)
     if sr is None or sr == file_sr:
         t = torch.from_numpy(y)
         return (y if as_numpy else t.to(_device(device))), file_sr
-    out = resample([y], file_sr, sr, device)[0]
+    out = resample([y], file_sr, sr, device, res_type=res_type)[0]
     return (out.cpu().numpy() if as_numpy else out), sr

@@ -1,5 +1,5 @@
-// Sanitizer harness for the host code that parses untrusted bytes: the FLAC decoder (csrc/flac.cpp) and the
-// safetensors checkpoint reader (csrc/safetensors.cpp), built with -fsanitize=address,undefined by
+// Sanitizer harness for the host code that parses untrusted bytes: the FLAC decoder (csrc/flac.cpp), the
+// safetensors checkpoint reader (csrc/safetensors.cpp) and the config.json reader (csrc/config_json.cpp), built with -fsanitize=address,undefined by
 // tools/asan/Makefile and driven by tests/test_sanitizers.py (CPU only: the GPU pool has no GPU sanitizers).
 //
 //   host_fuzz [--mutations N] file...
@@ -85,6 +85,15 @@ static int run_st(const std::vector<uint8_t>& d, uint64_t* sum) {
     return st;
 }
 
+// config.json (config_json.cpp): the status and a checksum of the struct it fills
+static int run_cfg(const std::vector<uint8_t>& d, uint64_t* sum) {
+    mimi_config c;
+    std::memset(&c, 0, sizeof(c));
+    const int st = mimi::config_from_json_text(std::string(d.begin(), d.end()), &c);
+    *sum = st ? 0 : fnv(&c, sizeof(c));
+    return st;
+}
+
 int main(int argc, char** argv) {
     int mutations = 200;
     std::vector<std::string> files;
@@ -105,8 +114,10 @@ int main(int argc, char** argv) {
     for (const auto& fn : files) {
         std::ifstream f(fn, std::ios::binary);
         std::vector<uint8_t> d((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-        const bool flac = ends_with(fn, ".flac");
-        auto run = [&](const std::vector<uint8_t>& x, uint64_t* s) { return flac ? run_flac(x, s) : run_st(x, s); };
+        const bool flac = ends_with(fn, ".flac"), json = ends_with(fn, ".json");
+        auto run = [&](const std::vector<uint8_t>& x, uint64_t* s) {
+            return flac ? run_flac(x, s) : json ? run_cfg(x, s) : run_st(x, s);
+        };
         uint64_t sum = 0;
         const int st = run(d, &sum);
         std::printf("%s status=%d sum=%016llx\n", fn.c_str(), st, (unsigned long long)sum);
