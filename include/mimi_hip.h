@@ -212,8 +212,9 @@ int64_t mimi_graph_replays(const mimi_engine* e);
  * chain gave up), "rvq_chain_fault" 0/1/2 (tests only: 1 = zero spin budget, 2 = every sweep gives up), "rvq_xcd"
  * 0/1.  "sc1_out" 0-7 (sc1 output stores: bit 0 q/k/v, 1 fc1 (default 2), 2 o_proj + fc2), "ln_rpw" 0/1/2/4/8
  * (LayerNorm rows per wave), "fc1_cg" 0/1/2/4 (fc1's tile order in XCD column groups, default 1 = none), "res1_form"
- * 0/1 (stage-1 block as one 8-wave or two 4-wave workgroups per CU, default 1), "res1_stream" 0/1 (stage 2's k = 1
- * residual conv as the streaming kernel with register-resident weights, default 1), "attn_band_split" 0/1/2 (items
+ * 0/1 (stage-1 block as one 8-wave or two 4-wave workgroups per CU, default 1), "res1_stream" 0/1/2 (the k = 1
+ * residual conv of stages 2 and 3 as the streaming kernel with register-resident weights: 1 both (default; stage 3
+ * uniform batches), 2 stage 2 only, 0 off), "attn_band_split" 0/1/2 (items
  * over 256 frames: the banded attention as 128-query workgroups, by grid size (default), or one 32-query tile per
  * workgroup).  Unknown keys and values:
  * MIMI_ERR_INVALID_ARGUMENT.  A change drops the captured graphs. */
@@ -272,6 +273,14 @@ int mimi_bpe_create(int device, const int32_t* symbols, int64_t n_symbols, const
 int mimi_bpe_best(mimi_bpe* h, int32_t* left, int32_t* right, int64_t* count);
 int mimi_bpe_merge(mimi_bpe* h, int32_t left, int32_t right, int32_t new_id, int32_t new_len);
 void mimi_bpe_destroy(mimi_bpe* h);
+
+/*
+ * Diagnostic: the fp16 plane split the kernels use (two v_fma_mix per value: hi = fp16(v s), lo = fp16(v s - hi))
+ * against the conversion form it replaces, on npairs value pairs of dev_in (device f32 [2 npairs], s a power of two):
+ * dev_out (device u32 [npairs][4]) = the kernels' (hi, lo) words and the conversion form's (hi, lo) words.  Tests
+ * require them equal on edge values (zeros of both signs, fp32 / fp16 subnormals, rounding ties, fp16 overflow).
+ */
+int mimi_split_check(const float* dev_in, int64_t npairs, float scale, uint32_t* dev_out, void* stream);
 
 /* Device bytes the workspace needs for (batch, length); the engine grows it on demand. */
 int64_t mimi_workspace_bytes(const mimi_engine* e, int32_t batch, int64_t length);

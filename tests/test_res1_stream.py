@@ -1,8 +1,10 @@
-"""Stage-2 k = 1 residual conv + skip + ELU as the streaming kernel (res1_stream.hip, engine option "res1_stream") against
-the planes GEMM it replaces (ROLE_RES1P): the same fragments, K order, product order and epilogue expressions, so the
-stage-2 block output (tap "res2_elu": the y planes the down conv reads) and all 32 codebooks must be equal BITWISE --
-uniform batches whose row count is not a multiple of the 16-step tile, a 1-sample item, ragged batches (per-item valid
-steps) and graph replays (TF/modeling_mimi.py:433-447 MimiResnetBlock, the 1 kHz stage)."""
+"""The k = 1 residual conv + skip + ELU of stages 2 and 3 as the streaming kernel (res1_stream.hip, engine option
+"res1_stream": 1 both stages, 2 stage 2 only, 0 the planes GEMM) against the planes GEMM it replaces (ROLE_RES1P): the
+same fragments, K order, product order and epilogue expressions, so the stage-2 and stage-3 block outputs (taps
+"res2_elu" / "res3_elu": the y planes the down convs read) and all 32 codebooks must be equal BITWISE -- uniform
+batches whose row count is not a multiple of the 16-step tile, a 1-sample item, ragged batches (per-item valid steps;
+stage 3 keeps the GEMM there) and graph replays (TF/modeling_mimi.py:433-447 MimiResnetBlock, the 1 kHz and 200 Hz
+stages)."""
 import numpy as np
 import pytest
 import torch
@@ -27,13 +29,13 @@ def run(engine, on, x, taps=True, K=32):
     engine.set_taps(taps)
     try:
         c = engine.encode_int32(x, K).cpu().numpy()
-        return c, (engine.get_tap("res2_elu").copy() if taps else None)
+        return c, ((engine.get_tap("res2_elu").copy(), engine.get_tap("res3_elu").copy()) if taps else None)
     finally:
         engine.set_taps(False)
         engine.set_option("res1_stream", 1)
 
 
-FORMS = [1]  # res1_stream on
+FORMS = [1, 2]  # res1_stream on (both stages), stage 2 only
 
 
 @pytest.mark.parametrize("B,L", [(8, 240000), (3, 24000 * 7 + 11), (2, 1), (5, 1920 * 33 + 7)])
@@ -42,7 +44,8 @@ def test_res1_stream_uniform_bitwise(engine, B, L):
     c0, y0 = run(engine, 0, x)
     for f in FORMS:
         c1, y1 = run(engine, f, x)
-        assert np.array_equal(y0.view(np.uint32), y1.view(np.uint32)), (f, int((y0 != y1).sum()))
+        for st, a, b in zip((2, 3), y0, y1):
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (f, st, int((a != b).sum()))
         assert np.array_equal(c0, c1), (f, B, L)
 
 

@@ -147,6 +147,14 @@ extern "C" int mimi_resample_poly(const float* dev_in, const int64_t* dev_in_off
     return MIMI_OK;
 }
 
+extern "C" int mimi_split_check(const float* dev_in, int64_t npairs, float scale, uint32_t* dev_out, void* stream) {
+    if (npairs < 0 || (npairs > 0 && (!dev_in || !dev_out)) || !(scale > 0.0f))
+        return set_err(MIMI_ERR_INVALID_ARGUMENT, "mimi_split_check: bad arguments");
+    const hipError_t e = launch_split_check(dev_in, npairs, scale, dev_out, (hipStream_t)stream);
+    if (e != hipSuccess) return set_err(MIMI_ERR_HIP, "split_check launch: %s", hipGetErrorString(e));
+    return MIMI_OK;
+}
+
 // ------------------------------------------------------------------------------------------------
 // engine
 // ------------------------------------------------------------------------------------------------
@@ -343,8 +351,9 @@ struct mimi_engine {
     // 8-wave workgroup per CU, 1 two 4-wave workgroups per CU (each wave both 16-step tiles of its M tile; their block
     // chains interleave on the SIMDs: 0.59 -> 0.555 ms per B = 32 step, profiles/r4aa_ab_res1_form.txt)
     int res1_form = 1;
-    // stage 2's k1 conv + skip + ELU as the streaming kernel (res1_stream.hip) instead of the planes GEMM
-    // (mimi_set_option "res1_stream"; same bits): res1_s2 0.229-0.231 -> 0.218-0.221 ms per B = 32 step
+    // the k1 conv + skip + ELU of stages 2 and 3 as the streaming kernel (res1_stream.hip) instead of the planes GEMM
+    // (mimi_set_option "res1_stream": 1 both stages, 2 stage 2 only, 0 off; same bits): res1_s2 0.229-0.231 ->
+    // 0.218-0.221 ms per B = 32 step (round 5); stage 3 (uniform batches) round 6
     int res1_stream = 1;
     struct Tap {
         float* d = nullptr;
@@ -1490,7 +1499,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             if (rg) a1.a_rows = a1.m_rows = dT[si];
             yact = new_act(nmf("y%d", si));
             out_act(a1, yact);
-            if (h16 && e->res1_stream && res1_stream_ok(a1))
+            if (h16 && e->res1_stream && res1_stream_ok(a1) && (e->res1_stream == 1 || a1.K == 128))
                 LAUNCH_TRY(launch_res1_stream(a1, s, &kname), "res1 stream");
             else
                 LAUNCH_TRY(launch_gemm(ROLE_RES1P, a1, s, &kname, prec), "res1");
@@ -2569,7 +2578,7 @@ static const EngineOption kEngineOptions[] = {
     {"attn_band_split", &mimi_engine::attn_band_split, 0x7u, "0, 1 or 2"},
     {"fc1_cg", &mimi_engine::fc1_cg, 0x17u, "0, 1, 2 or 4"},
     {"res1_form", &mimi_engine::res1_form, 0x3u, "0 or 1"},
-    {"res1_stream", &mimi_engine::res1_stream, 0x3u, "0 or 1"},
+    {"res1_stream", &mimi_engine::res1_stream, 0x7u, "0, 1 or 2"},
 };
 
 extern "C" int mimi_set_option(mimi_engine* e, const char* key, int64_t value) {

@@ -624,7 +624,10 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                 } else if (EPI == EPI_BIAS_ELU) {
                     v = elu1(v + bias);
                 } else if (EPI == EPI_BIAS_RES_ELU) {
-                    v = v + bias;  // + R and ELU in phase 2 (vector R loads)
+                    // + R and ELU in phase 2 (vector R loads).  fp16 planes: acc * unscale + bias as one FMA -- the same
+                    // value (the power-of-two unscale makes the product exact) in one instruction, as res1_stream and
+                    // the fused blocks form it
+                    v = F16 ? __builtin_fmaf(acc[i][j][r], us, bias) : v + bias;
                 } else if (EPI == EPI_GELU) {
                     v = gelu_erf(v);
                 } else if (EPI == EPI_SCALE_RES) {
@@ -688,15 +691,13 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                 for (int e = 0; e < 8; ++e) pv[e] = elu1(pv[e]);
             }
             if constexpr (SC1) {  // store_act8's fp16 split, stored sc1
-                typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
-                f16x8_t ha, hb;
+                uint4 ha, hb;
+                split2_f16s(pv[0], pv[1], p.out_scale, ha.x, hb.x);
+                split2_f16s(pv[2], pv[3], p.out_scale, ha.y, hb.y);
+                split2_f16s(pv[4], pv[5], p.out_scale, ha.z, hb.z);
+                split2_f16s(pv[6], pv[7], p.out_scale, ha.w, hb.w);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float t = pv[e] * p.out_scale;
-                    ha[e] = (_Float16)t;
-                    hb[e] = (_Float16)(t - (float)ha[e]);
-                    omx = fmaxf(omx, fabsf(pv[e]));
-                }
+                for (int e = 0; e < 8; ++e) omx = fmaxf(omx, fabsf(pv[e]));
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ha), cp_rs, (int)(off * 2), 0, 16);
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hb), cp_rs,
                                                        (int)((off + p.c_pstride) * 2), 0, 16);

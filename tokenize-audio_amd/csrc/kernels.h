@@ -50,22 +50,38 @@ __device__ __forceinline__ void store_act(float* f32, void* planes, long long ps
 }
 
 // 8 consecutive values as planes (16-B stores per plane): bf16 (ns = 2/3) or scaled fp16 (hscale > 0)
+// The 2 fp16 planes of (v0, v1) * s (s a power of two) as exact arithmetic defines them: hi = RN16(v s),
+// lo = RN16(v s - hi), two values per dword.  lo is one FMA (v s - hi exact, then one rounding), which hipcc emits as
+// v_fma_mix_f32 (hi read straight from its fp16 half) + one v_cvt_pk per pair: 6 instructions a pair instead of 8
+// for mul, cvt, cvt back, sub, cvt.  The same bits as that form wherever v s is exact in fp32 (a power-of-two
+// scale); where v s underflows fp32 both give a zero lo plane, this form with the sign of the exact product
+// (tests/test_split_planes.py checks it against float64 arithmetic).
+__device__ __forceinline__ void split2_f16s(float v0, float v1, float s, unsigned& hi, unsigned& lo) {
+    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+    typedef float f2_t __attribute__((ext_vector_type(2)));
+    const f2_t t = {v0 * s, v1 * s};
+    const h2_t h = __builtin_convertvector(t, h2_t);
+    h2_t l;
+    l[0] = (_Float16)__builtin_fmaf(v0, s, -(float)h[0]);
+    l[1] = (_Float16)__builtin_fmaf(v1, s, -(float)h[1]);
+    hi = __builtin_bit_cast(unsigned, h);
+    lo = __builtin_bit_cast(unsigned, l);
+}
+
 __device__ __forceinline__ void store_act8(void* planes, long long pstride, int ns, long long idx, const float (&v)[8],
                                            float hscale, float* mx) {
     typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-    typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
     if (hscale > 0.0f) {
-        f16x8_t a, b;
+        uint4 a, b;
+        split2_f16s(v[0], v[1], hscale, a.x, b.x);
+        split2_f16s(v[2], v[3], hscale, a.y, b.y);
+        split2_f16s(v[4], v[5], hscale, a.z, b.z);
+        split2_f16s(v[6], v[7], hscale, a.w, b.w);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float t = v[e] * hscale;
-            a[e] = (_Float16)t;
-            b[e] = (_Float16)(t - (float)a[e]);
-            *mx = fmaxf(*mx, fabsf(v[e]));
-        }
+        for (int e = 0; e < 8; ++e) *mx = fmaxf(*mx, fabsf(v[e]));
         _Float16* hp = reinterpret_cast<_Float16*>(planes) + idx;
-        *reinterpret_cast<f16x8_t*>(hp) = a;
-        *reinterpret_cast<f16x8_t*>(hp + pstride) = b;
+        *reinterpret_cast<uint4*>(hp) = a;
+        *reinterpret_cast<uint4*>(hp + pstride) = b;
         return;
     }
     float rem[8];
@@ -131,16 +147,8 @@ __device__ __forceinline__ void ln_row_coeffs(const float (&v)[C / 64], float ep
 __device__ __forceinline__ float ln_affine(float v, float sc, float bi, float g, float b) { return (v * sc + bi) * g + b; }
 // fp16 planes of 4 LayerNorm outputs o * yscale (PREC_F16X3): hi / lo as 4 halves each
 __device__ __forceinline__ void ln_split4_f16(const float (&o)[4], float yscale, uint2& hi, uint2& lo) {
-    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
-    h4_t h0, h1;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const float t = o[e] * yscale;
-        h0[e] = (_Float16)t;
-        h1[e] = (_Float16)(t - (float)h0[e]);
-    }
-    hi = __builtin_bit_cast(uint2, h0);
-    lo = __builtin_bit_cast(uint2, h1);
+    split2_f16s(o[0], o[1], yscale, hi.x, lo.x);
+    split2_f16s(o[2], o[3], yscale, hi.y, lo.y);
 }
 
 // A pointer a captured hipGraph reads at run time: the engine's io block, written by set_io_kernel in front of
@@ -153,6 +161,7 @@ __device__ __forceinline__ T* io_pointer(T* const* ref, T* direct) {
     return reinterpret_cast<T*>(((unsigned long long)hi << 32) | lo);
 }
 // io[0] = audio, io[1] = codes (the pointers of one graph replay)
+hipError_t launch_split_check(const float* in, long long npairs, float s, unsigned* out, hipStream_t st);
 hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStream_t s, unsigned* hamax = nullptr,
                          unsigned* hflag = nullptr, void* zero = nullptr, size_t zero_bytes = 0);
 

@@ -1203,6 +1203,35 @@ hipError_t launch_ragged_rows(const int* tlen, const int* toff, int B, int* rpos
     return hipGetLastError();
 }
 
+// Self-check of the fp16 plane split (kernels.h split2_f16s, the form every planes epilogue, LayerNorm and conv0 use)
+// against the plain form it replaces (fp16(v s), fp16(v s - hi) by conversions): per value pair, out[4 i .. 4 i + 3]
+// = split2_f16s's (hi, lo) words and the plain form's (hi, lo) words.  Diagnostic entry mimi_split_check.
+__global__ __launch_bounds__(256) void split_check_kernel(const float* __restrict__ in, long long npairs, float s,
+                                                          unsigned* __restrict__ out) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < npairs; i += (long long)gridDim.x * 256) {
+        const float v0 = in[2 * i], v1 = in[2 * i + 1];
+        unsigned hi, lo;
+        split2_f16s(v0, v1, s, hi, lo);
+        const float t0 = v0 * s, t1 = v1 * s;
+        h2 a, b;
+        a[0] = (_Float16)t0;
+        a[1] = (_Float16)t1;
+        b[0] = (_Float16)(t0 - (float)a[0]);
+        b[1] = (_Float16)(t1 - (float)a[1]);
+        out[4 * i] = hi;
+        out[4 * i + 1] = lo;
+        out[4 * i + 2] = __builtin_bit_cast(unsigned, a);
+        out[4 * i + 3] = __builtin_bit_cast(unsigned, b);
+    }
+}
+hipError_t launch_split_check(const float* in, long long npairs, float s, unsigned* out, hipStream_t st) {
+    if (npairs <= 0) return hipSuccess;
+    const long long blocks = std::min<long long>((npairs + 255) / 256, 4096);
+    hipLaunchKernelGGL(split_check_kernel, dim3((unsigned)blocks), dim3(256), 0, st, in, npairs, s, out);
+    return hipGetLastError();
+}
+
 // (+ zeroes the replay's RVQ chain flag and granules, n16 16-B units from zero: the memset node a graph would hold)
 __global__ __launch_bounds__(256) void set_io_kernel(void** io, const float* audio, int32_t* codes, unsigned* hamax,
                                                      unsigned* hflag, uint4* zero, long long n16) {

@@ -16,8 +16,10 @@
 //
 // Every output element is the planes GEMM's: the same fragments (k chunk 8 (lane / 16) of each 32-wide K step, K
 // steps in order), the same product order per K step (h_lo W_hi, h_hi W_lo, h_hi W_hi; the transposition swaps
-// the MFMA operands, not the products -- as in stage0_fused.hip), and the same epilogue expressions (acc * unscale
-// + bias, then R + that, ELU, store_act8's fp16 split).  Bitwise the ROLE_RES1P output (tests/test_res1_stream.py).
+// the MFMA operands, not the products -- as in stage0_fused.hip), and the same epilogue expressions (fma(acc,
+// unscale, bias), then R + that, ELU, store_act8's fp16 split).  Bitwise the ROLE_RES1P output (tests/test_res1_stream.py).
+#include <algorithm>
+
 #include "gemm_planes.h"
 #include "kernels.h"
 
@@ -31,14 +33,20 @@ constexpr int R1S_MAXB = 256;  // ragged batches: items the in-kernel tile table
 
 // RG: a ragged batch (p.m_rows) -- its own instantiation, so the uniform kernel's loop carries none of the tile-table
 // lookups (run-time-branched into one kernel they cost the uniform batches 13 %: 0.220 -> 0.249 ms per B = 32 step)
+// A workgroup is 4 waves x CPW output channels; NG = N / (4 CPW) workgroup columns (blockIdx.y) cover N.  Stage 2
+// (K = 128, N = 256): one column, W1 128 VGPRs per wave.  Stage 3 (K = 256, N = 512): two columns, W1 256 registers
+// per wave -- the compiler keeps them beside the ring in the accumulation registers (256 VGPRs + 236 AGPRs, no
+// scratch; one wave per SIMD), and both columns of a tile run at the same time on one XCD (workgroup x and x + G
+// share x mod 8), so its h rows come from that XCD's L2 the second time.
 template <int K, int DEPTH, int CPW, bool RG>
-__global__ __launch_bounds__(2 * K / CPW * 64) void res1_stream_kernel(GemmArgs p, int ntiles) {
+__global__ __launch_bounds__(256) void res1_stream_kernel(GemmArgs p, int ntiles) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    constexpr int N = 2 * K, KS = K / 32, CT = CPW / 16, LC = CPW / 4;
+    constexpr int N = 2 * K, KS = K / 32, CT = CPW / 16, LC = CPW / 4, NG = N / (4 * CPW);
+    static_assert(NG >= 1 && NG * 4 * CPW == N, "4 waves x CPW channels per workgroup column");
     typedef _Float16 h8 __attribute__((ext_vector_type(8)));
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int c0 = wave * CPW;
+    const int c0 = ((NG > 1 ? (int)blockIdx.y : 0) * 4 + wave) * CPW;
     const int l16 = lane & 15, q = lane >> 4;
     // W1 fragments: [channel tile][k step][plane]; row l16 of tile ct = channel c0 + LC (l16 / 4) + 4 ct + l16 % 4
     h8 wf[CT][KS][2];
@@ -150,8 +158,7 @@ __global__ __launch_bounds__(2 * K / CPW * 64) void res1_stream_kernel(GemmArgs 
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     const int c = 8 * g + e;
-                    float v = acc[c >> 2][c & 3] * us;  // (the planes GEMM's phase 1: acc * unscale, + bias)
-                    v = v + bias[c];
+                    const float v = __builtin_fmaf(acc[c >> 2][c & 3], us, bias[c]);  // (the planes GEMM's phase 1)
                     const float rv = t.r[c >> 2][c & 3];
                     pv[e] = elu1(rv + v);  // phase 2: R + (acc + bias), ELU
                 }
@@ -180,22 +187,24 @@ __global__ __launch_bounds__(2 * K / CPW * 64) void res1_stream_kernel(GemmArgs 
 #endif
 }
 
-// the stage-2 shape (K = 128, N = 256) with the engine's layouts: h planes [rows][K], skip / planes out [rows][N],
-// items back to back (rows = batch x M), no fp32 output; otherwise hipErrorInvalidValue (the engine keeps the GEMM)
+// the stage-2 shape (K = 128, N = 256; uniform or ragged) or the stage-3 shape (K = 256, N = 512; uniform batches)
+// with the engine's layouts: h planes [rows][K], skip / planes out [rows][N], items back to back (rows = batch x M),
+// no fp32 output; otherwise hipErrorInvalidValue (the engine keeps the GEMM)
 bool res1_stream_ok(const GemmArgs& a) {
-    return a.K == 128 && a.N == 256 && a.Ap && a.Wsplit && a.R && a.Cp && !a.C && a.bias && a.out_amax &&
+    return ((a.K == 128 && a.N == 256) || (a.K == 256 && a.N == 512 && !a.m_rows)) && a.Ap && a.Wsplit && a.R &&
+           a.Cp && !a.C && a.bias && a.out_amax &&
            a.a_rs == a.K && a.a_cin == a.K && a.a_off == 0 && a.ldc == a.N && a.a_bstride == (long long)a.M * a.K &&
            a.c_bstride == (long long)a.M * a.N && !a.a_boff && !a.c_boff && (!a.m_rows == !a.a_rows) &&
            (!a.m_rows || a.batch <= R1S_MAXB) &&
            (long long)a.M * a.batch * a.N * 4 < 0x7fffffffLL && a.out_scale > 0.0f && a.unscale > 0.0f;
 }
 
-template <int DEPTH, int CPW>
+template <int K, int DEPTH, int CPW>
 static hipError_t run_res1_stream(const GemmArgs& a, hipStream_t s, const char** kname) {
-    constexpr int NT = 256 / CPW * 64;
+    constexpr int NT = 256, NG = 2 * K / (4 * CPW);
     static thread_local char nm[80];
     const bool rg = a.m_rows != nullptr;
-    snprintf(nm, sizeof nm, "mimi::res1_stream_kernel<128, %d, %d, %s>(mimi::GemmArgs, int)", DEPTH, CPW,
+    snprintf(nm, sizeof nm, "mimi::res1_stream_kernel<%d, %d, %d, %s>(mimi::GemmArgs, int)", K, DEPTH, CPW,
              rg ? "true" : "false");
     if (kname) *kname = nm;
     const long long rows = (long long)a.M * a.batch;
@@ -204,15 +213,22 @@ static hipError_t run_res1_stream(const GemmArgs& a, hipStream_t s, const char**
         int dev = 0, ncu = 256, occ = 1;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, res1_stream_kernel<128, DEPTH, CPW, false>, NT, 0);
-        return ncu * (occ > 0 ? occ : 1);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, res1_stream_kernel<K, DEPTH, CPW, false>, NT, 0);
+        // NG columns share the resident slots; a multiple of the 8 XCDs per column keeps a tile's columns on one XCD
+        return std::max(8, ncu * (occ > 0 ? occ : 1) / NG / 8 * 8);
     }();
     const int grid = ntiles < slots ? ntiles : slots;
-    if (rg)
-        hipLaunchKernelGGL((res1_stream_kernel<128, DEPTH, CPW, true>), dim3((unsigned)grid), dim3(NT), 0, s, a, ntiles);
-    else
-        hipLaunchKernelGGL((res1_stream_kernel<128, DEPTH, CPW, false>), dim3((unsigned)grid), dim3(NT), 0, s, a,
-                           ntiles);
+    if constexpr (K == 128) {
+        if (rg) {
+            hipLaunchKernelGGL((res1_stream_kernel<K, DEPTH, CPW, true>), dim3((unsigned)grid), dim3(NT), 0, s, a,
+                               ntiles);
+            return hipGetLastError();
+        }
+    } else if (rg) {
+        return hipErrorInvalidValue;  // (res1_stream_ok keeps ragged stage-3 batches on the planes GEMM)
+    }
+    hipLaunchKernelGGL((res1_stream_kernel<K, DEPTH, CPW, false>), dim3((unsigned)grid, (unsigned)NG), dim3(NT), 0, s,
+                       a, ntiles);
     return hipGetLastError();
 }
 
@@ -221,9 +237,16 @@ static hipError_t run_res1_stream(const GemmArgs& a, hipStream_t s, const char**
 // per wave with a 1- / 2- / 3-deep ring 0.288 / 0.31 / 0.31 (half-line stores); 64 per wave without a ring 0.315, with
 // the 2-deep ring 0.218-0.221 (kept); W1 in LDS, 64 per wave, 2 row groups x 2- / 3-deep, 3 groups x 2-deep:
 // 0.235-0.243)
+#ifndef MIMI_R1S_DEPTH2
+#define MIMI_R1S_DEPTH2 2  // ring depth of the stage-2 form (A/B builds: tools/build_variant.sh)
+#endif
+#ifndef MIMI_R1S_DEPTH3
+#define MIMI_R1S_DEPTH3 2  // ring depth of the stage-3 form
+#endif
 hipError_t launch_res1_stream(const GemmArgs& a, hipStream_t s, const char** kname) {
     if (!res1_stream_ok(a)) return hipErrorInvalidValue;
-    return run_res1_stream<2, 64>(a, s, kname);
+    if (a.K == 256) return run_res1_stream<256, MIMI_R1S_DEPTH3, 64>(a, s, kname);
+    return run_res1_stream<128, MIMI_R1S_DEPTH2, 64>(a, s, kname);
 }
 
 }  // namespace mimi

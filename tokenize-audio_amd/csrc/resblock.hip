@@ -569,11 +569,11 @@ __global__ __launch_bounds__(768) void resblock0_h16_kernel(ResArgs p) {
         f16x8 bq;  // taps audio[t - 6 + k], k = 0..7 (k = 7 has zero weight): hi plane (hh = 0) | lo plane
 #pragma unroll
         for (int k = 0; k < 8; k += 2) {
-            const f32x2 t = {aud[j + 2 + k] * sa, aud[j + 3 + k] * sa};
-            const f16x2 h = __builtin_convertvector(t, f16x2);
-            const f16x2 l = __builtin_convertvector(t - __builtin_convertvector(h, f32x2), f16x2);
-            bq[k] = hh ? l[0] : h[0];
-            bq[k + 1] = hh ? l[1] : h[1];
+            unsigned hi2, lo2;  // (fp16(a sa), fp16(a sa - hi): kernels.h split2_f16s, the same bits as the cvt form)
+            split2_f16s(aud[j + 2 + k], aud[j + 3 + k], sa, hi2, lo2);
+            const f16x2 pair = __builtin_bit_cast(f16x2, hh ? lo2 : hi2);
+            bq[k] = pair[0];
+            bq[k + 1] = pair[1];
         }
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {

@@ -212,21 +212,23 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
         const float v = audio[ok ? (long long)bb * T + pos : 0];
         return ok ? v : 0.0f;
     };
+    // the audio window as its two fp16 planes: each lane splits its own sample once (kernels.h split2_f16s) and
+    // stores hi / lo halves; a lane then reads its 8 taps' halves of the plane it feeds (hh) -- 8 d16 LDS reads
+    // instead of 8 float reads and 4 pair splits per lane on the block wave's chain (the same values)
+    _Float16* audh = reinterpret_cast<_Float16*>(aud);  // [AUD] hi plane, then [AUD] lo plane (the AUD floats' bytes)
     auto conv0 = [&](float av, f32x16 (&x0)[2]) {
         if (lane < AUD) {
             mxa = fmaxf(mxa, fabsf(av));
-            aud[lane] = av;
+            unsigned hw, lw;
+            split2_f16s(av, 0.0f, sa, hw, lw);
+            audh[lane] = __builtin_bit_cast(f16x2, hw)[0];
+            audh[AUD + lane] = __builtin_bit_cast(f16x2, lw)[0];
         }
         S0F_DRAIN();
         f16x8 bq;
+        const _Float16* ap = audh + (hh ? AUD : 0) + j + 2;
 #pragma unroll
-        for (int k = 0; k < 8; k += 2) {
-            const f32x2 t = {aud[j + 2 + k] * sa, aud[j + 3 + k] * sa};
-            const f16x2 h = __builtin_convertvector(t, f16x2);
-            const f16x2 l = __builtin_convertvector(t - __builtin_convertvector(h, f32x2), f16x2);
-            bq[k] = hh ? l[0] : h[0];
-            bq[k + 1] = hh ? l[1] : h[1];
-        }
+        for (int k = 0; k < 8; ++k) bq[k] = ap[k];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
             f32x16 acc;

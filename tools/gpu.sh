@@ -14,6 +14,8 @@
 #   taps             tools/race_taps.py: engine A's stage taps vs A alone while a clone loads the GPU (REPS, 300)
 #   race             tools/race_probe.py: codes of two engines encoding at once vs one alone
 #   pk_probe         tools/pk_probe.hip: each packed-f32 operand form vs scalar, idle and under concurrent load
+#   bits             tools/lib_codes.py for each ab/libmimi_hip_<name>.so in BITS_LIBS and the in-tree library, then
+#                    tools/cmp_codes.py: codes and every stage tap bitwise against the first of BITS_LIBS
 #   gloo2            the N-rank bench path rehearsed on this box: --gpus 2 over gloo, both ranks sharing its GPU
 #                    (the line must list both ranks on one PCI bus and say `sharing`)
 #   b:NAME:ARGS      one bench run with ARGS (spaces as '+'), -> bench_NAME.json
@@ -79,6 +81,16 @@ for step in "$@"; do
         || fail pk_build $? "$O/pk_build.log"
       timeout -k 10 300 tools/bin/pk_probe ${LAUNCHES:-40} > "$O/pk_probe.log" 2>&1 || fail pk_probe $? "$O/pk_probe.log"
       cat "$O/pk_probe.log" ;;
+    bits)
+      for v in ${BITS_LIBS:?BITS_LIBS} new; do
+        if [ $v = new ]; then unset MIMI_HIP_LIB; else export MIMI_HIP_LIB=$R/ab/libmimi_hip_$v.so; fi
+        timeout -k 10 300 python -u tools/lib_codes.py ${TAG}_$v > "$O/bits_$v.log" 2>&1 || fail "bits $v" $? "$O/bits_$v.log"
+      done
+      unset MIMI_HIP_LIB
+      ref=${BITS_LIBS%% *}
+      python3 tools/cmp_codes.py ${TAG}_$ref $(for v in ${BITS_LIBS#$ref} new; do echo ${TAG}_$v; done) > "$O/bits_cmp.txt" 2>&1
+      rc=$?; grep -c "bitwise equal" "$O/bits_cmp.txt"; grep -v "bitwise equal" "$O/bits_cmp.txt" | head -20
+      [ $rc -eq 0 ] || fail bits_cmp $rc "$O/bits_cmp.txt" ;;
     gloo2)
       MIMI_BENCH_DIST_BACKEND=gloo timeout -k 10 400 python -u bench.py --gpus 2 --steps 5 --warmup 2 \
         --cpu-baseline-seconds 0 --no-f32-mode --json-out "$O/bench_gloo2.json" > "$O/bench_gloo2.log" 2>&1 \

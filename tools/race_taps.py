@@ -28,7 +28,8 @@ def run_a():
     with torch.cuda.stream(sa):
         c = A.encode_int32(xu, 32).cpu().numpy()
     if names is None:
-        names = ["conv0", "encoder", "xfmr0", "xfmr7", "ds_gemm", "downsample", "proj"]
+        names = ["conv0", "res0_elu", "down0", "res1_elu", "down1", "res2_elu", "down2", "res3_elu", "down3_elu",
+                 "encoder", "xfmr0", "xfmr7", "ds_gemm", "downsample", "proj"]
     return c, {n: A.get_tap(n).copy() for n in names}
 
 
