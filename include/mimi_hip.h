@@ -213,8 +213,8 @@ int64_t mimi_graph_replays(const mimi_engine* e);
  * 0/1.  "sc1_out" 0-7 (sc1 output stores: bit 0 q/k/v, 1 fc1 (default 2), 2 o_proj + fc2), "ln_rpw" 0/1/2/4/8
  * (LayerNorm rows per wave), "fc1_cg" 0/1/2/4 (fc1's tile order in XCD column groups, default 1 = none), "res1_form"
  * 0/1 (stage-1 block as one 8-wave or two 4-wave workgroups per CU, default 1), "res1_stream" 0/1/2 (the k = 1
- * residual conv of stages 2 and 3 as the streaming kernel with register-resident weights: 1 both (default; stage 3
- * uniform batches), 2 stage 2 only, 0 off), "attn_band_split" 0/1/2 (items
+ * residual conv as the streaming kernel with register-resident weights: 1 stage 2 (default), 2 stages 2 and 3 (stage 3
+ * uniform batches; measured slower there), 0 off), "attn_band_split" 0/1/2 (items
  * over 256 frames: the banded attention as 128-query workgroups, by grid size (default), or one 32-query tile per
  * workgroup).  Unknown keys and values:
  * MIMI_ERR_INVALID_ARGUMENT.  A change drops the captured graphs. */

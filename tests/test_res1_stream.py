@@ -1,5 +1,5 @@
 """The k = 1 residual conv + skip + ELU of stages 2 and 3 as the streaming kernel (res1_stream.hip, engine option
-"res1_stream": 1 both stages, 2 stage 2 only, 0 the planes GEMM) against the planes GEMM it replaces (ROLE_RES1P): the
+"res1_stream": 1 stage 2 (default), 2 stages 2 and 3, 0 the planes GEMM) against the planes GEMM it replaces (ROLE_RES1P): the
 same fragments, K order, product order and epilogue expressions, so the stage-2 and stage-3 block outputs (taps
 "res2_elu" / "res3_elu": the y planes the down convs read) and all 32 codebooks must be equal BITWISE -- uniform
 batches whose row count is not a multiple of the 16-step tile, a 1-sample item, ragged batches (per-item valid steps;
@@ -35,7 +35,7 @@ def run(engine, on, x, taps=True, K=32):
         engine.set_option("res1_stream", 1)
 
 
-FORMS = [1, 2]  # res1_stream on (both stages), stage 2 only
+FORMS = [1, 2]  # res1_stream on for stage 2 (default), for stages 2 and 3
 
 
 @pytest.mark.parametrize("B,L", [(8, 240000), (3, 24000 * 7 + 11), (2, 1), (5, 1920 * 33 + 7)])

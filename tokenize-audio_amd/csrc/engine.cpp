@@ -351,9 +351,9 @@ struct mimi_engine {
     // 8-wave workgroup per CU, 1 two 4-wave workgroups per CU (each wave both 16-step tiles of its M tile; their block
     // chains interleave on the SIMDs: 0.59 -> 0.555 ms per B = 32 step, profiles/r4aa_ab_res1_form.txt)
     int res1_form = 1;
-    // the k1 conv + skip + ELU of stages 2 and 3 as the streaming kernel (res1_stream.hip) instead of the planes GEMM
-    // (mimi_set_option "res1_stream": 1 both stages, 2 stage 2 only, 0 off; same bits): res1_s2 0.229-0.231 ->
-    // 0.218-0.221 ms per B = 32 step (round 5); stage 3 (uniform batches) round 6
+    // the k1 conv + skip + ELU as the streaming kernel (res1_stream.hip) instead of the planes GEMM (mimi_set_option
+    // "res1_stream": 1 stage 2 (default), 2 stages 2 and 3, 0 off; same bits): res1_s2 0.229-0.231 -> 0.218-0.221 ms
+    // per B = 32 step (round 5); stage 3 measured slower on it, 0.116-0.117 vs 0.109-0.113 (round 6, r6d / r6e)
     int res1_stream = 1;
     struct Tap {
         float* d = nullptr;
@@ -1499,7 +1499,7 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
             if (rg) a1.a_rows = a1.m_rows = dT[si];
             yact = new_act(nmf("y%d", si));
             out_act(a1, yact);
-            if (h16 && e->res1_stream && res1_stream_ok(a1) && (e->res1_stream == 1 || a1.K == 128))
+            if (h16 && e->res1_stream && res1_stream_ok(a1) && (e->res1_stream == 2 || a1.K == 128))
                 LAUNCH_TRY(launch_res1_stream(a1, s, &kname), "res1 stream");
             else
                 LAUNCH_TRY(launch_gemm(ROLE_RES1P, a1, s, &kname, prec), "res1");
