@@ -27,6 +27,14 @@
 #ifndef MIMI_FC1_V
 #define MIMI_FC1_V 0
 #endif
+// the smallest small-grid tile (16 rows) at 16 x 32 with one compute wave instead of 16 x 64 with two, per role (bit 0
+// o_proj, 1 final conv, 2 downsample, 3 input_proj): twice the workgroups on a batch-1 grid, the same instruction
+// sequence per output element.  o_proj: 87-89 -> 80-82 us per batch-1 encode, 10.19k -> 10.32k audio-s/s
+// (gpurun_out/r6f/ab.log, three alternations)
+#ifndef MIMI_SMALL16_32
+#define MIMI_SMALL16_32 1
+#endif
+
 
 namespace mimi {
 
@@ -268,6 +276,7 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
             return run_planes<16, 64, 1, 1, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
         }
         if (tiles(a, 64, 64) >= 256) return run_planes<64, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
+        // (16 x 64 tiles at batch 1 measured slower: fc1 0.142 -> 0.188 ms per encode, gpurun_out/r6f/ab.log)
         if (tiles(a, 32, 64) >= 256) return run_planes<32, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
         return run_planes<16, 64, 1, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
     }
@@ -285,17 +294,24 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         // <EPI, OUTP, TAG, 64-row BN, 32-row BM x BN / waves, 16-row BN / waves>; 16 x 16 wave tiles are too small for
         // the staged epilogue (64 lanes x 8 columns), and RoPE needs 64 columns per wave
         switch (role) {
-            case ROLE_FINAL: return run_small_h16<EPI_BIAS_OUT, 0, 4, 64, 32, 64, 2, 2, 64, 2>(a, s);
+            case ROLE_FINAL:
+                if (MIMI_SMALL16_32 & 2) return run_small_h16<EPI_BIAS_OUT, 0, 4, 64, 32, 64, 2, 2, 32, 1>(a, s);
+                return run_small_h16<EPI_BIAS_OUT, 0, 4, 64, 32, 64, 2, 2, 64, 2>(a, s);
             case ROLE_QKV: return run_small_h16<EPI_ROPE, 0, 5, 128, 32, 128, 2, 2, 64, 1>(a, s);
-            case ROLE_OPROJ: return run_small_h16<EPI_SCALE_RES, 0, 6, 64, 32, 64, 2, 2, 64, 2>(a, s);
+            case ROLE_OPROJ:
+                if (MIMI_SMALL16_32 & 1) return run_small_h16<EPI_SCALE_RES, 0, 6, 64, 32, 64, 2, 2, 32, 1>(a, s);
+                return run_small_h16<EPI_SCALE_RES, 0, 6, 64, 32, 64, 2, 2, 64, 2>(a, s);
             case ROLE_FC1: return run_small_h16<EPI_GELU, 2, 7, 64, 32, 64, 2, 2, 64, 2>(a, s);
             case ROLE_FC2:  // K = 2048: 6-deep rings retired 2 stages per barrier (-14 % at batch 1, profiles/r2c_ab_b1.log)
                 if (a.Cp)  // the last layer: fp32 residual stream + its planes (the downsample's input)
                     return run_small_h16<EPI_SCALE_RES, 2, 8, 32, 32, 32, 1, 2, 32, 1, 6, FL_KG2>(a, s);
                 return run_small_h16<EPI_SCALE_RES, 0, 8, 32, 32, 32, 1, 2, 32, 1, 6, FL_KG2>(a, s);
             case ROLE_DOWNSAMPLE:  // zero-padded here; engine.cpp adds the replicate rows (launch_ds_edge_fix)
+                if (MIMI_SMALL16_32 & 4) return run_small_h16<EPI_NONE, 2, 9, 64, 32, 64, 2, 2, 32, 1>(a, s);
                 return run_small_h16<EPI_NONE, 2, 9, 64, 32, 64, 2, 2, 64, 2>(a, s);
-            case ROLE_INPROJ: return run_small_h16<EPI_NONE, 0, 10, 64, 32, 64, 2, 2, 64, 2>(a, s);
+            case ROLE_INPROJ:
+                if (MIMI_SMALL16_32 & 8) return run_small_h16<EPI_NONE, 0, 10, 64, 32, 64, 2, 2, 32, 1>(a, s);
+                return run_small_h16<EPI_NONE, 0, 10, 64, 32, 64, 2, 2, 64, 2>(a, s);
             case ROLE_RES3P: return run_small_h16<EPI_BIAS_ELU, 2, 12, 64, 32, 64, 2, 2, 64, 2, 3>(a, s);
             default: break;
         }

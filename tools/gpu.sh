@@ -19,6 +19,7 @@
 #   gloo2            the N-rank bench path rehearsed on this box: --gpus 2 over gloo, both ranks sharing its GPU
 #                    (the line must list both ranks on one PCI bus and say `sharing`)
 #   b:NAME:ARGS      one bench run with ARGS (spaces as '+'), -> bench_NAME.json
+#   t:FILE          one GPU test file (tests/FILE), log t_FILE.log
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
@@ -96,6 +97,11 @@ for step in "$@"; do
         --cpu-baseline-seconds 0 --no-f32-mode --json-out "$O/bench_gloo2.json" > "$O/bench_gloo2.log" 2>&1 \
         || fail gloo2 $? "$O/bench_gloo2.log"
       python3 -c "import json; d=json.load(open('$O/bench_gloo2.json')); print('gloo2', d['value'], d['dist'], [(r['rank'], r['pci_bus']) for r in d['ranks']])" ;;
+    t:*)
+      f=${step#t:}
+      timeout -k 10 600 python -u -m pytest "tests/$f" -m gpu -x -v --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > "$O/t_$f.log" 2>&1 || fail "test $f" $? "$O/t_$f.log"
+      tail -1 "$O/t_$f.log" ;;
     b:*)
       spec=${step#b:}; name=${spec%%:*}; args=${spec#*:}
       bench_line "$name" ${args//+/ } ;;
