@@ -29,10 +29,11 @@
 #endif
 // the smallest small-grid tile (16 rows) at 16 x 32 with one compute wave instead of 16 x 64 with two, per role (bit 0
 // o_proj, 1 final conv, 2 downsample, 3 input_proj): twice the workgroups on a batch-1 grid, the same instruction
-// sequence per output element.  o_proj: 87-89 -> 80-82 us per batch-1 encode, 10.19k -> 10.32k audio-s/s
-// (gpurun_out/r6f/ab.log, three alternations)
+// sequence per output element (codes and taps bitwise equal, r6f / r6g).  Per batch-1 encode (three alternations each,
+// gpurun_out/r6f/ab.log, r6g/ab.log): o_proj 85-89 -> 80-82 us, final 27-29 -> 25, downsample 26-28 -> 23-25, input_proj
+// equal; all four on: 10.14k -> 10.28k audio-s/s on the r6g box
 #ifndef MIMI_SMALL16_32
-#define MIMI_SMALL16_32 1
+#define MIMI_SMALL16_32 15
 #endif
 
 
