@@ -156,6 +156,8 @@ static hipError_t run_planes_small_ld(const GemmArgs& a, hipStream_t s, int prec
     // waves instead of 4 (N = 512: 252 tiles, one round, so shorter per-tile chains win): o_proj -3 %, fc2 -1.4 %
     // (profiles/r2e_ab_8waves_oproj_fc2.log)
     if (prec == PREC_F16X3) {
+        // (128 x 64 tiles, twice the workgroups: fc2 0.50 -> 0.61, o_proj 0.21 -> 0.23, final 0.088 -> 0.112 ms per B = 32
+        // step, gpurun_out/r6h/ab.log)
         if (a.sc1) return run_planes<128, 128, 4, 2, 2, 3, EPI, 0, TAG, 4, 32, 16, FL_SC1OUT, true>(a, s);
         return run_planes<128, 128, 4, 2, 2, 3, EPI, 0, TAG, 4, 32, 16, 0, true>(a, s);
     }
