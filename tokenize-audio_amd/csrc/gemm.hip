@@ -32,6 +32,9 @@
 // sequence per output element (codes and taps bitwise equal, r6f / r6g).  Per batch-1 encode (three alternations each,
 // gpurun_out/r6f/ab.log, r6g/ab.log): o_proj 85-89 -> 80-82 us, final 27-29 -> 25, downsample 26-28 -> 23-25, input_proj
 // equal; all four on: 10.14k -> 10.28k audio-s/s on the r6g box
+#ifndef MIMI_SMALL16_32W
+#define MIMI_SMALL16_32W 1  // (A/B) compute waves of the 16 x 32 small-grid tile: 1 (16 x 32 each) or 2 (16 x 16 each,
+#endif                      // same bits; batch 1 equal within noise, o_proj 0.081 -> 0.084 ms: gpurun_out/r6j/ab.log)
 #ifndef MIMI_SMALL16_32
 #define MIMI_SMALL16_32 15
 #endif
@@ -298,22 +301,22 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         // the staged epilogue (64 lanes x 8 columns), and RoPE needs 64 columns per wave
         switch (role) {
             case ROLE_FINAL:
-                if (MIMI_SMALL16_32 & 2) return run_small_h16<EPI_BIAS_OUT, 0, 4, 64, 32, 64, 2, 2, 32, 1>(a, s);
+                if (MIMI_SMALL16_32 & 2) return run_small_h16<EPI_BIAS_OUT, 0, 4, 64, 32, 64, 2, 2, 32, MIMI_SMALL16_32W>(a, s);
                 return run_small_h16<EPI_BIAS_OUT, 0, 4, 64, 32, 64, 2, 2, 64, 2>(a, s);
             case ROLE_QKV: return run_small_h16<EPI_ROPE, 0, 5, 128, 32, 128, 2, 2, 64, 1>(a, s);
             case ROLE_OPROJ:
-                if (MIMI_SMALL16_32 & 1) return run_small_h16<EPI_SCALE_RES, 0, 6, 64, 32, 64, 2, 2, 32, 1>(a, s);
+                if (MIMI_SMALL16_32 & 1) return run_small_h16<EPI_SCALE_RES, 0, 6, 64, 32, 64, 2, 2, 32, MIMI_SMALL16_32W>(a, s);
                 return run_small_h16<EPI_SCALE_RES, 0, 6, 64, 32, 64, 2, 2, 64, 2>(a, s);
             case ROLE_FC1: return run_small_h16<EPI_GELU, 2, 7, 64, 32, 64, 2, 2, 64, 2>(a, s);
             case ROLE_FC2:  // K = 2048: 6-deep rings retired 2 stages per barrier (-14 % at batch 1, profiles/r2c_ab_b1.log)
                 if (a.Cp)  // the last layer: fp32 residual stream + its planes (the downsample's input)
-                    return run_small_h16<EPI_SCALE_RES, 2, 8, 32, 32, 32, 1, 2, 32, 1, 6, FL_KG2>(a, s);
-                return run_small_h16<EPI_SCALE_RES, 0, 8, 32, 32, 32, 1, 2, 32, 1, 6, FL_KG2>(a, s);
+                    return run_small_h16<EPI_SCALE_RES, 2, 8, 32, 32, 32, 1, 2, 32, MIMI_SMALL16_32W, 6, FL_KG2>(a, s);
+                return run_small_h16<EPI_SCALE_RES, 0, 8, 32, 32, 32, 1, 2, 32, MIMI_SMALL16_32W, 6, FL_KG2>(a, s);
             case ROLE_DOWNSAMPLE:  // zero-padded here; engine.cpp adds the replicate rows (launch_ds_edge_fix)
-                if (MIMI_SMALL16_32 & 4) return run_small_h16<EPI_NONE, 2, 9, 64, 32, 64, 2, 2, 32, 1>(a, s);
+                if (MIMI_SMALL16_32 & 4) return run_small_h16<EPI_NONE, 2, 9, 64, 32, 64, 2, 2, 32, MIMI_SMALL16_32W>(a, s);
                 return run_small_h16<EPI_NONE, 2, 9, 64, 32, 64, 2, 2, 64, 2>(a, s);
             case ROLE_INPROJ:
-                if (MIMI_SMALL16_32 & 8) return run_small_h16<EPI_NONE, 0, 10, 64, 32, 64, 2, 2, 32, 1>(a, s);
+                if (MIMI_SMALL16_32 & 8) return run_small_h16<EPI_NONE, 0, 10, 64, 32, 64, 2, 2, 32, MIMI_SMALL16_32W>(a, s);
                 return run_small_h16<EPI_NONE, 0, 10, 64, 32, 64, 2, 2, 64, 2>(a, s);
             case ROLE_RES3P: return run_small_h16<EPI_BIAS_ELU, 2, 12, 64, 32, 64, 2, 2, 64, 2, 3>(a, s);
             default: break;

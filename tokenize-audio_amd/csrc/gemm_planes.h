@@ -664,10 +664,13 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
     const __amdgpu_buffer_rsrc_t cp_rs = make_rsrc(SC1 ? (void*)Cpb : nullptr, SC1 ? 0x7fffffffLL : 0);
     constexpr int LPR = CWC / 8;  // lanes per row
     constexpr int RPS = 64 / LPR;  // rows per pass
-    static_assert(RW % RPS == 0, "epilogue: a wave's tile holds whole passes of 64 lanes x 8 columns");
+    // (16 x 16 wave tiles: one pass of 32 lanes, the upper half idle)
+    static_assert(RW % RPS == 0 || RW < RPS, "epilogue: a wave's tile holds whole passes of 64 lanes x 8 columns");
+    constexpr int NPS = RW < RPS ? 1 : RW / RPS;
 #pragma unroll
-    for (int ps = 0; ps < RW / RPS; ++ps) {
+    for (int ps = 0; ps < NPS; ++ps) {
         const int lr = ps * RPS + lane / LPR, lc = (lane % LPR) * 8;
+        if (RW < RPS && lr >= RW) continue;
         f32x4 v0 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc);
         f32x4 v1 = *reinterpret_cast<const f32x4*>(stg + lr * LDE + lc + 4);
         const int row = m0 + wm * RW + lr, col = n0 + wn * CW + jh * CWC + lc;
