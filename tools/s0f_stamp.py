@@ -11,6 +11,8 @@ from mimi_hip.model import MimiHipModel  # noqa: E402
 
 m = MimiHipModel(synthetic.make_state_dict(seed=0, num_quantizers=8), device="cuda:0")
 m.set_graphs(False)
+if len(sys.argv) > 1:
+    m.set_option("stage0_fused", int(sys.argv[1]))
 x = torch.from_numpy(np.stack([synthetic.speech_like(240000, 1, i) for i in range(32)])).cuda()
 for _ in range(2):
     m.encode_int32(x, 8)
