@@ -30,6 +30,10 @@ namespace mimi {
 // the block waves' row writes (ds_write_b64) and the conv waves' fragment reads (ds_read_b128) are conflict-free.
 // LDS: block weights 36 KB + biases + 4 x 9.75 KB slabs + 2 x 40.75 KB y buffers = 157.3 KB.
 // ------------------------------------------------------------------------------------------------
+#ifndef S0F_HELP
+#define S0F_HELP 1  // the conv waves (idle ~2.9k of the 10.7k-cycle round) split the next round's audio window into
+#endif              // planes and copy each section's y halo, off the block waves' chain (0: the block waves do both;
+                    // same bits, stage 0 1.29 / 1.29 / 1.30 -> 1.28 / 1.27 / 1.29 ms alternated, gpurun_out/r6o/ab.log)
 #ifndef S0F_DIAG
 #define S0F_DIAG 0  // tuning diagnostics (results are garbage): 1 = conv waves skip their MFMAs, 2 = block waves skip
 #endif              // their blocks, 3 = block waves without the explicit LDS drains (s_waitcnt lgkmcnt(0))
@@ -44,7 +48,8 @@ constexpr int YLD = 72, YSR = 36, YSS = YSR * YLD + 16, YPS = 4 * YSS, YBS = 2 *
 constexpr int OFF_SLAB = r0h::NFRAG * 1024 + r0h::BIAS * 4;
 constexpr int OFF_Y = OFF_SLAB + NA * r0h::WAVE_BYTES;
 constexpr int OFF_D = OFF_Y + 2 * YBS * 2;
-constexpr int LDS_BYTES = OFF_D + 2 * NA * 16 + 16;
+constexpr int OFF_A2 = OFF_D + 2 * NA * 16 + 16;  // (S0F_HELP) audio plane images [block wave][round parity 2][2][AUD]
+constexpr int LDS_BYTES = OFF_A2 + (S0F_HELP ? NA * 2 * 2 * r0h::AUD * 2 : 0);
 static_assert(OFF_SLAB % 16 == 0 && OFF_Y % 16 == 0 && (YSS * 2) % 16 == 0, "16-B alignment");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 static_assert(NC * 16 == 128, "conv waves x 16 channels = down conv 0's output channels");
@@ -111,6 +116,10 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
     int R = 0;
 #pragma unroll
     for (int w = 0; w < NA; ++w) R = max(R, rcount[w]);
+    // global (not flat) loads: a flat load in flight also holds lgkmcnt, so every LDS drain would wait for HBM
+    const __attribute__((address_space(1))) float* __restrict__ audio =
+        (const __attribute__((address_space(1))) float*)io_pointer(p.audio_ref, p.audio);
+    [[maybe_unused]] _Float16* aud2 = reinterpret_cast<_Float16*>(lds + s0f::OFF_A2);  // (S0F_HELP) [wave][parity][hi | lo]
 
     if (wave >= NA) {
         // ---------------- conv waves: output channels co0 .. co0 + 15 ----------------
@@ -135,8 +144,54 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
         // output tile i: channels co0 + 4 kq + r (acc row) x 6 kHz step 16 i + (lane & 15) of the round = section
         // 2 i + sec_l, step rho of that section (acc column)
         const int sec_l = (lane >> 3) & 1, rho = lane & 7;
+#if S0F_HELP
+        // helper work for block wave hw = (wave - NA) / 2, walking its blocks: the even conv wave splits the audio
+        // window of its next round's block into aud2 (planes as the block wave's conv0 reads them), the odd one
+        // copies the section's y halo (rows 0..3 = rows 32..35 of the previous round's y, zeros at t = 0)
+        const int hw = (wave - NA) >> 1, hrole = (wave - NA) & 1;
+        unsigned hg0, hg1;
+        range(hw, hg0, hg1);
+        TileWalk htw(p, tpi, hg0);
+        const int hhs = (hg0 < hg1 && htw.t0 > 0) ? 1 : 0;
+        htw.t0 -= 32 * hhs;
+        const int hRw = (int)(hg1 - hg0) + hhs;
+        float mxa = 0.0f;
+        auto haload = [&]() {
+            const long long pos = htw.t0 - 8 + lane;
+            const bool ok = lane < AUD && pos >= 0 && pos < htw.Tb;
+            const float v = audio[ok ? (long long)htw.b * T + pos : 0];
+            return ok ? v : 0.0f;
+        };
+        auto hsplit = [&](int n, float av) {  // the block wave's conv0 operand image for its round-n block
+            if (lane < AUD) {
+                mxa = fmaxf(mxa, fabsf(av));
+                unsigned hw_, lw_;
+                split2_f16s(av, 0.0f, p.ascale, hw_, lw_);
+                _Float16* im = aud2 + (hw * 2 + (n & 1)) * (2 * AUD);
+                im[lane] = __builtin_bit_cast(f16x2, hw_)[0];
+                im[AUD + lane] = __builtin_bit_cast(f16x2, lw_)[0];
+            }
+        };
+        const int hrow_ = (lane >> 3) & 3;
+        const int hoff_ = (lane >> 5) * YPS + hw * YSS + hrow_ * YLD + 8 * ((lane & 7) ^ ((hrow_ & 1) * 2));
+        float hnext = 0.0f;
+        if (hrole == 0 && hRw > 0) {
+            hsplit(0, haload());
+            htw.next();
+            if (hRw > 1) hnext = haload();
+        }
+        __syncthreads();  // round 0's audio images
+#endif
         S0F_T0();
         for (int n = 0; n <= R; ++n) {
+#if S0F_HELP
+            if (hrole == 1 && n < hRw) {  // y halo of this round's section hw (the block wave writes rows 4..35)
+                uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                if (htw.t0 > 0) v = *reinterpret_cast<const uint4*>(ybase + ((n + 1) & 1) * YBS + hoff_ + 32 * YLD);
+                *reinterpret_cast<uint4*>(ybase + (n & 1) * YBS + hoff_) = v;
+                htw.next();
+            }
+#endif
             if (n > 0) {
                 const _Float16* yb = ybase + ((n + 1) & 1) * YBS;
                 const int4* dsc = desc + ((n + 1) & 1) * NA;
@@ -175,10 +230,20 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
                 }
                 S0F_T(1);
             }
+#if S0F_HELP
+            if (hrole == 0 && n + 1 < hRw) {  // the next round's audio image (loaded a round ahead)
+                hsplit(n + 1, hnext);
+                htw.next();
+                if (n + 2 < hRw) hnext = haload();
+            }
+#endif
             __syncthreads();
             S0F_T(2);
         }
         S0F_TPRINT("conv");
+#if S0F_HELP
+        amax_commit(p.aamax, mxa);
+#endif
         return;
     }
 
@@ -191,9 +256,6 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
     _Float16* slab = reinterpret_cast<_Float16*>(lds + s0f::OFF_SLAB + wave * WAVE_BYTES);
     _Float16* hb = slab + 2 * SLD;
     float* aud = reinterpret_cast<float*>(slab + 2 * SPL);
-    // global (not flat) loads: a flat load in flight also holds lgkmcnt, so every LDS drain would wait for HBM
-    const __attribute__((address_space(1))) float* __restrict__ audio =
-        (const __attribute__((address_space(1))) float*)io_pointer(p.audio_ref, p.audio);
     unsigned g0, g1;
     range(wave, g0, g1);
     TileWalk tw(p, tpi, g0);
@@ -216,17 +278,10 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
     // stores hi / lo halves; a lane then reads its 8 taps' halves of the plane it feeds (hh) -- 8 d16 LDS reads
     // instead of 8 float reads and 4 pair splits per lane on the block wave's chain (the same values)
     _Float16* audh = reinterpret_cast<_Float16*>(aud);  // [AUD] hi plane, then [AUD] lo plane (the AUD floats' bytes)
-    auto conv0 = [&](float av, f32x16 (&x0)[2]) {
-        if (lane < AUD) {
-            mxa = fmaxf(mxa, fabsf(av));
-            unsigned hw, lw;
-            split2_f16s(av, 0.0f, sa, hw, lw);
-            audh[lane] = __builtin_bit_cast(f16x2, hw)[0];
-            audh[AUD + lane] = __builtin_bit_cast(f16x2, lw)[0];
-        }
-        S0F_DRAIN();
+    // conv0 from an audio plane image (this wave's own, or the one a conv wave split for this round: S0F_HELP)
+    auto conv0_img = [&](const _Float16* img, f32x16 (&x0)[2]) {
         f16x8 bq;
-        const _Float16* ap = audh + (hh ? AUD : 0) + j + 2;
+        const _Float16* ap = img + (hh ? AUD : 0) + j + 2;
 #pragma unroll
         for (int k = 0; k < 8; ++k) bq[k] = ap[k];
 #pragma unroll
@@ -243,6 +298,17 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
                 for (int q = 0; q < 4; ++q) x0[mt][4 * g + q] = __builtin_fmaf(acc[4 * g + q], u0, bb[q]);
             }
         }
+    };
+    auto conv0 = [&](float av, f32x16 (&x0)[2]) {
+        if (lane < AUD) {
+            mxa = fmaxf(mxa, fabsf(av));
+            unsigned hw, lw;
+            split2_f16s(av, 0.0f, sa, hw, lw);
+            audh[lane] = __builtin_bit_cast(f16x2, hw)[0];
+            audh[AUD + lane] = __builtin_bit_cast(f16x2, lw)[0];
+        }
+        S0F_DRAIN();
+        conv0_img(audh, x0);
     };
     auto slab_put = [&](const f32x16 (&x0)[2], int rowoff) {
         const int row = j + rowoff;
@@ -273,7 +339,11 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
             for (int q = 0; q < 4; ++q)
                 *reinterpret_cast<uint4*>(ybase + q * YPS + wave * YSS + 8 * i) = make_uint4(0u, 0u, 0u, 0u);
     }
+#if S0F_HELP
+    __syncthreads();  // round 0's audio images (the conv waves' prologue)
+#else
     float anext = Rw > 0 ? aload(tw.b, tw.t0) : 0.0f;
+#endif
     S0F_T0();
     for (int n = 0; n <= R; ++n) {
         _Float16* ycur = ybase + (n & 1) * YBS;
@@ -286,7 +356,7 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
             const unsigned b = tw.b;
             const long long t0 = tw.t0;
             const long long Tb = tw.Tb;
-            {
+            if (!S0F_HELP) {
                 uint4 v = make_uint4(0u, 0u, 0u, 0u);
                 if (t0 > 0) v = *reinterpret_cast<const uint4*>(yprev + hoff + 32 * YLD);
                 *reinterpret_cast<uint4*>(ycur + hoff) = v;
@@ -304,11 +374,16 @@ __global__ __launch_bounds__(768) void stage0_fused_h16_kernel(ResArgs p) {
                 slab_put(xp, -30);
             }
             S0F_T(0);
+            f32x16 x0[2];
+#if S0F_HELP
+            tw.next();
+            conv0_img(aud2 + (wave * 2 + (n & 1)) * (2 * AUD), x0);
+#else
             const float acur = anext;
             tw.next();
             anext = aload(tw.b, tw.t0);  // (past the range: a valid address, never used)
-            f32x16 x0[2];
             conv0(acur, x0);
+#endif
             S0F_T(1);
             slab_put(x0, 2);
             S0F_DRAIN();
