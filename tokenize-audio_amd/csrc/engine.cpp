@@ -168,11 +168,18 @@ struct DevConv {
     float* b = nullptr;      // [cout] or null
 };
 
+#ifndef MIMI_LN_CHECK_SKIP
+#define MIMI_LN_CHECK_SKIP 1  // (A/B) 0: every LayerNorm output keeps its range-check atomics
+#endif
 struct DevXfmr {
     float *ln1_w, *ln1_b, *wqkv, *wo, *ls1, *ln2_w, *ln2_b, *w1, *w2, *ls2;
     void *wqkv_s, *wo_s, *w1_s, *w2_s;  // bf16 planes
     void *wqkv_h, *wo_h, *w1_h, *w2_h;  // fp16 planes (x scale)
     float wqkv_hs, wo_hs, w1_hs, w2_hs;
+    // max |LayerNorm output| any input can give: max_c |gamma_c| sqrt(D - 1) + |beta_c| (a normalised value is at most
+    // sqrt(D - 1) in magnitude; x 1.001 for rounding).  Below the fp16 plane limit at the tensor's scale, the
+    // output's range check cannot fire and its max |x| atomics are skipped.
+    float ln1_bound = INFINITY, ln2_bound = INFINITY;
 };
 
 struct ProfEvent {
@@ -866,6 +873,18 @@ extern "C" int mimi_finalize(mimi_engine* e) {
             float* hs = sp.d == &x.wo ? &x.wo_hs : sp.d == &x.w1 ? &x.w1_hs : sp.d == &x.w2 ? &x.w2_hs : nullptr;
             if (sd && ((rc = upload_split(e, sd, *t)) || (rc = upload_f16(e, hd, *t, hs)))) return rc;
         }
+        for (int k = 0; k < 2; ++k) {
+            std::vector<float>*g, *bb;
+            const std::string n = k ? "post_attention_layernorm." : "input_layernorm.";
+            if ((rc = get_w(e, p + n + "weight", &g)) || (rc = get_w(e, p + n + "bias", &bb))) return rc;
+            double bound = 0.0;
+            const double r = std::sqrt((double)h - 1.0) * 1.001;
+            for (size_t i = 0; i < g->size() && i < bb->size(); ++i) {
+                const double v = std::fabs((double)(*g)[i]) * r + std::fabs((double)(*bb)[i]);
+                bound = std::isfinite(v) ? std::max(bound, v) : INFINITY;
+            }
+            (k ? x.ln2_bound : x.ln1_bound) = (float)bound;
+        }
     }
     if ((rc = make_conv(e, e->ds, "downsample.conv.", h, h, c.downsample_kernel, c.downsample_stride, false))) return rc;
     if (c.downsample_kernel == 4 && c.downsample_stride == 2) {  // replicate-edge terms of the planes downsample
@@ -1326,6 +1345,11 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         a.amax = e->amax_dev + (size_t)slot * AMAX_SLOT_WORDS;
         return a;
     };
+    // a LayerNorm output whose bound (DevXfmr::ln*_bound) times its scale stays under half the fp16 plane limit
+    // (2^15) needs no range check (calibration still records its maximum: it sets the scale)
+    auto ln_check_free = [&](const Act& a, float bound) {
+        return MIMI_LN_CHECK_SKIP && !e->calibrating && a.amax && a.scale > 0.0f && bound * a.scale < 16384.0f;
+    };
     // fp16 weight planes + 1 / (activation scale x weight scale) for a GEMM reading plane tensor `in`
     auto use_h = [&](GemmArgs& a, const void* wh, float wscale, const Act& in) {
         if (!h16) return;
@@ -1581,7 +1605,8 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
     for (int l = 0; l < c.num_hidden_layers; ++l) {
         const DevXfmr& x = e->xf[l];
         const long long nact = rows * Hd;
-        const Act t1a = new_act(nmf("xf%d.ln1", l));
+        Act t1a = new_act(nmf("xf%d.ln1", l));
+        if (ln_check_free(t1a, x.ln1_bound)) t1a.amax = nullptr;
         // LayerNorm + fc1 (ln_fused >= 1) / q/k/v (ln_fused 2): on small grids one launch whose tiles compute their
         // rows' LayerNorm (the same bits as the LayerNorm kernel's planes, gemm_planes.h FL_LNA)
         auto ln_into = [&](GemmArgs& g, int role, const float* lw, const float* lb, const Act& act) {
@@ -1673,7 +1698,8 @@ static int encode_pass(mimi_engine* e, const float* audio, int B, int64_t L, int
         if (ns) planes_in(ao, w.att, nact);
         use_h(ao, x.wo_h, x.wo_hs, atta);
         ao.sc1 = (e->sc1_out & 4) != 0;
-        const Act t1b = new_act(nmf("xf%d.ln2", l));
+        Act t1b = new_act(nmf("xf%d.ln2", l));
+        if (ln_check_free(t1b, x.ln2_bound)) t1b.amax = nullptr;
         LAUNCH_TRY(launch_gemm(ROLE_OPROJ, ao, s, &kname, prec), "o_proj");
         rec.mark("o_proj", gemm_flops(ao), gemm_bytes(ao, true), kname);
         if ((rc = save_tap(e, nmf("oproj%d", l).c_str(), w.t0, tapB, tapT, Hd, s))) return rc;

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(512) void layernorm_kernel(const float* __restrict_
 #define MIMI_LN_AMAX 1  // 1: one atomic per workgroup (0.182 vs 0.186 ms per wave, same bits); 0: one per wave; 2: none (timing only)
 #endif
 #if MIMI_LN_AMAX == 1
-    {
+    if (yamax) {  // (null: the engine proved the range check cannot fire -- uniform)
         __shared__ float wmx[8];
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));

@@ -9,7 +9,7 @@ R="$(cd "$(dirname "$0")/.." && pwd)"
 C="$R/tokenize-audio_amd/csrc"
 T=$(mktemp -d)
 EXTRA=""
-case "$SRC" in stage0_fused.hip|ops.hip) EXTRA="-fno-slp-vectorize" ;; esac
+case "$SRC" in stage0_fused.hip|ops.hip) EXTRA="-fno-slp-vectorize" ;; engine.cpp) EXTRA="-x hip" ;; esac
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result --offload-arch=gfx950 \
   -Xclang -target-feature -Xclang -packed-fp32-ops $EXTRA $DEFS -c "$C/$SRC" -o "$T/$SRC.o" 2> >(grep -v "not a recognized feature" >&2)
 OBJS=$(ls "$C"/build/*.o | grep -v "/$SRC.o$")
