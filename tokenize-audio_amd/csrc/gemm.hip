@@ -224,6 +224,15 @@ static long long tiles(const GemmArgs& a, int bm, int bn) {
     return (long long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn) * a.batch;
 }
 
+// ring depths of the small-grid down convs (ring depth changes only when bytes land, not the arithmetic).  Batch 1,
+// one box, alternated twice (profiles/r6h1_ab_small_rings.txt): down_s3 6 vs 4 stages 0.050-0.051 vs 0.061 ms (8: 0.051),
+// down_s2 3 vs 2 stages 0.034-0.036 vs 0.040 ms (down_s1 equal; 4: 0.048-0.049, slower); 10.43-10.46k -> 10.48-10.49k
+#ifndef MIMI_DOWN_SMALL_ST
+#define MIMI_DOWN_SMALL_ST 6  // long K (down_s3) at batch 1 (32x32 tiles), 2 pair stages per barrier
+#endif
+#ifndef MIMI_DOWN_SMALL2_ST
+#define MIMI_DOWN_SMALL2_ST 3  // shorter K (down_s1 / s2), 1 pair stage per barrier
+#endif
 template <int EPI, int OUTP, int TAG>
 static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
     // small grids: long K (down_s3, K = 8192) retires 2 pair stages per barrier from a 4-deep ring (batch 1:
@@ -233,11 +242,11 @@ static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
         // batch 1: 64x64 tiles leave 64 workgroups, each at its CU's LDS-DMA ceiling for 8192 / 64 pair stages;
         // 32x32 tiles spread the same stream over 256 CUs
         if (tiles(a, 64, 64) < 256)
-            return run_planes<32, 32, 1, 2, 2, 4, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR | FL_KG2, true>(a, s);
+            return run_planes<32, 32, 1, 2, 2, MIMI_DOWN_SMALL_ST, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR | FL_KG2, true>(a, s);
         return run_planes<64, 64, 2, 2, 2, 4, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR | FL_KG2, true>(a, s);
     }
     if (pair_ok(a) && tiles(a, 256, 128) < kSmallGrid)
-        return run_planes<64, 64, 2, 2, 2, 2, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR, true>(a, s);
+        return run_planes<64, 64, 2, 2, 2, MIMI_DOWN_SMALL2_ST, EPI, OUTP, TAG, 4, 32, 16, FL_PAIR, true>(a, s);
     // fp32-only output (down_s0): the next tile's first stage loads under the epilogue (FL_PF: -2.6 %; with the
     // planes epilogues of down_s1 / s2 it costs +2..3 %, profiles/r2c_ab_pf_pair.log)
     constexpr int PF = OUTP == 0 ? FL_PF : 0;
@@ -253,7 +262,13 @@ static hipError_t run_planes_down_h16(const GemmArgs& a, hipStream_t s) {
 // workgroup streaming its own A and W slices), so more, smaller tiles finish sooner even though they re-read more.
 // Measured per role at B = 1 and B = 4 (profiles/r2d_ab_small_tiles.log): the rule picks the fastest of the three
 // everywhere; B = 1: 7.3k -> 8.0k audio-s/s.
-template <int EPI, int OUTP, int TAG, int BN0, int BM1, int BN1, int WM1, int WN1, int BN2, int WN2, int ST = 4,
+#ifndef MIMI_SMALL_ST
+#define MIMI_SMALL_ST 4  // (A/B knob) ring depth of the small-grid tiles; 6 measured slower at batch 1 (q/k/v 0.109 ->
+#endif                   // 0.137 ms per encode: fewer workgroups per CU fit, profiles/r6h1_ab_small_rings.txt)
+#ifndef MIMI_LNA_ST
+#define MIMI_LNA_ST 4  // (A/B knob) ring depth of the LayerNorm-prologue q/k/v and fc1 tiles
+#endif
+template <int EPI, int OUTP, int TAG, int BN0, int BM1, int BN1, int WM1, int WN1, int BN2, int WN2, int ST = MIMI_SMALL_ST,
           int FL = 0, int BM0 = 64, int WN0 = 2>
 static hipError_t run_small_h16(const GemmArgs& a, hipStream_t s) {
     if (tiles(a, BM0, BN0) >= 256) return run_planes<BM0, BN0, 2, WN0, 2, ST, EPI, OUTP, TAG, 4, 32, 16, FL, true>(a, s);
@@ -276,15 +291,15 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
         if (!gemm_ln_prologue_ok(role, a, prec) || !a.ln_g || !a.ln_b || !(a.ln_scale > 0.0f)) return hipErrorInvalidValue;
         // the tile rule of run_small_h16 (q/k/v never reaches its 64-row tile on a small grid)
         if (role == ROLE_QKV) {
-            if (tiles(a, 32, 128) >= 256) return run_planes<32, 128, 2, 2, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
-            if (a.ln_tile == 1) return run_planes<32, 64, 2, 1, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
-            if (a.ln_tile == 2) return run_planes<16, 128, 1, 2, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
-            return run_planes<16, 64, 1, 1, 2, 4, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
+            if (tiles(a, 32, 128) >= 256) return run_planes<32, 128, 2, 2, 2, MIMI_LNA_ST, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
+            if (a.ln_tile == 1) return run_planes<32, 64, 2, 1, 2, MIMI_LNA_ST, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
+            if (a.ln_tile == 2) return run_planes<16, 128, 1, 2, 2, MIMI_LNA_ST, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
+            return run_planes<16, 64, 1, 1, 2, MIMI_LNA_ST, EPI_ROPE, 0, 5, 4, 32, 16, FL_LNA, true>(a, s);
         }
-        if (tiles(a, 64, 64) >= 256) return run_planes<64, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
+        if (tiles(a, 64, 64) >= 256) return run_planes<64, 64, 2, 2, 2, MIMI_LNA_ST, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
         // (16 x 64 tiles at batch 1 measured slower: fc1 0.142 -> 0.188 ms per encode, gpurun_out/r6f/ab.log)
-        if (tiles(a, 32, 64) >= 256) return run_planes<32, 64, 2, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
-        return run_planes<16, 64, 1, 2, 2, 4, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
+        if (tiles(a, 32, 64) >= 256) return run_planes<32, 64, 2, 2, 2, MIMI_LNA_ST, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
+        return run_planes<16, 64, 1, 2, 2, MIMI_LNA_ST, EPI_GELU, 2, 7, 4, 32, 16, FL_LNA, true>(a, s);
     }
 #ifndef MIMI_SMALL_ROLES
 #define MIMI_SMALL_ROLES 1
