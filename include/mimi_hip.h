@@ -282,6 +282,13 @@ void mimi_bpe_destroy(mimi_bpe* h);
  */
 int mimi_split_check(const float* dev_in, int64_t npairs, float scale, uint32_t* dev_out, void* stream);
 
+/*
+ * Diagnostic: fc1's f16x3 GELU epilogue (the branch-free erfc form, gemm_kernel.h gelu_fast) on n values:
+ * dev_out[i] = GELU(dev_in[i]) (device f32 [n] each).  Replaces torch's GELU(approximate='none') at
+ * TF/modeling_mimi.py:602-615 (MimiMLP fc1 -> activation); tests bound it against float64 and torch.
+ */
+int mimi_gelu_check(const float* dev_in, int64_t n, float* dev_out, void* stream);
+
 /* Device bytes the workspace needs for (batch, length); the engine grows it on demand. */
 int64_t mimi_workspace_bytes(const mimi_engine* e, int32_t batch, int64_t length);
 

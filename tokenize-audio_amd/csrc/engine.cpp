@@ -155,6 +155,13 @@ extern "C" int mimi_split_check(const float* dev_in, int64_t npairs, float scale
     return MIMI_OK;
 }
 
+extern "C" int mimi_gelu_check(const float* dev_in, int64_t n, float* dev_out, void* stream) {
+    if (n < 0 || (n > 0 && (!dev_in || !dev_out))) return set_err(MIMI_ERR_INVALID_ARGUMENT, "mimi_gelu_check: bad arguments");
+    const hipError_t e = launch_gelu_check(dev_in, n, dev_out, (hipStream_t)stream);
+    if (e != hipSuccess) return set_err(MIMI_ERR_HIP, "gelu_check launch: %s", hipGetErrorString(e));
+    return MIMI_OK;
+}
+
 // ------------------------------------------------------------------------------------------------
 // engine
 // ------------------------------------------------------------------------------------------------

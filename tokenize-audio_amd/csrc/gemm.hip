@@ -193,6 +193,19 @@ static hipError_t run_prec(const GemmArgs& a, hipStream_t s, int prec) {
     return run_auto<ELU_IN, PAD, EPI, TAG>(a, s);
 }
 
+// Self-check of fc1's f16x3 GELU (gemm_kernel.h gelu_fast): out[i] = gelu_fast(in[i]).  Diagnostic entry
+// mimi_gelu_check (tests/test_gelu.py compares it with float64 GELU and with torch's)
+__global__ __launch_bounds__(256) void gelu_check_kernel(const float* __restrict__ in, long long n,
+                                                         float* __restrict__ out) {
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) out[i] = gelu_fast(in[i]);
+}
+hipError_t launch_gelu_check(const float* in, long long n, float* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const long long blocks = std::min<long long>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(gelu_check_kernel, dim3((unsigned)blocks), dim3(256), 0, st, in, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_gemm(int role, const GemmArgs& a, hipStream_t s, const char** kname, int precision) {
     if (a.K % 32 != 0 || a.a_cin % 4 != 0 || a.a_rs % 4 != 0 || a.M <= 0 || a.N <= 0 || a.batch <= 0)
         return hipErrorInvalidValue;

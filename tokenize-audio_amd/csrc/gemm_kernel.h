@@ -9,6 +9,28 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float elu1(float x) { return elu_fast(x); }
 
+// GELU(x) = x Phi(x) = x erfc(-x / sqrt 2) / 2 with one branch-free erfc (Numerical Recipes' erfcc Chebyshev fit,
+// fractional error < 1.2e-7 for every argument): erfc(a) = t exp(-a^2 + P(t)), t = 1 / (1 + a / 2), a = |x| / sqrt 2;
+// Phi(-|x|) = erfc(a) / 2 carries full relative precision where GELU's (1 + erf) cancels.  ~19 VALU (one rcp, one
+// exp2) against ~40 for both of OCML erff's branches under divergence.  P's coefficients carry the log2(e) of exp2.
+__device__ __forceinline__ float gelu_fast(float x) {
+    constexpr float L2E = 1.4426950408889634f;
+    const float a = fabsf(x) * 0.70710678118654752440f;
+    const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.5f, a, 1.0f));
+    float p = 0.17087277f * L2E;
+    p = __builtin_fmaf(p, t, -0.82215223f * L2E);
+    p = __builtin_fmaf(p, t, 1.48851587f * L2E);
+    p = __builtin_fmaf(p, t, -1.13520398f * L2E);
+    p = __builtin_fmaf(p, t, 0.27886807f * L2E);
+    p = __builtin_fmaf(p, t, -0.18628806f * L2E);
+    p = __builtin_fmaf(p, t, 0.09678418f * L2E);
+    p = __builtin_fmaf(p, t, 0.37409196f * L2E);
+    p = __builtin_fmaf(p, t, 1.00002368f * L2E);
+    const float y = __builtin_fmaf(t, p, __builtin_fmaf(-a * L2E, a, -1.26551223f * L2E));
+    const float h = 0.5f * (t * __builtin_amdgcn_exp2f(y));  // Phi(-|x|)
+    return x * (x > 0.0f ? 1.0f - h : h);
+}
+
 // torch CPU GELU(approximate='none'): (x * 0.5) * (1 + erf(x * M_SQRT1_2))
 __device__ __forceinline__ float gelu_erf(float x) {
 #ifdef MIMI_GELU_DIAG  // timing diagnostic builds only (results wrong): the epilogue without erf

@@ -629,7 +629,9 @@ __global__ __launch_bounds__((WM * WN + LW) * 64) void gemm_planes_kernel(GemmAr
                     // the fused blocks form it
                     v = F16 ? __builtin_fmaf(acc[i][j][r], us, bias) : v + bias;
                 } else if (EPI == EPI_GELU) {
-                    v = gelu_erf(v);
+                    // f16x3: the branch-free erfc form (fc1 0.583 -> 0.561-0.565 ms per B = 32 step; codes bitwise
+                    // equal on the bench batches, profiles/r6g1_ab_gelu.txt); the bf16 modes keep OCML's erff
+                    v = F16 ? gelu_fast(v) : gelu_erf(v);
                 } else if (EPI == EPI_SCALE_RES) {
                     v = scale * v;  // + R in phase 2
                 } else if (EPI == EPI_ROPE) {

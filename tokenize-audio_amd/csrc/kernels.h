@@ -162,6 +162,7 @@ __device__ __forceinline__ T* io_pointer(T* const* ref, T* direct) {
 }
 // io[0] = audio, io[1] = codes (the pointers of one graph replay)
 hipError_t launch_split_check(const float* in, long long npairs, float s, unsigned* out, hipStream_t st);
+hipError_t launch_gelu_check(const float* in, long long n, float* out, hipStream_t st);
 hipError_t launch_set_io(void** io, const float* audio, int32_t* codes, hipStream_t s, unsigned* hamax = nullptr,
                          unsigned* hflag = nullptr, void* zero = nullptr, size_t zero_bytes = 0);
 

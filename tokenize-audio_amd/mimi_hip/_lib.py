@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "mimi_workspace_bytes", "mimi_destroy", "mimi_last_error", "mimi_set_profiling", "mimi_profile_read",
     "mimi_profile_reset", "mimi_profile_sequence", "mimi_set_taps", "mimi_get_tap", "mimi_resample_poly",
     "mimi_bpe_create", "mimi_bpe_best", "mimi_bpe_merge", "mimi_bpe_destroy", "mimi_flac_info", "mimi_flac_decode",
-    "mimi_split_check",
+    "mimi_split_check", "mimi_gelu_check",
 )
 RESAMPLE_MAX_TAPS = 65536  # MIMI_RESAMPLE_MAX_TAPS
 
@@ -122,6 +122,7 @@ def _declare(lib):
                                      c.POINTER(c.c_int32), c.POINTER(c.c_int64)]),
         "mimi_flac_decode": (c.c_int, [vp, c.c_int64, vp, c.c_int64, c.POINTER(c.c_int64)]),
         "mimi_split_check": (c.c_int, [vp, c.c_int64, c.c_float, vp, vp]),
+        "mimi_gelu_check": (c.c_int, [vp, c.c_int64, vp, vp]),
         "mimi_resample_poly": (c.c_int, [vp, vp, vp, c.c_int32, vp, vp, vp, c.c_int64, vp, c.c_int32, c.c_int32,
                                          c.c_int32, c.c_int64, vp]),
     }
