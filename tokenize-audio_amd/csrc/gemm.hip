@@ -394,7 +394,7 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
             // (256x128 persistent tiles with FL_PF: -8 % in tools/gemm_bench.hip, +5 % in the engine with the GELU
             // planes epilogue -- profiles/r2c_gemm_bench_pf.log, r2c_ab_fc1.log)
             if (prec == PREC_F16X3) {
-#if MIMI_FC1_V == 1
+#if MIMI_FC1_V == 1  // (+6 % again in round 6 with the cheaper GELU epilogue, profiles/r6g3_ab_fc_rings.txt)
                 return run_planes<128, 128, 4, 2, 2, 3, EPI_GELU, 2, 7, 4, 32, 16, FL_PERSIST | FL_PF, true>(a, s);
 #else
                 if (a.sc1) return run_planes<128, 128, 4, 2, 2, 2, EPI_GELU, 2, 7, 0, 32, 16, FL_SC1OUT, true>(a, s);
@@ -403,6 +403,11 @@ static hipError_t dispatch_planes(int role, const GemmArgs& a, hipStream_t s) {
             }
             return run_planes_big<EPI_GELU, 3, 2, 7>(a, s, prec);
         case ROLE_FC2:
+#ifdef MIMI_FC2_ST  // (A/B knob) fc2's ring depth / flags on large grids (K = 2048, one 128 x 128 tile per CU):
+                    // 4 / 5 stages and 4 stages x 2 per barrier measured 2 / 3 / 10 % slower (profiles/r6g3_ab_fc_rings.txt)
+            if (prec == PREC_F16X3 && !a.sc1)
+                return run_planes<128, 128, 4, 2, 2, MIMI_FC2_ST, EPI_SCALE_RES, 0, 8, 4, 32, 16, MIMI_FC2_FL, true>(a, s);
+#endif
             return run_planes_small_ld<EPI_SCALE_RES, 8>(a, s, prec);
         case ROLE_DOWN_XE: return run_planes_big<EPI_BIAS, 3 | 8, 2 | 8, 11>(a, s, prec);
         case ROLE_RES3P:  // fp16: 256x128 on a 3-stage ring fed by 4 loader waves: -8 / -13 % vs 128x128 x 2
