@@ -1996,6 +1996,9 @@ __global__ __launch_bounds__(64 * NWV, (PF <= 4 && FT == 32) ? 4 : 2) void rvq_l
 // workgroup leaves at its next sweep once it sees the flag, and the host, which reads the flag back behind the encode,
 // re-runs the encode without the chain (engine.cpp encode_wait).  So a give-up costs time, never codes.
 constexpr int RVQC_MAX_WG = 128;
+#ifndef MIMI_RVQC_XCD
+#define MIMI_RVQC_XCD 1  // (A/B knob) 1: a group's 8 slice workgroups on one XCD (1-D grid); 0: the 3-D grid
+#endif
 constexpr int RVQC_SPIN = 1 << 20;
 constexpr int RVQC_HDR = 2;  // u64 words in front of the granules: [0] the give-up flag (u32), [1] padding
 constexpr int RVQC_NSTG = 64;  // candidates whose code rows the exact re-score stages in LDS (more: global reads)
@@ -2014,7 +2017,7 @@ __device__ __forceinline__ unsigned long long rvqc_granule(unsigned epoch, unsig
         st_last = now_;                                               \
     } while (0)
 #define RVQC_TPRINT()                                                                                              \
-    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid == 0)                                       \
+    if (ftile == 0 && slice == 0 && chain == 0 && tid == 0)                                                      \
     printf("rvqc levels %d: r2 %llu planes %llu mfma %llu cand %llu exact %llu sweep %llu merge %llu resid %llu\n", \
            Le - Lb, st_acc[0], st_acc[1], st_acc[2], st_acc[3], st_acc[4], st_acc[5], st_acc[6], st_acc[7])
 #else
@@ -2043,21 +2046,35 @@ __global__ __launch_bounds__(512, 2) void rvq_chain_h16_kernel(RvqArgs p, unsign
     __shared__ int codes_l[FT][32];  // this tile's codes per level, stored at the end (slice 0)
     __shared__ float ynl[SLC];       // |e|^2 of the slice's codes at this level
     __shared__ __attribute__((aligned(16))) float rowbuf[RVQC_NSTG * (D + 4)];  // candidates' code rows (exact)
+#if MIMI_RVQC_XCD
+    // a 1-D grid whose 8 slices of one (frame tile, chain) group share an XCD (workgroups are dealt round-robin over
+    // the 8 XCDs): workgroup b runs slice (b >> 3) & 7 of group (b & 7) + 8 (b >> 6), so the winning code rows the
+    // residual update gathers were staged by a peer on the same XCD (its L2), as were the group's projection rows.
+    // Groups past 2 x ftiles (grid padding to whole 64s) leave at once; they join no sweep.
+    const unsigned ftiles = (unsigned)((p.frames + FT - 1) / FT);
+    const unsigned group = (blockIdx.x & 7u) + 8u * (blockIdx.x >> 6);
+    if (group >= 2u * ftiles) return;  // (workgroup-uniform)
+    const int chain = (int)(group / ftiles);
+    const unsigned ftile = group % ftiles;
+    const int slice = (int)((blockIdx.x >> 3) & 7u);
+#else
     const int chain = blockIdx.z;
+    const unsigned ftile = blockIdx.x;
+    const int slice = blockIdx.y;
+    const unsigned ftiles = gridDim.x;
+#endif
     const int Lb = chain ? 0 : p.nsem, Le = chain ? min(p.nsem, p.levels) : p.levels;
     if (Lb >= Le) return;  // (workgroup-uniform)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-    const long long f0 = (long long)blockIdx.x * FT;
-    const int slice = blockIdx.y;
+    const long long f0 = (long long)ftile * FT;
     const int code0 = slice * SLC + wave * CW;
-    const unsigned ftiles = gridDim.x;
     typedef __attribute__((address_space(1))) unsigned gu32;
     gu32* const flag = (gu32*)gbase;  // the launch's give-up flag
     unsigned long long* const gran = gbase + RVQC_HDR;
     const unsigned spin_limit = p.chain_fault == 1 ? 0u : (unsigned)RVQC_SPIN;
     // granules [parity 2][chain 2][frame tile][slice 8][32 frames]
     auto gslot = [&](int par, int sl) {
-        return gran + ((((long long)par * 2 + chain) * ftiles + blockIdx.x) * NSL + sl) * FT;
+        return gran + ((((long long)par * 2 + chain) * ftiles + ftile) * NSL + sl) * FT;
     };
     // the chain's first residual: the projection (as rvq_level_h16_kernel's fresh levels), zero for invalid frames
     const int coff = chain ? 0 : D;
@@ -2293,8 +2310,10 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname, un
         // small grids: every level in one persistent launch (rvq_chain_h16_kernel), unless the form asks otherwise
         const int nchain = (a.levels > a.nsem ? 1 : 0) + (a.nsem > 0 ? 1 : 0);
         // (only for a caller that reads the give-up flag back: chain_flag non-null)
-        if (small && a.chain && chain_flag && form != 1 && ftiles32 * 8 * 2 <= (unsigned)RVQC_MAX_WG && a.nsem <= 1 &&
-            rvq_chain_fits(ftiles32 * 8 * 2)) {
+        // (MIMI_RVQC_XCD: the 1-D grid of 8-slice groups on one XCD each, padded to whole 64s)
+        const unsigned cgrid = MIMI_RVQC_XCD ? 64u * ((2u * ftiles32 + 7u) / 8u) : ftiles32 * 8u * 2u;
+        if (small && a.chain && chain_flag && form != 1 && cgrid <= (unsigned)RVQC_MAX_WG && a.nsem <= 1 &&
+            rvq_chain_fits(cgrid)) {
             const size_t gbytes = (size_t)RVQC_HDR * 8 + (size_t)2 * 2 * ftiles32 * 8 * 32 * 8;
             const size_t pd_off = (size_t)2 * ((a.frames + RVQ_FT - 1) / RVQ_FT * RVQ_FT) * a.D * 4;
             if (gbytes > rvq_work_bytes(a.frames) - pd_off) return hipErrorInvalidValue;
@@ -2311,7 +2330,10 @@ hipError_t launch_rvq(const RvqArgs& args, hipStream_t s, const char** kname, un
             snprintf(knc, sizeof knc, "mimi::rvq_chain_h16_kernel<256, 16>");
             *kname = knc;
             (void)nchain;
-            hipLaunchKernelGGL((rvq_chain_h16_kernel<256, 16>), dim3(ftiles32, 8, 2), dim3(512), 0, s, a, gbase);
+            if (MIMI_RVQC_XCD)
+                hipLaunchKernelGGL((rvq_chain_h16_kernel<256, 16>), dim3(cgrid), dim3(512), 0, s, a, gbase);
+            else
+                hipLaunchKernelGGL((rvq_chain_h16_kernel<256, 16>), dim3(ftiles32, 8, 2), dim3(512), 0, s, a, gbase);
             *chain_flag = reinterpret_cast<unsigned*>(gbase);
             return hipGetLastError();
         }
